@@ -1,0 +1,156 @@
+"""ctypes binding of the MI355X checksum engine's C ABI (include/aws_crt_amd/checksums_batch.h,
+include/aws/checksums/crc.h).  Used by tests/ and bench.py; torch supplies device memory and
+streams only.  Every compute call goes through lib/libaws-crt-cpp-amd.so -- there is no Python
+or CPU fallback: if the library or a gfx950 device is missing, calls raise.
+
+Reference API being mirrored: Aws::Crt::Checksum (include/aws/crt/checksum/CRC.h:20-51,
+XXHash.h:21-37) -> aws-checksums (source/checksum/CRC.cpp:17-42, XXHash.cpp:17-65).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-crt-cpp-amd.so")
+
+CRC32, CRC32C, CRC64NVME, XXH64 = 0, 1, 2, 3
+ALGORITHMS = {"crc32": CRC32, "crc32c": CRC32C, "crc64nvme": CRC64NVME, "xxh64": XXH64}
+WIDE = {CRC64NVME, XXH64}  # 64-bit results
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load the native engine (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(f"native engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
+        L.aws_crt_amd_init.restype = ctypes.c_int
+        L.aws_crt_amd_device_count.restype = ctypes.c_int
+        L.aws_crt_amd_last_error.restype = ctypes.c_char_p
+        L.aws_crt_amd_checksum_strided.argtypes = [ctypes.c_int, vp, sz, sz, sz, vp, vp, vp]
+        L.aws_crt_amd_checksum_list.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp, vp]
+        L.aws_crt_amd_checksum_host.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp]
+        L.aws_crt_amd_crc_combine_batch.argtypes = [ctypes.c_int, vp, vp, ctypes.POINTER(u64), sz, vp, vp]
+        for name, rt, st in (("crc32", u32, u32), ("crc32c", u32, u32), ("crc64nvme", u64, u64)):
+            f = getattr(L, f"aws_checksums_{name}_ex")
+            f.restype, f.argtypes = rt, [vp, sz, st]
+            f = getattr(L, f"aws_checksums_{name}_combine")
+            f.restype, f.argtypes = rt, [st, st, u64]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise EngineError(f"aws_crt_amd error {rc}: {lib().aws_crt_amd_last_error().decode()}")
+
+
+def device_count() -> int:
+    return lib().aws_crt_amd_device_count()
+
+
+def init() -> None:
+    _check(lib().aws_crt_amd_init())
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _out_dtype(alg: int):
+    import torch
+
+    return torch.int64 if alg in WIDE else torch.int32
+
+
+def checksum_strided(alg: int, base, stride: int, length: int, count: int, seeds=None, out=None, stream=None,
+                     base_offset: int = 0):
+    """Batch of `count` device buffers [base + i*stride + base_offset, +length).  `base` is a torch
+    device tensor (or raw address).  Returns the int32/int64 result tensor (reinterpret as unsigned)."""
+    import torch
+
+    addr = (base.data_ptr() if hasattr(base, "data_ptr") else int(base)) + base_offset
+    dev = base.device if hasattr(base, "device") else torch.device("cuda")
+    if out is None:
+        out = torch.empty(count, dtype=_out_dtype(alg), device=dev)
+    sp = seeds.data_ptr() if seeds is not None else None
+    _check(lib().aws_crt_amd_checksum_strided(alg, addr, stride, length, count, sp, out.data_ptr(),
+                                              _stream_handle(stream)))
+    return out
+
+
+def checksum_list(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, out=None, stream=None, device=None):
+    """Ragged batch of device buffers given by raw device addresses and lengths (host lists)."""
+    import torch
+
+    n = len(ptrs)
+    if out is None:
+        out = torch.empty(n, dtype=_out_dtype(alg), device=device or "cuda")
+    P = (ctypes.c_void_p * n)(*ptrs)
+    S = (ctypes.c_size_t * n)(*lens)
+    sp = seeds.data_ptr() if seeds is not None else None
+    _check(lib().aws_crt_amd_checksum_list(alg, P, S, n, sp, out.data_ptr(), _stream_handle(stream)))
+    return out
+
+
+def combine_batch(alg: int, crc1, crc2, len2: Sequence[int], out=None, stream=None):
+    import torch
+
+    n = len(len2)
+    if out is None:
+        out = torch.empty(n, dtype=_out_dtype(alg), device=crc1.device)
+    L2 = (ctypes.c_uint64 * n)(*len2)
+    _check(lib().aws_crt_amd_crc_combine_batch(alg, crc1.data_ptr(), crc2.data_ptr(), L2, n, out.data_ptr(),
+                                               _stream_handle(stream)))
+    return out
+
+
+def checksum_host(alg: int, buffers: Sequence[bytes], seeds: Optional[Sequence[int]] = None):
+    """Host buffers -> host results, through pinned staging and the GPU (synchronous)."""
+    n = len(buffers)
+    keep = [ctypes.create_string_buffer(bytes(b), len(b)) for b in buffers]
+    P = (ctypes.c_void_p * n)(*[ctypes.addressof(k) for k in keep])
+    S = (ctypes.c_size_t * n)(*[len(b) for b in buffers])
+    T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
+    out = (T * n)()
+    sd = (T * n)(*seeds) if seeds is not None else None
+    _check(lib().aws_crt_amd_checksum_host(alg, P, S, n, ctypes.cast(sd, ctypes.c_void_p) if sd else None,
+                                           ctypes.cast(out, ctypes.c_void_p)))
+    return list(out)
+
+
+def crc(alg_name: str, data, previous: int = 0) -> int:
+    """aws_checksums_<alg>_ex on a bytes object (host) or a device tensor (in place)."""
+    L = lib()
+    f = getattr(L, f"aws_checksums_{alg_name}_ex")
+    if hasattr(data, "data_ptr"):
+        return f(data.data_ptr(), data.numel() * data.element_size(), previous)
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    return f(ctypes.addressof(buf), len(data), previous)
+
+
+def combine(alg_name: str, crc1: int, crc2: int, len2: int) -> int:
+    return getattr(lib(), f"aws_checksums_{alg_name}_combine")(crc1, crc2, len2)
+
+
+def as_unsigned(t) -> list:
+    """Result tensor (int32/int64 bit patterns) -> list of python unsigned ints."""
+    bits = 64 if t.dtype.itemsize == 8 else 32
+    mask = (1 << bits) - 1
+    return [int(v) & mask for v in t.cpu().tolist()]

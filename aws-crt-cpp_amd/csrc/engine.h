@@ -1,0 +1,73 @@
+// Internal structures shared by the HIP kernels (crc_kernels.hip) and the host engine (engine.cpp).
+// Not part of the public C ABI (that is include/aws_crt_amd/checksums_batch.h).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace amdcrc {
+
+// Work decomposition (DESIGN.md "Data layout"): every buffer is split into
+//   head  [ptr, H)      H = ptr rounded up to 16      -- bytewise, folded into the first word
+//   main  [H, E)        E = end rounded down to 16    -- the bulk, 16-byte vector loads
+//   tail  [E, end)                                     -- bytewise after the main partial
+// main is front-padded (virtually, with zeros: free for a raw CRC) to T*TILE bytes and cut into T
+// tiles of TILE = 64 lanes * seg bytes.  One wavefront scans one tile; lane l scans the
+// contiguous segment [l*seg, (l+1)*seg) of it.
+constexpr int kWave = 64;
+constexpr int kBlock = 1024;  // 16 waves: one workgroup per CU (the tables take 128 KiB of LDS)
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kGroupBytes = 128;  // bytes per lane per prefetch group (8 x 16-byte loads)
+
+struct ScanParams {
+    // ---- batch description: strided (base != 0) or list (d_ptrs != 0)
+    uint64_t base;                 // strided: device address of buffer 0
+    uint64_t stride;               // strided: bytes between buffer starts
+    uint64_t len;                  // strided: uniform length
+    uint64_t tiles_per_buf;        // strided: T (uniform)
+    const uint64_t *d_ptrs;        // list: device addresses
+    const uint64_t *d_lens;        // list: lengths
+    const uint64_t *d_tile_prefix; // list: exclusive prefix of T_b (nbuf + 1 entries)
+    const uint64_t *d_wave_buf;    // list: buffer index holding each wave's first tile
+    uint64_t nbuf;
+    uint64_t ntiles;
+    // ---- seeds (previous CRC, finalised) and results
+    const void *d_seeds;           // u32/u64 per buffer, or null -> seed_all
+    uint64_t seed_all;
+    void *d_out;                   // u32/u64 per buffer
+    // ---- geometry and constants
+    uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
+    uint32_t nthreads_hint;        // unused (ABI padding)
+    const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
+    const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
+    uint64_t pcols_tmax;
+    // ---- cross-tile combine workspace (zero on entry, left zero on exit)
+    unsigned long long *d_acc;     // per buffer
+    unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
+};
+
+struct XxhParams {
+    const uint64_t *d_ptrs;  // device addresses (list) or null (strided)
+    const uint64_t *d_lens;
+    uint64_t base, stride, len;
+    uint64_t nbuf;
+    const uint64_t *d_seeds;
+    uint64_t seed_all;
+    uint64_t *d_out;
+};
+
+struct CombineParams {
+    const void *d_crc1;
+    const void *d_crc2;
+    const uint64_t *d_len2;
+    uint64_t n;
+    void *d_out;
+    const uint64_t *d_xpow2;  // x^(8 * 2^i) mod P, i < 64
+};
+
+}  // namespace amdcrc
+
+extern "C" {
+int amdcrc_launch_combine(int alg, const amdcrc::CombineParams *p, void *stream);
+int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *stream);
+int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream);
+}

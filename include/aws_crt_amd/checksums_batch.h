@@ -1,0 +1,119 @@
+#pragma once
+/*
+ * MI355X batched checksum engine -- C ABI (the drop-in boundary below Aws::Crt::Checksum).
+ *
+ * Single-buffer entry points with aws-checksums' names and signatures live in
+ * include/aws/checksums/crc.h and include/aws/checksums/xxhash.h.  This header adds the batched,
+ * device-resident entry points that the reference has no counterpart for: the
+ * reference computes one buffer per call on the calling CPU thread
+ * (source/checksum/CRC.cpp:15-43 -> aws_checksums_*_ex).
+ *
+ * Conventions (identical to the reference per buffer):
+ *   CRC32      reflected 0x04C11DB7, init/xorout ~0       (CRC.h:15-20)
+ *   CRC32C     reflected 0x1EDC6F41, init/xorout ~0       (CRC.h:22-27)
+ *   CRC64NVME  reflected 0xAD93D23594C93659, ~0           (CRC.h:29-36)
+ *   XXH64      published xxHash64; raw 64-bit value here  (XXHash.h:21, digest byte order is the
+ *              caller's business: the C++ wrapper writes it big-endian)
+ *   seed       = the finalised CRC of the preceding bytes ("previousCRC", CRC.h:20,27,36), or the
+ *                XXH64 seed.
+ *
+ * All pointers named d_* are device addresses on the current HIP device.  Results are written
+ * to d_out (uint32_t per buffer for CRC32/CRC32C, uint64_t for CRC64NVME/XXH64).  Calls are
+ * asynchronous on `hip_stream` (a hipStream_t; NULL = the legacy default stream).  Inputs must stay
+ * valid until the stream reaches the work.  Every call returns 0 on success or a negative
+ * aws_crt_amd_status; aws_crt_amd_last_error() describes the last failure on the calling thread.
+ * There is no CPU fallback: without a usable gfx950 device every call fails.
+ */
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(AWS_CRT_AMD_BUILD)
+#    define AWS_CRT_AMD_API __attribute__((visibility("default")))
+#else
+#    define AWS_CRT_AMD_API
+#endif
+
+enum aws_crt_amd_algorithm {
+    AWS_CRT_AMD_CRC32 = 0,
+    AWS_CRT_AMD_CRC32C = 1,
+    AWS_CRT_AMD_CRC64NVME = 2,
+    AWS_CRT_AMD_XXH64 = 3,
+};
+
+enum aws_crt_amd_status {
+    AWS_CRT_AMD_OK = 0,
+    AWS_CRT_AMD_ERR_NO_DEVICE = -1,
+    AWS_CRT_AMD_ERR_INVALID_ARG = -2,
+    AWS_CRT_AMD_ERR_HIP = -3,
+    AWS_CRT_AMD_ERR_OOM = -4,
+};
+
+/* Bring up the engine on the current device (idempotent; called implicitly by every entry point). */
+AWS_CRT_AMD_API int aws_crt_amd_init(void);
+/* Number of visible HIP devices (0 when the runtime has none); never initialises a device. */
+AWS_CRT_AMD_API int aws_crt_amd_device_count(void);
+AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void);
+
+/*
+ * Uniform batch: buffer i = [d_base + i*stride, + len), i < count.  stride must be a multiple of
+ * 16 (or count == 1).  d_seeds: device array of count seeds (uint32_t for CRC32/32C, uint64_t
+ * otherwise) or NULL for seed 0.  This is the shape of BASELINE.json configs 2, 4 and 5.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(
+    int algorithm,
+    const void *d_base,
+    size_t stride,
+    size_t len,
+    size_t count,
+    const void *d_seeds,
+    void *d_out,
+    void *hip_stream);
+
+/*
+ * Ragged batch: buffer i = [d_ptrs[i], + lens[i]).  d_ptrs and lens are HOST arrays describing
+ * device buffers (any alignment, any length including 0).  The engine uploads a compact
+ * descriptor (16 B per buffer + tile prefix) per call.  d_seeds as above.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_checksum_list(
+    int algorithm,
+    const void *const *d_ptrs,
+    const size_t *lens,
+    size_t count,
+    const void *d_seeds,
+    void *d_out,
+    void *hip_stream);
+
+/*
+ * Device-side combine of running CRCs (CombineCRC32/32C/64NVME, CRC.h:41-51, over a batch):
+ * d_out[i] = d_crc1[i] * x^(8*len2[i]) ^ d_crc2[i].  len2 is a HOST array.  For S3 multipart
+ * composition of part CRCs into an object CRC.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(
+    int algorithm,
+    const void *d_crc1,
+    const void *d_crc2,
+    const uint64_t *len2,
+    size_t count,
+    void *d_out,
+    void *hip_stream);
+
+/*
+ * Host-memory convenience: checksum `count` host buffers (pageable or pinned), staging them
+ * through pinned memory and the GPU; results written to the HOST array h_out.  Synchronous.
+ * This is the end-to-end (PCIe-inclusive) path DESIGN.md reports separately.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_checksum_host(
+    int algorithm,
+    const void *const *h_ptrs,
+    const size_t *lens,
+    size_t count,
+    const void *h_seeds,
+    void *h_out);
+
+#ifdef __cplusplus
+}
+#endif

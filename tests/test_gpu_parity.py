@@ -1,0 +1,236 @@
+"""GPU parity: the HIP engine (through its C ABI) against the oracle, bit-exact.
+
+Covers the reference's known-answer tests (tests/CRCTest.cpp:16,29,42), the golden fixtures, the
+BASELINE.json configs at full size where the oracle is fast enough (C2: 1024 x 64 KiB) and through
+size-independent properties beyond that (C3: one-shot == chained running CRC == Combine of parts),
+plus the edge cases the API admits: empty and tiny buffers, every alignment mod 16, ragged lengths,
+non-zero previousCRC seeds, lengths not a multiple of the tile, repeated and concurrent launches.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.golden.patterns import pattern
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "vectors.json")))
+ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3}
+W64 = {"crc64nvme", "xxh64"}
+
+
+def dev_random(n, seed):
+    import torch
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (max(n, 1),), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def host_bytes(t, off=0, n=None):
+    a = t.cpu().numpy()
+    return a[off: off + (len(a) - off if n is None else n)]
+
+
+def seeds_tensor(alg, vals):
+    import torch
+
+    if alg in W64:
+        return torch.tensor([v - (1 << 64) if v >= 1 << 63 else v for v in vals], dtype=torch.int64, device="cuda")
+    return torch.tensor([v - (1 << 32) if v >= 1 << 31 else v for v in vals], dtype=torch.int32, device="cuda")
+
+
+def test_reference_kats_single_abi(engine):
+    # tests/CRCTest.cpp:12-42 through the aws_checksums_*_ex ABI, host memory
+    z = bytes(32)
+    assert engine.crc("crc32", z) == 0x190A55AD
+    assert engine.crc("crc32c", z) == 0x8A9136AA
+    assert engine.crc("crc64nvme", z) == 0xCF3473434D4ECF3B
+    for alg, want in GOLDEN["check_123456789"].items():
+        assert engine.crc(alg, b"123456789") == want
+
+
+def test_single_abi_device_pointer(engine):
+    t = dev_random(100003, 1)
+    h = host_bytes(t)
+    for alg in ("crc32", "crc32c", "crc64nvme"):
+        assert engine.crc(alg, t, 77) == oracle.crc(alg, h, 77)
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
+def test_golden_vectors_list(engine, alg):
+    import torch
+
+    vs = [v for v in GOLDEN["vectors"] if v["alg"] == alg]
+    blobs = [pattern(v["pattern"], v["len"]) for v in vs]
+    # pack with varying misalignment so the list path sees every offset mod 16
+    offs, pos = [], 0
+    for i, b in enumerate(blobs):
+        pos += i % 16
+        offs.append(pos)
+        pos += len(b) + 16
+    buf = np.zeros(pos + 16, dtype=np.uint8)
+    for o, b in zip(offs, blobs):
+        buf[o: o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    d = torch.from_numpy(buf).cuda()
+    base = d.data_ptr()
+    out = engine.checksum_list(ALG[alg], [base + o for o in offs], [len(b) for b in blobs],
+                               seeds=seeds_tensor(alg, [v["seed"] for v in vs]))
+    torch.cuda.synchronize()
+    got = engine.as_unsigned(out)
+    for v, g in zip(vs, got):
+        assert g == v["expect"], v
+
+
+@pytest.mark.parametrize("alg", ["crc32c", "crc32", "crc64nvme"])
+def test_config2_full_size(engine, alg):
+    """BASELINE config 2: 1024 x 64 KiB contiguous, device-resident, seed 0."""
+    import torch
+
+    n, L = 1024, 65536
+    d = dev_random(n * L, 2)
+    out = engine.checksum_strided(ALG[alg], d, L, L, n)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    ptrs = [h.ctypes.data + i * L for i in range(n)]
+    want = oracle.batch(alg, ptrs, [L] * n, 8)
+    assert engine.as_unsigned(out) == want
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+@pytest.mark.parametrize("L,off,count", [(8192, 0, 4096), (8192 + 16, 0, 300), (65536 + 48, 0, 200),
+                                         (1000, 0, 257), (4096, 3, 1), (100, 0, 999), (1 << 20, 0, 16),
+                                         ((1 << 20) + 5, 7, 1), (0, 0, 5), (1, 0, 33), (17, 0, 64)])
+def test_strided_shapes_with_seeds(engine, alg, L, off, count):
+    import torch
+
+    stride = (L + 15) // 16 * 16 if count > 1 else L
+    d = dev_random(stride * count + off + 16, 3 + L)
+    rng = random.Random(L * 31 + count)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in range(count)]
+    out = engine.checksum_strided(ALG[alg], d, stride, L, count, seeds=seeds_tensor(alg, seeds), base_offset=off)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[off + i * stride: off + i * stride + L], seeds[i]) for i in range(count)]
+    assert engine.as_unsigned(out) == want
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
+def test_ragged_list_random(engine, alg):
+    import torch
+
+    rng = random.Random(ALG[alg] + 100)
+    lens = [rng.choice([0, 1, 3, 15, 16, 31, 33, 255, 4097, 8192, 30000, 65536, 65557, 200001, 1 << 20])
+            for _ in range(300)]
+    offs, pos = [], 0
+    for ln in lens:
+        pos += rng.randrange(0, 64)
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 5)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.checksum(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert engine.as_unsigned(out) == want
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
+def test_config3_chunked_running_crc(engine, alg):
+    """BASELINE config 3 shape (256 MiB buffers, 8 MiB chunks): one-shot == chained == combine."""
+    import torch
+
+    L, chunk, nbuf = 256 << 20, 8 << 20, 2
+    d = dev_random(L * nbuf, 9)
+    one = engine.as_unsigned(engine.checksum_strided(ALG[alg], d, L, L, nbuf))
+    # chained: chunk c of every buffer seeded on device with chunk c-1's result
+    prev = None
+    parts = []
+    for c in range(L // chunk):
+        prev = engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, seeds=prev, base_offset=c * chunk)
+        parts.append(engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, base_offset=c * chunk))
+    torch.cuda.synchronize()
+    chained = engine.as_unsigned(prev)
+    assert chained == one
+    for b in range(nbuf):
+        acc = engine.as_unsigned(parts[0])[b]
+        for p in parts[1:]:
+            acc = engine.combine(alg, acc, engine.as_unsigned(p)[b], chunk)
+        assert acc == one[b]
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[b * L:(b + 1) * L]) for b in range(nbuf)]
+    assert one == want
+
+
+def test_combine_batch_device(engine):
+    import torch
+
+    rng = random.Random(4)
+    for alg in ("crc32", "crc32c", "crc64nvme"):
+        bits = 64 if alg in W64 else 32
+        n = 1000
+        c1 = [rng.getrandbits(bits) for _ in range(n)]
+        c2 = [rng.getrandbits(bits) for _ in range(n)]
+        l2 = [rng.choice([0, 1, 7, 1 << 20, rng.getrandbits(40)]) for _ in range(n)]
+        out = engine.combine_batch(ALG[alg], seeds_tensor(alg, c1), seeds_tensor(alg, c2), l2)
+        torch.cuda.synchronize()
+        assert engine.as_unsigned(out) == [oracle.combine(alg, a, b, l) for a, b, l in zip(c1, c2, l2)]
+
+
+def test_host_path_chunked(engine):
+    rng = random.Random(8)
+    bufs = [rng.randbytes(n) for n in (0, 1, 5000, (16 << 20) + 77, (40 << 20) + 3)]
+    for alg in ("crc32", "crc32c", "crc64nvme", "xxh64"):
+        seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
+        got = engine.checksum_host(ALG[alg], bufs, seeds)
+        assert got == [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)]
+
+
+def test_repeat_and_concurrent_streams(engine):
+    """multi-tile buffers use per-stream self-cleaning workspaces: repeat + overlap must agree"""
+    import torch
+
+    L, n = (3 << 20) + 16, 12
+    d = dev_random(L * n, 12)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for i in range(6):
+        st = s1 if i % 2 == 0 else s2
+        outs.append(engine.checksum_strided(ALG["crc32c"], d, L, L, n, stream=st))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc("crc32c", h[i * L:(i + 1) * L]) for i in range(n)]
+    for o in outs:
+        assert engine.as_unsigned(o) == want
+
+
+def test_config4_shape_one_shard(engine):
+    """BASELINE config 4 per-GPU shard at reduced count: 8 KiB parts, round-robin shard 0 of 8."""
+    import torch
+
+    total, L, G = 16384, 8192, 8
+    d = dev_random((total // G) * L, 13)
+    out = engine.checksum_strided(ALG["crc32c"], d, L, L, total // G)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = oracle.batch("crc32c", [h.ctypes.data + i * L for i in range(total // G)], [L] * (total // G), 8)
+    assert engine.as_unsigned(out) == want
+
+
+def test_config5_crc64_xxh64_64mib(engine):
+    import torch
+
+    L, n = 64 << 20, 2
+    d = dev_random(L * n, 14)
+    crc = engine.as_unsigned(engine.checksum_strided(ALG["crc64nvme"], d, L, L, n))
+    xx = engine.as_unsigned(engine.checksum_strided(ALG["xxh64"], d, L, L, n))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    assert crc == [oracle.crc("crc64nvme", h[i * L:(i + 1) * L]) for i in range(n)]
+    assert xx == [oracle.xxh64(h[i * L:(i + 1) * L]) for i in range(n)]
