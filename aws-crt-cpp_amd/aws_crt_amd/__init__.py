@@ -30,6 +30,10 @@ def lib() -> ctypes.CDLL:
     """Load the native engine (raises if it was not built)."""
     global _lib
     if _lib is None:
+        # torch ships its own HIP runtime (SONAME libamdhip64.so.7, loaded by the unversioned name).
+        # Load it first so the engine's DT_NEEDED libamdhip64.so.7 binds to that same instance:
+        # one HIP runtime per process, and torch's streams / allocations are valid handles for us.
+        import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise EngineError(f"native engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)

@@ -32,16 +32,8 @@ constexpr uint32_t kTabBytes = 131072;
 constexpr uint32_t kKmatBytes = 8192;  // W=32 only: 64 lanes x 32 columns x 4 B
 constexpr uint32_t kLdsBytes = kTabBytes + kKmatBytes;
 
-// Global-address-space loads (global_load_*, not flat_*: flat loads also count on lgkmcnt and
-// would serialise against the LDS table lookups).
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 gu32x4;
-typedef __attribute__((address_space(1))) const uint8_t gu8;
-__device__ __forceinline__ uint4 gload16(uint64_t a) {
-    const u32x4 v = *(gu32x4 *)a;
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint32_t gbyte(uint64_t a) { return *(gu8 *)a; }
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
 
 __device__ __forceinline__ uint32_t lds32(const char *L, uint32_t a) { return *(const uint32_t *)(L + a); }
 __device__ __forceinline__ uint64_t lds64(const char *L, uint32_t a) { return *(const uint64_t *)(L + a); }
@@ -65,11 +57,12 @@ struct Eng32 {
     const char *L;
     uint32_t srcA, srcB;  // per-lane perm constants: copy<<2 (| 1<<16 for tables 2,3)
 
-    __device__ void init(const char *lds, int lane) {
+    __device__ void init(const char *lds, int lane, const ScanParams &) {
         L = lds;
         srcA = (uint32_t)(lane & 31) << 2;
         srcB = srcA | 0x10000u;
     }
+    uint64_t kl;  // unused (K in LDS)
 
     static __device__ void build(char *L, const ScanParams &p) {
         for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
@@ -84,16 +77,9 @@ struct Eng32 {
                 *(uint4 *)(L + base + m * 16) = vv;
             }
         }
-        if (threadIdx.x < 64) {
-            const uint32_t l = threadIdx.x;
-            uint32_t col = (uint32_t)p.d_kvals[l];
-            uint32_t *km = (uint32_t *)(L + kTabBytes);
-            for (int j = 0; j < 32; ++j) {
-                km[((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
-                col = (uint32_t)gf2_mulx(col, POLY);
-            }
-        }
     }
+    // the host-built K-matrix image (engine.cpp get_kvals) arrives 8 bytes per thread
+    static constexpr bool kKmatInLds = true;
 
     // s <- (s ^ w) * x^32 mod P : four conflict-free lookups
     __device__ __forceinline__ uint32_t word(uint32_t s, uint32_t w) const {
@@ -109,7 +95,7 @@ struct Eng32 {
         return (s >> 8) ^ lds32(L, (e << 8) | srcA);
     }
     // r * x^(8*seg*(63-lane)) : 32 LDS matrix columns
-    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane, const ScanParams &) const {
+    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
         uint32_t acc = 0;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
@@ -131,8 +117,11 @@ struct Eng64 {
     static constexpr int W = 64;
     const char *L;
     uint32_t src0, src1;  // copy<<3 | table<<16
+    uint64_t kl;          // K_l = x^(8*seg*(63-lane))
 
-    __device__ void init(const char *lds, int lane) {
+    static constexpr bool kKmatInLds = false;
+
+    __device__ void init(const char *lds, int lane, const ScanParams &) {
         L = lds;
         src0 = (uint32_t)(lane & 31) << 3;
         src1 = src0 | 0x10000u;
@@ -168,8 +157,8 @@ struct Eng64 {
         const uint32_t e = ((uint32_t)s ^ b) & 0xffu;
         return (s >> 8) ^ lds64(L, (e << 8) | src0);
     }
-    __device__ __forceinline__ uint64_t mulK(uint64_t r, int lane, const ScanParams &p) const {
-        uint64_t b = p.d_kvals[lane], acc = 0;
+    __device__ __forceinline__ uint64_t mulK(uint64_t r, int) const {
+        uint64_t b = kl, acc = 0;
 #pragma unroll 8
         for (int j = 0; j < 64; ++j) {
             acc ^= b & (uint64_t)((int64_t)(r << j) >> 63);
@@ -195,13 +184,14 @@ struct EngFor<ALG_CRC64NVME> {
 };
 
 // ------------------------------------------------------------------------------------------
+// Tile descriptor (wave-uniform, SGPRs).  Built twice per tile: by the prefetch cursor (address
+// fields only) and by the scan cursor (everything); both are pure arithmetic in strided mode.
 struct Tile {
     uint64_t b, k, T;
     uint64_t vbase;  // device address of this tile's virtual offset 0
     uint64_t H;      // first byte of the 16-aligned main region
-    uint64_t tail;   // first tail byte
-    uint64_t s_h;    // head state (tile 0 only): ~seed advanced over the head bytes
-    uint32_t pad;    // virtual zero bytes in front of main (k == 0 only)
+    uint64_t ptr, headend, tail;
+    uint32_t pad;  // virtual zero bytes in front of main (k == 0 only)
     uint32_t ngroups;
     uint32_t tail_len;
 };
@@ -210,33 +200,28 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint32_t rfl32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Tile fields are wave-uniform: keep them in SGPRs.
-__device__ __forceinline__ Tile uniform(Tile d) {
-    d.b = rfl64(d.b);
-    d.k = rfl64(d.k);
-    d.T = rfl64(d.T);
-    d.vbase = rfl64(d.vbase);
-    d.H = rfl64(d.H);
-    d.tail = rfl64(d.tail);
-    d.s_h = rfl64(d.s_h);
-    d.pad = rfl32(d.pad);
-    d.ngroups = rfl32(d.ngroups);
-    d.tail_len = rfl32(d.tail_len);
-    return d;
+// Scalar (SMEM) loads of wave-uniform descriptor words: they retire on lgkmcnt, so waiting for them
+// never drains the vector-memory queue holding the prefetched payload groups.
+__device__ __forceinline__ uint64_t sload64(const void *a) {
+    uint64_t v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint32_t sload32(const void *a) {
+    uint32_t v;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+    return v;
 }
 
 struct Walker {  // list mode: running position in the tile prefix
     uint64_t b, lo, hi;
 };
 
-template <class E>
-__device__ Tile make_tile(const ScanParams &p, uint64_t t, Walker &wk, const E &eng) {
-    using T = typename E::T;
+__device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walker &wk) {
     Tile d;
     uint64_t ptr, n;
-    if (p.base) {
+    if (!p.list_mode) {
         d.T = p.tiles_per_buf;
         d.b = t / d.T;
         d.k = t - d.b * d.T;
@@ -246,142 +231,234 @@ __device__ Tile make_tile(const ScanParams &p, uint64_t t, Walker &wk, const E &
         while (t >= wk.hi) {
             ++wk.b;
             wk.lo = wk.hi;
-            wk.hi = p.d_tile_prefix[wk.b + 1];
+            wk.hi = sload64(p.d_tile_prefix + wk.b + 1);
         }
         d.b = wk.b;
         d.k = t - wk.lo;
         d.T = wk.hi - wk.lo;
-        ptr = p.d_ptrs[d.b];
-        n = p.d_lens[d.b];
+        ptr = sload64(p.d_ptrs + d.b);
+        n = sload64(p.d_lens + d.b);
     }
     const uint64_t end = ptr + n;
     const uint64_t H = (ptr + 15) & ~15ull;
     const uint64_t Ea = end & ~15ull;
     const uint64_t tile_bytes = (uint64_t)p.seg * kWave;
-    uint64_t mainlen, headend;
+    uint64_t mainlen;
     if (Ea > H) {
         mainlen = Ea - H;
-        headend = H;
+        d.headend = H;
         d.tail = Ea;
         d.tail_len = (uint32_t)(end - Ea);
     } else {
         mainlen = 0;
-        headend = end;
+        d.headend = end;
         d.tail = end;
         d.tail_len = 0;
     }
     const uint64_t pad = d.T * tile_bytes - mainlen;
+    d.ptr = ptr;
     d.pad = d.k == 0 ? (uint32_t)pad : 0u;
     d.H = H;
     d.vbase = H - pad + d.k * tile_bytes;
     d.ngroups = mainlen ? p.seg / kGroupBytes : 0u;
-    d.s_h = 0;
-    if (d.k == 0) {
-        uint64_t seed = p.seed_all;
-        if (p.d_seeds) seed = E::W == 32 ? (uint64_t)((const uint32_t *)p.d_seeds)[d.b] : ((const uint64_t *)p.d_seeds)[d.b];
-        T s = (T)~seed;
-        for (uint64_t a = ptr; a < headend; ++a) s = eng.byte(s, gbyte(a));
-        d.s_h = (uint64_t)s;
-    }
     return d;
 }
 
-__device__ __forceinline__ void load_group(uint4 (&v)[8], const Tile &d, uint32_t g, uint32_t seg, int lane, bool masked) {
+// Payload groups are plain global loads (address space 1) into registers.  Everything else the
+// loop reads -- descriptors, seeds, head/tail bytes, the P columns -- is a scalar (SMEM) load that
+// retires on lgkmcnt, so the compiler's vmcnt accounting sees only the ring loads (and the combine
+// atomic) and can keep two groups in flight across tile boundaries.
+struct Group {
+    v4u v[kVecPerGroup];
+};
+typedef __attribute__((address_space(1))) const v4u gv4u;
+
+__device__ __forceinline__ void issue_group(Group &g, uint64_t a) {
+#pragma unroll
+    for (int i = 0; i < kVecPerGroup; ++i) g.v[i] = ((gv4u *)a)[i];
+}
+__device__ __forceinline__ void issue_group4(Group &g, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3) {
+    g.v[0] = *(gv4u *)a0;
+    g.v[1] = *(gv4u *)a1;
+    g.v[2] = *(gv4u *)a2;
+    g.v[3] = *(gv4u *)a3;
+}
+template <int N>
+__device__ __forceinline__ void wait_group(Group &) {}
+
+__device__ __forceinline__ void load_group(Group &grp, const Tile &d, uint32_t g, uint32_t seg, int lane) {
     const uint32_t vo0 = (uint32_t)lane * seg + g * kGroupBytes;
-    if (!masked) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = gload16(d.vbase + vo0 + 16u * i);
+    if (d.pad == 0) {
+        issue_group(grp, d.vbase + vo0);
     } else {
+        // virtual zero bytes [0, pad): read a valid address (the main start) and zero in proc_group
+        uint64_t a[kVecPerGroup];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < kVecPerGroup; ++i) {
             const uint32_t vo = vo0 + 16u * i;
-            const bool ok = vo >= d.pad;
-            const uint4 x = gload16(ok ? d.vbase + vo : d.H);
-            v[i] = ok ? x : make_uint4(0, 0, 0, 0);
+            a[i] = vo >= d.pad ? d.vbase + vo : d.H;
         }
+        issue_group4(grp, a[0], a[1], a[2], a[3]);
     }
 }
 
 template <class E>
-__device__ __forceinline__ typename E::T proc_group(typename E::T s, const uint4 (&v)[8], const E &eng, const Tile &d,
-                                                   uint32_t g, uint32_t seg, int lane, bool masked) {
-    using T = typename E::T;
-    if (!masked) {
+__device__ __forceinline__ typename E::T proc_group(typename E::T s, const Group &grp, const E &eng, const Tile &d,
+                                                   uint32_t g, uint32_t seg, int lane, typename E::T s_h) {
+    if (d.pad == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            s = eng.word(s, v[i].x);
-            s = eng.word(s, v[i].y);
-            s = eng.word(s, v[i].z);
-            s = eng.word(s, v[i].w);
+        for (int i = 0; i < kVecPerGroup; ++i) {
+            s = eng.word(s, grp.v[i].x);
+            s = eng.word(s, grp.v[i].y);
+            s = eng.word(s, grp.v[i].z);
+            s = eng.word(s, grp.v[i].w);
         }
     } else {
         const uint32_t vo0 = (uint32_t)lane * seg + g * kGroupBytes;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (vo0 + 16u * i == d.pad) s ^= (T)d.s_h;  // lane state is 0 here: inject the head state
-            s = eng.word(s, v[i].x);
-            s = eng.word(s, v[i].y);
-            s = eng.word(s, v[i].z);
-            s = eng.word(s, v[i].w);
+        for (int i = 0; i < kVecPerGroup; ++i) {
+            const uint32_t vo = vo0 + 16u * i;
+            const uint32_t keep = vo >= d.pad ? ~0u : 0u;
+            if (vo == d.pad) s ^= s_h;  // lane state is 0 here: inject the head state
+            s = eng.word(s, grp.v[i].x & keep);
+            s = eng.word(s, grp.v[i].y & keep);
+            s = eng.word(s, grp.v[i].z & keep);
+            s = eng.word(s, grp.v[i].w & keep);
         }
     }
     return s;
 }
 
+// bytes [a, end) folded into state s (a < end, both inside 16-aligned blocks read by SMEM)
 template <class E>
-__device__ void finish_tile(const ScanParams &p, const Tile &d, typename E::T s, const E &eng, int lane) {
+__device__ __forceinline__ typename E::T fold_bytes(typename E::T s, uint64_t a, uint64_t end, const E &eng) {
+    for (uint64_t blk = a & ~15ull; blk < end; blk += 16) {
+        v4u w;
+        asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(blk) : "memory");
+        const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+        const uint64_t lo = a > blk ? a : blk, hi = end < blk + 16 ? end : blk + 16;
+        for (uint64_t x = lo; x < hi; ++x) {
+            const uint32_t o = (uint32_t)(x - blk);
+            const uint32_t word = o < 4 ? wv[0] : o < 8 ? wv[1] : o < 12 ? wv[2] : wv[3];
+            s = eng.byte(s, (word >> (8 * (o & 3))) & 0xffu);
+        }
+    }
+    return s;
+}
+
+// head state of a buffer: ~seed advanced over the unaligned head bytes [ptr, headend)
+template <class E>
+__device__ __forceinline__ typename E::T head_state(const ScanParams &p, const Tile &d, const E &eng) {
+    using T = typename E::T;
+    uint64_t seed = p.seed_all;
+    if (p.d_seeds)
+        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)p.d_seeds + d.b) : sload64((const uint64_t *)p.d_seeds + d.b);
+    T s = (T)~seed;
+    if (d.headend > d.ptr) s = fold_bytes(s, d.ptr, d.headend, eng);
+    return s;
+}
+
+// r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time
+template <class T, int W>
+__device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
+    T acc = 0;
+#pragma unroll
+    for (int c = 0; c < W; c += 8) {
+        uint64_t k0, k1, k2, k3, k4, k5, k6, k7;
+        asm volatile(
+            "s_load_dwordx2 %0, %8, 0x0\n\ts_load_dwordx2 %1, %8, 0x8\n\t"
+            "s_load_dwordx2 %2, %8, 0x10\n\ts_load_dwordx2 %3, %8, 0x18\n\t"
+            "s_load_dwordx2 %4, %8, 0x20\n\ts_load_dwordx2 %5, %8, 0x28\n\t"
+            "s_load_dwordx2 %6, %8, 0x30\n\ts_load_dwordx2 %7, %8, 0x38\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=s"(k0), "=s"(k1), "=s"(k2), "=s"(k3), "=s"(k4), "=s"(k5), "=s"(k6), "=s"(k7)
+            : "s"(cols + c)
+            : "memory");
+        const uint64_t k[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if ((r >> (W - 1 - (c + j))) & 1) acc ^= (T)k[j];
+    }
+    return acc;
+}
+
+// A tile's contribution to the per-buffer accumulator is published with one device-scope atomic;
+// its returned value (who arrived last) is examined at the next tile boundary, by which time at
+// least one more payload group (4 loads) has been issued behind it: vmcnt(4) then covers it.
+struct Pending {
+    bool valid;
+    unsigned long long val, old;
+    uint64_t b, T_, tail;
+    uint32_t tail_len;
+};
+
+__device__ __forceinline__ unsigned long long atomic_xor_ret(unsigned long long *a, unsigned long long v) {
+    return __hip_atomic_fetch_xor(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <class E>
+__device__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, uint64_t tail, uint32_t tail_len, const E &eng) {
+    if (tail_len) fin = fold_bytes(fin, tail, tail + tail_len, eng);
+    fin = ~fin;
+    if (E::W == 32)
+        ((uint32_t *)p.d_out)[b] = (uint32_t)fin;
+    else
+        ((uint64_t *)p.d_out)[b] = (uint64_t)fin;
+}
+
+template <class E>
+__device__ void resolve(const ScanParams &p, Pending &pd, const E &eng, int lane) {
+    using T = typename E::T;
+    if (!pd.valid) return;
+    pd.valid = false;
+    const unsigned long long old = rfl64(pd.old);  // lane 0 issued the atomic
+    const unsigned long long now = old ^ pd.val;
+    const unsigned long long full = pd.T_ == 32 ? 0xFFFFFFFF00000000ull : (((1ull << pd.T_) - 1) << 32);
+    if ((now & 0xFFFFFFFF00000000ull) == full) {
+        if (lane == 0) __hip_atomic_exchange(&p.d_acc[pd.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const T fin = (T)(uint32_t)now;
+        if (lane == 0) finalize(p, pd.b, fin, pd.tail, pd.tail_len, eng);
+    }
+}
+
+template <class E>
+__device__ void finish_tile(const ScanParams &p, const Tile &d, typename E::T s, typename E::T s_h, const E &eng,
+                            int lane, Pending &pd) {
     using T = typename E::T;
     constexpr int W = E::W;
     T r = 0;
-    if (d.ngroups) r = wave_xor(eng.mulK(s, lane, p));
-    bool last;
-    T fin;
+    if (d.ngroups) r = wave_xor(eng.mulK(s, lane));
     if (d.T == 1) {
-        last = true;
-        fin = d.ngroups ? r : (T)d.s_h;
-    } else {
-        const uint64_t kk = d.T - 1 - d.k;
-        T v = 0;
-        if (lane < W) {
-            const T col = (T)p.d_pcols[kk * W + lane];
-            v = ((r >> (W - 1 - lane)) & 1) ? col : (T)0;
-        }
-        v = wave_xor(v);
-        last = false;
-        fin = 0;
-        if (lane == 0) {
-            if (W == 32 && d.T <= 32) {
-                const unsigned long long bit = 1ull << (32 + d.k);
-                const unsigned long long val = (unsigned long long)(uint32_t)v | bit;
-                const unsigned long long old =
-                    __hip_atomic_fetch_xor(&p.d_acc[d.b], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long now = old ^ val;
-                const unsigned long long full = d.T == 32 ? 0xFFFFFFFF00000000ull : (((1ull << d.T) - 1) << 32);
-                if ((now & 0xFFFFFFFF00000000ull) == full) {
-                    last = true;
-                    fin = (T)(uint32_t)now;
-                    __hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else {
-                const unsigned long long old =
-                    __hip_atomic_fetch_xor(&p.d_acc[d.b], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");  // XOR performed before we count
-                const unsigned int c = __hip_atomic_fetch_add(&p.d_cnt[d.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (c == d.T - 1) {
-                    last = true;
-                    fin = (T)__hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&p.d_cnt[d.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-        }
+        const T fin = d.ngroups ? r : s_h;
+        if (lane == 0) finalize(p, d.b, fin, d.tail, d.tail_len, eng);
+        return;
     }
-    if (lane == 0 && last) {
-        for (uint32_t i = 0; i < d.tail_len; ++i) fin = eng.byte(fin, gbyte(d.tail + i));
-        fin = ~fin;
-        if (W == 32)
-            ((uint32_t *)p.d_out)[d.b] = (uint32_t)fin;
-        else
-            ((uint64_t *)p.d_out)[d.b] = (uint64_t)fin;
+    // move the (wave-uniform) tile partial to the buffer end: r * x^(8*TILE*(T-1-k))
+    const T v = mul_pcols<T, W>((T)rfl64((uint64_t)r), p.d_pcols + (d.T - 1 - d.k) * W);
+    resolve(p, pd, eng, lane);
+    if (W == 32 && d.T <= 32) {
+        // one 64-bit word per buffer: {arrival bit of each tile | XOR of the tile partials}
+        const unsigned long long val = (unsigned long long)(uint32_t)v | (1ull << (32 + d.k));
+        unsigned long long old = 0;
+        if (lane == 0) old = atomic_xor_ret(&p.d_acc[d.b], val);
+        pd.valid = true;
+        pd.val = val;
+        pd.old = old;
+        pd.b = d.b;
+        pd.T_ = d.T;
+        pd.tail = d.tail;
+        pd.tail_len = d.tail_len;
+    } else if (lane == 0) {
+        // wide state or more than 32 tiles: XOR, wait for it to be performed, then count arrivals
+        const unsigned long long old =
+            __hip_atomic_fetch_xor(&p.d_acc[d.b], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
+        const unsigned int c = __hip_atomic_fetch_add(&p.d_cnt[d.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == d.T - 1) {
+            const T fin = (T)__hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&p.d_cnt[d.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            finalize(p, d.b, fin, d.tail, d.tail_len, eng);
+        }
     }
 }
 
@@ -390,52 +467,122 @@ __global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p)
     using E = typename EngFor<ALG>::E;
     using T = typename E::T;
     __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-    E::build(lds, p);
-    __syncthreads();
 
     const int lane = threadIdx.x & 63;
-    E eng;
-    eng.init(lds, lane);
     const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t gw = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
-    if (t0 >= t1) return;
-
-    Walker wk{0, 0, 0};
-    if (!p.base) {
-        wk.b = p.d_wave_buf[gw];
-        wk.lo = p.d_tile_prefix[wk.b];
-        wk.hi = p.d_tile_prefix[wk.b + 1];
-    }
     const uint32_t seg = p.seg;
-    for (uint64_t t = t0; t < t1; ++t) {
-        const Tile d = uniform(make_tile(p, t, wk, eng));
-        const uint32_t ng = d.ngroups;
-        T s;
-        if (d.pad == 0) {
-            // fast path: every vector is real; one prefetch group in flight while the other is scanned
-            s = (d.k == 0 && lane == 0) ? (T)d.s_h : (T)0;
-            uint4 A[8], B[8];
-            if (ng) load_group(A, d, 0, seg, lane, false);
-            for (uint32_t g = 0; g < ng; g += 2) {
-                if (g + 1 < ng) load_group(B, d, g + 1, seg, lane, false);
-                s = proc_group(s, A, eng, d, g, seg, lane, false);
-                if (g + 1 >= ng) break;
-                if (g + 2 < ng) load_group(A, d, g + 2, seg, lane, false);
-                s = proc_group(s, B, eng, d, g + 1, seg, lane, false);
-            }
-        } else {
-            // first tile of a buffer whose main region is not a multiple of TILE: the leading
-            // `pad` virtual bytes are zeros and the head state is injected at offset `pad`
-            s = 0;
-            for (uint32_t g = 0; g < ng; ++g) {
-                uint4 A[8];
-                load_group(A, d, g, seg, lane, true);
-                s = proc_group(s, A, eng, d, g, seg, lane, true);
+
+    Walker w0{0, 0, 0};
+    if (p.list_mode && t0 < t1) {
+        w0.b = sload64(p.d_wave_buf + gw);
+        w0.lo = sload64(p.d_tile_prefix + w0.b);
+        w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
+    }
+    // ---- prefetch cursor: the next (tile, group) to load; parks on the last group when exhausted
+    Walker wf = w0;
+    uint64_t tf = t0;
+    uint32_t gf = 0;
+    Tile df{};
+    bool any = false;
+    for (; tf < t1; ++tf) {
+        df = make_tile(p, tf, wf);
+        if (df.ngroups) {
+            any = true;
+            break;
+        }
+    }
+    bool pf_done = !any;
+    auto pf_advance = [&]() {
+        if (gf + 1 < df.ngroups) {
+            ++gf;
+            return;
+        }
+        if (pf_done) return;
+        Walker w2 = wf;
+        for (uint64_t t = tf + 1; t < t1; ++t) {
+            Tile d2 = make_tile(p, t, w2);
+            if (d2.ngroups) {
+                df = d2;
+                wf = w2;
+                tf = t;
+                gf = 0;
+                return;
             }
         }
-        finish_tile(p, d, s, eng, lane);
+        pf_done = true;
+    };
+    // K data first (W=32: 8 bytes of the LDS K-matrix image per thread; W=64: this lane's K_l),
+    // then the first two payload groups, all before the LDS table build so their latency overlaps it
+    const uint64_t kq = *(const __attribute__((address_space(1))) uint64_t *)(E::kKmatInLds ? p.d_kvals + threadIdx.x
+                                                                                        : p.d_kvals + lane);
+    Group r0, r1, r2;
+    if (any) {
+        load_group(r0, df, gf, seg, lane);
+        pf_advance();
+        load_group(r1, df, gf, seg, lane);
+        pf_advance();
     }
+
+    E::build(lds, p);
+    if (E::kKmatInLds) *(uint64_t *)(lds + kTabBytes + 8 * threadIdx.x) = kq;
+    // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched groups
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    E eng;
+    eng.init(lds, lane, p);
+    eng.kl = kq;
+    if (t0 >= t1) return;
+
+    // ---- scan cursor
+    Walker wp = w0;
+    uint64_t tp = t0;
+    uint32_t gp = 0;
+    Tile dp = make_tile(p, tp, wp);
+    T s_h = dp.k == 0 ? head_state(p, dp, eng) : (T)0;
+    T s = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : (T)0;
+    Pending pd{};
+    pd.valid = false;
+
+    // finish tiles whose groups are all scanned (and empty tiles); false once the wave is done
+    auto settle = [&]() -> bool {
+        while (gp >= dp.ngroups) {
+            finish_tile(p, dp, s, s_h, eng, lane, pd);
+            if (++tp >= t1) return false;
+            dp = make_tile(p, tp, wp);
+            gp = 0;
+            s_h = dp.k == 0 ? head_state(p, dp, eng) : (T)0;
+            s = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : (T)0;
+        }
+        return true;
+    };
+
+    if (any) {
+        // three-slot ring, prefetch distance two groups; each step issues 4 loads, then waits
+        // for the oldest group with 8 younger loads allowed in flight
+        for (;;) {
+            load_group(r2, df, gf, seg, lane);
+            pf_advance();
+            if (!settle()) break;
+            wait_group<8>(r0);
+            s = proc_group(s, r0, eng, dp, gp++, seg, lane, s_h);
+
+            load_group(r0, df, gf, seg, lane);
+            pf_advance();
+            if (!settle()) break;
+            wait_group<8>(r1);
+            s = proc_group(s, r1, eng, dp, gp++, seg, lane, s_h);
+
+            load_group(r1, df, gf, seg, lane);
+            pf_advance();
+            if (!settle()) break;
+            wait_group<8>(r2);
+            s = proc_group(s, r2, eng, dp, gp++, seg, lane, s_h);
+        }
+    } else {
+        settle();
+    }
+    resolve(p, pd, eng, lane);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -121,15 +121,29 @@ int upload(DevBuf &b, const void *host, size_t bytes) {
     return 0;
 }
 
-// K_l = x^(8*seg*(63-l)) : moves lane l's partial to the end of its tile
+// K_l = x^(8*seg*(63-l)) moves lane l's partial to the end of its tile.
+//   W=64: the 64 values K_l.
+//   W=32: the kernel's LDS image of the 32 matrix columns K_l * x^j, laid out [j/4][lane][j%4] as
+//         u32 so one ds_read_b128 fetches four columns conflict-free (8 KiB = 1024 threads x 8 B).
 int get_kvals(Device *d, int alg, uint32_t seg, const uint64_t **out) {
     auto key = std::make_pair(alg, seg);
     auto it = d->kvals.find(key);
     if (it == d->kvals.end()) {
         const uint64_t poly = alg_poly(alg);
         const int w = width_of(alg);
-        std::vector<uint64_t> k(64);
-        for (int l = 0; l < 64; ++l) k[l] = gf2_xpow8n((uint64_t)seg * (63 - l), poly, w);
+        std::vector<uint64_t> k(w == 64 ? 64 : kBlock, 0);
+        if (w == 64) {
+            for (int l = 0; l < 64; ++l) k[l] = gf2_xpow8n((uint64_t)seg * (63 - l), poly, w);
+        } else {
+            uint32_t *img = (uint32_t *)k.data();
+            for (int l = 0; l < 64; ++l) {
+                uint64_t col = gf2_xpow8n((uint64_t)seg * (63 - l), poly, w);
+                for (int j = 0; j < 32; ++j) {
+                    img[((j >> 2) * 64 + l) * 4 + (j & 3)] = (uint32_t)col;
+                    col = gf2_mulx(col, poly);
+                }
+            }
+        }
         DevBuf b;
         int rc = upload(b, k.data(), k.size() * 8);
         if (rc) return rc;
@@ -372,6 +386,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     }
     ScanParams p{};
     p.seg = seg;
+    p.list_mode = 1;
     p.d_ptrs = dd;
     p.d_lens = dd + count;
     p.d_tile_prefix = dd + 2 * count;

@@ -16,7 +16,8 @@ namespace amdcrc {
 constexpr int kWave = 64;
 constexpr int kBlock = 1024;  // 16 waves: one workgroup per CU (the tables take 128 KiB of LDS)
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kGroupBytes = 128;  // bytes per lane per prefetch group (8 x 16-byte loads)
+constexpr int kGroupBytes = 64;  // bytes per lane per prefetch group (4 x 16-byte loads)
+constexpr int kVecPerGroup = kGroupBytes / 16;
 
 struct ScanParams {
     // ---- batch description: strided (base != 0) or list (d_ptrs != 0)
@@ -36,7 +37,7 @@ struct ScanParams {
     void *d_out;                   // u32/u64 per buffer
     // ---- geometry and constants
     uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
-    uint32_t nthreads_hint;        // unused (ABI padding)
+    uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;

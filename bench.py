@@ -10,6 +10,12 @@ Each rank scans its own batches (buffers shard across GPUs with no collective: w
 Steps rotate over --batches distinct batches (default 8 = 512 MiB per GPU, twice the 256 MiB
 Infinity Cache) so every launch streams from HBM, not from the on-die cache.
 
+Timed region: the K launches are replayed from a captured HIP graph (one launch per batch, the
+batches split over --branches independent graph branches so consecutive launches overlap their
+ramp-up and tail); any K % batches remainder is launched eagerly.  Kernel duration for the
+roofline: a separate pass queues --timing-launches eager launches bracketed by HIP events behind a
+GPU-side hold (so host launch latency never sits between an event pair).
+
 Prints one JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per launch (1 byte read per
 payload byte) / mean kernel duration from HIP events recorded on the launch stream.
 `cpu_baseline` = the oracle's SSE4.2 crc32q 3-way path (the technique class of aws-checksums)
@@ -39,7 +45,9 @@ def parse():
     ap.add_argument("--buffers", type=int, default=1024)
     ap.add_argument("--buffer-bytes", type=int, default=65536)
     ap.add_argument("--batches", type=int, default=8)
-    ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--branches", type=int, default=2)
+    ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--timing-launches", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -101,30 +109,45 @@ def main():
     data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
     wide = alg in ("crc64nvme", "xxh64")
     outs = [torch.empty(count, dtype=torch.int64 if wide else torch.int32, device=dev) for _ in range(nb)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.streams))]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.branches))]
 
-    def launch(i):
+    def launch(i, st=None):
         b = i % nb
-        st = streams[i % len(streams)]
+        st = st or streams[i % len(streams)]
         eng.checksum_strided(ALG[alg], data, L, L, count, out=outs[b], stream=st, base_offset=b * step_bytes)
-        return st
 
     torch.cuda.synchronize()
-    for i in range(args.warmup):
+    for i in range(max(args.warmup, 2 * nb)):  # every (batch, stream) pair once: caches + workspaces
         launch(i)
     torch.cuda.synchronize()
+
+    graph = None
+    if args.mode == "graph":
+        graph = torch.cuda.CUDAGraph()
+        cap = streams[0]
+        with torch.cuda.graph(graph, stream=cap):
+            for st in streams[1:]:
+                st.wait_stream(cap)
+            for i in range(nb):
+                launch(i, streams[i % len(streams)])
+            for st in streams[1:]:
+                cap.wait_stream(st)
+        for _ in range(2):
+            graph.replay()
+        torch.cuda.synchronize()
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        st = streams[i % len(streams)]
-        starts[i].record(st)
-        launch(i)
-        ends[i].record(st)
+    if graph is not None:
+        for _ in range(args.steps // nb):
+            graph.replay()
+        for i in range(args.steps % nb):
+            launch(i)
+    else:
+        for i in range(args.steps):
+            launch(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -134,10 +157,24 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
-    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
-    achieved_gbs = step_bytes / (kernel_ms * 1e-3) / 1e9
     value = world * args.steps * step_bytes / elapsed / 2**30
+
+    # kernel duration: eager launches on one stream, each between two HIP events, queued while
+    # the stream is held by a GPU sleep so the events bracket back-to-back kernels
+    st = streams[0]
+    nt = max(1, args.timing_launches)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(int(40e6))
+    for i in range(nt):
+        starts[i].record(st)
+        launch(i, st)
+        ends[i].record(st)
+    torch.cuda.synchronize()
+    durs = sorted(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends))
+    kernel_ms = sum(durs) / nt
+    achieved_gbs = step_bytes / (kernel_ms * 1e-3) / 1e9
 
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -175,12 +212,14 @@ def main():
             "config": {"workload": f"C2: {count} x {L // 1024} KiB independent buffers, {alg.upper()}, "
                                    f"device-resident, per GPU per step",
                        "buffers_per_step": count, "buffer_bytes": L, "rotating_batches": nb,
-                       "resident_bytes_per_gpu": nb * step_bytes, "streams": len(streams),
+                       "resident_bytes_per_gpu": nb * step_bytes, "launch": args.mode,
+                       "graph_branches": len(streams) if graph is not None else 1,
                        "parallelism": f"buffers sharded over {world} GPU(s), no collective"},
             "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kernel_ms, 5), "bytes_per_launch": step_bytes},
+                         "kernel_ms": round(kernel_ms, 5), "kernel_ms_median": round(durs[nt // 2], 5),
+                         "bytes_per_launch": step_bytes, "timing_launches": nt},
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)

@@ -503,3 +503,245 @@ int oracle_batch(int alg, const uint8_t *const *ptrs, const size_t *lens, uint64
         pthread_join(th[t], NULL);
     return 0;
 }
+
+/* ------------------------------------------------------------------ XXH3 (64 / 128) */
+/* Restatement of the published XXH3 algorithm (xxHash 0.8, Yann Collet) behind
+ * aws_xxhash3_64_compute / aws_xxhash3_128_compute (XXHash.cpp:22,27).  Pinned by
+ * tests/XXHashTest.cpp:44 and :73-74 and by python xxhash 3.8.1 over every length class. */
+static const uint8_t XXH3_SECRET[192] = {
+    0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad, 0x1c,
+    0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3, 0x67, 0x1f,
+    0xcb, 0x79, 0xe6, 0x4e, 0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc, 0xff, 0x72, 0x21,
+    0xb8, 0x08, 0x46, 0x74, 0xf7, 0x43, 0x24, 0x8e, 0xe0, 0x35, 0x90, 0xe6, 0x81, 0x3a, 0x26, 0x4c,
+    0x3c, 0x28, 0x52, 0xbb, 0x91, 0xc3, 0x00, 0xcb, 0x88, 0xd0, 0x65, 0x8b, 0x1b, 0x53, 0x2e, 0xa3,
+    0x71, 0x64, 0x48, 0x97, 0xa2, 0x0d, 0xf9, 0x4e, 0x38, 0x19, 0xef, 0x46, 0xa9, 0xde, 0xac, 0xd8,
+    0xa8, 0xfa, 0x76, 0x3f, 0xe3, 0x9c, 0x34, 0x3f, 0xf9, 0xdc, 0xbb, 0xc7, 0xc7, 0x0b, 0x4f, 0x1d,
+    0x8a, 0x51, 0xe0, 0x4b, 0xcd, 0xb4, 0x59, 0x31, 0xc8, 0x9f, 0x7e, 0xc9, 0xd9, 0x78, 0x73, 0x64,
+    0xea, 0xc5, 0xac, 0x83, 0x34, 0xd3, 0xeb, 0xc3, 0xc5, 0x81, 0xa0, 0xff, 0xfa, 0x13, 0x63, 0xeb,
+    0x17, 0x0d, 0xdd, 0x51, 0xb7, 0xf0, 0xda, 0x49, 0xd3, 0x16, 0x55, 0x26, 0x29, 0xd4, 0x68, 0x9e,
+    0x2b, 0x16, 0xbe, 0x58, 0x7d, 0x47, 0xa1, 0xfc, 0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce,
+    0x45, 0xcb, 0x3a, 0x8f, 0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e,
+};
+static const uint64_t XQ32_1 = 0x9E3779B1u, XQ32_2 = 0x85EBCA77u, XQ32_3 = 0xC2B2AE3Du;
+static const uint64_t XMX1 = 0x165667919E3779F9ull, XMX2 = 0x9FB21C651E98DF25ull;
+
+static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+static inline uint64_t mul128_fold64(uint64_t a, uint64_t b) {
+    __uint128_t p = (__uint128_t)a * b;
+    return (uint64_t)p ^ (uint64_t)(p >> 64);
+}
+static inline uint64_t x3_avalanche(uint64_t h) { h ^= h >> 37; h *= XMX1; return h ^ (h >> 32); }
+static inline uint64_t x64_avalanche(uint64_t h) {
+    h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; return h ^ (h >> 32);
+}
+static inline uint64_t rrmxmx(uint64_t h, uint64_t len) {
+    h ^= rotl64(h, 49) ^ rotl64(h, 24);
+    h *= XMX2;
+    h ^= (h >> 35) + len;
+    h *= XMX2;
+    return h ^ (h >> 28);
+}
+static inline uint64_t mix16(const uint8_t *in, const uint8_t *sec, uint64_t seed) {
+    return mul128_fold64(load_le64(in) ^ (load_le64(sec) + seed), load_le64(in + 8) ^ (load_le64(sec + 8) - seed));
+}
+
+static void x3_accumulate_512(uint64_t *acc, const uint8_t *in, const uint8_t *sec) {
+    for (int i = 0; i < 8; ++i) {
+        uint64_t v = load_le64(in + 8 * i), k = v ^ load_le64(sec + 8 * i);
+        acc[i ^ 1] += v;
+        acc[i] += (k & 0xFFFFFFFFull) * (k >> 32);
+    }
+}
+static void x3_scramble(uint64_t *acc, const uint8_t *sec) {
+    for (int i = 0; i < 8; ++i) {
+        uint64_t a = acc[i];
+        a ^= a >> 47;
+        a ^= load_le64(sec + 8 * i);
+        acc[i] = a * XQ32_1;
+    }
+}
+static void x3_long_loop(uint64_t *acc, const uint8_t *in, size_t len, const uint8_t *sec) {
+    const size_t stripes_per_block = (192 - 64) / 8, block = 64 * stripes_per_block;
+    const size_t nb = (len - 1) / block;
+    for (size_t n = 0; n < nb; ++n) {
+        for (size_t s = 0; s < stripes_per_block; ++s) x3_accumulate_512(acc, in + n * block + 64 * s, sec + 8 * s);
+        x3_scramble(acc, sec + 192 - 64);
+    }
+    const size_t ns = ((len - 1) - block * nb) / 64;
+    for (size_t s = 0; s < ns; ++s) x3_accumulate_512(acc, in + nb * block + 64 * s, sec + 8 * s);
+    x3_accumulate_512(acc, in + len - 64, sec + 192 - 64 - 7);
+}
+static uint64_t x3_merge(const uint64_t *acc, const uint8_t *sec, uint64_t start) {
+    uint64_t r = start;
+    for (int i = 0; i < 4; ++i)
+        r += mul128_fold64(acc[2 * i] ^ load_le64(sec + 16 * i), acc[2 * i + 1] ^ load_le64(sec + 16 * i + 8));
+    return x3_avalanche(r);
+}
+static void x3_custom_secret(uint8_t *out, uint64_t seed) {
+    for (int i = 0; i < 12; ++i) {
+        uint64_t lo = load_le64(XXH3_SECRET + 16 * i) + seed, hi = load_le64(XXH3_SECRET + 16 * i + 8) - seed;
+        memcpy(out + 16 * i, &lo, 8);
+        memcpy(out + 16 * i + 8, &hi, 8);
+    }
+}
+static void x3_long_acc(uint64_t *acc, const uint8_t *p, size_t n, uint64_t seed, uint8_t *secbuf, const uint8_t **sec) {
+    const uint64_t init[8] = {XQ32_3, XP1, XP2, XP3, XP4, XQ32_2, XP5, XQ32_1};
+    memcpy(acc, init, sizeof(init));
+    *sec = XXH3_SECRET;
+    if (seed) {
+        x3_custom_secret(secbuf, seed);
+        *sec = secbuf;
+    }
+    x3_long_loop(acc, p, n, *sec);
+}
+
+uint64_t oracle_xxh3_64(const uint8_t *p, size_t n, uint64_t seed) {
+    const uint8_t *s = XXH3_SECRET;
+    if (n <= 16) {
+        if (n > 8) {
+            uint64_t bf1 = (load_le64(s + 24) ^ load_le64(s + 32)) + seed;
+            uint64_t bf2 = (load_le64(s + 40) ^ load_le64(s + 48)) - seed;
+            uint64_t lo = load_le64(p) ^ bf1, hi = load_le64(p + n - 8) ^ bf2;
+            return x3_avalanche(n + bswap64(lo) + hi + mul128_fold64(lo, hi));
+        }
+        if (n >= 4) {
+            uint64_t sd = seed ^ ((uint64_t)bswap32((uint32_t)seed) << 32);
+            uint64_t in64 = ld32(p + n - 4) + ((uint64_t)ld32(p) << 32);
+            uint64_t bf = (load_le64(s + 8) ^ load_le64(s + 16)) - sd;
+            return rrmxmx(in64 ^ bf, n);
+        }
+        if (n > 0) {
+            uint32_t c = ((uint32_t)p[0] << 16) | ((uint32_t)p[n >> 1] << 24) | p[n - 1] | ((uint32_t)n << 8);
+            uint64_t bf = (uint64_t)(ld32(s) ^ ld32(s + 4)) + seed;
+            return x64_avalanche((uint64_t)c ^ bf);
+        }
+        return x64_avalanche(seed ^ (load_le64(s + 56) ^ load_le64(s + 64)));
+    }
+    if (n <= 128) {
+        uint64_t acc = n * XP1;
+        if (n > 32) {
+            if (n > 64) {
+                if (n > 96) {
+                    acc += mix16(p + 48, s + 96, seed);
+                    acc += mix16(p + n - 64, s + 112, seed);
+                }
+                acc += mix16(p + 32, s + 64, seed);
+                acc += mix16(p + n - 48, s + 80, seed);
+            }
+            acc += mix16(p + 16, s + 32, seed);
+            acc += mix16(p + n - 32, s + 48, seed);
+        }
+        acc += mix16(p, s, seed);
+        acc += mix16(p + n - 16, s + 16, seed);
+        return x3_avalanche(acc);
+    }
+    if (n <= 240) {
+        uint64_t acc = n * XP1;
+        const int rounds = (int)(n / 16);
+        for (int i = 0; i < 8; ++i) acc += mix16(p + 16 * i, s + 16 * i, seed);
+        acc = x3_avalanche(acc);
+        for (int i = 8; i < rounds; ++i) acc += mix16(p + 16 * i, s + 16 * (i - 8) + 3, seed);
+        acc += mix16(p + n - 16, s + 136 - 17, seed);
+        return x3_avalanche(acc);
+    }
+    uint64_t acc[8];
+    uint8_t secbuf[192];
+    const uint8_t *sec;
+    x3_long_acc(acc, p, n, seed, secbuf, &sec);
+    return x3_merge(acc, sec + 11, n * XP1);
+}
+
+static void mix32(uint64_t *lo, uint64_t *hi, const uint8_t *a, const uint8_t *b, const uint8_t *sec, uint64_t seed) {
+    *lo += mix16(a, sec, seed);
+    *lo ^= load_le64(b) + load_le64(b + 8);
+    *hi += mix16(b, sec + 16, seed);
+    *hi ^= load_le64(a) + load_le64(a + 8);
+}
+
+/* out[0] = high 64 bits, out[1] = low 64 bits */
+void oracle_xxh3_128(const uint8_t *p, size_t n, uint64_t seed, uint64_t *out) {
+    const uint8_t *s = XXH3_SECRET;
+    uint64_t lo, hi;
+    if (n <= 16) {
+        if (n > 8) {
+            uint64_t bfl = (load_le64(s + 32) ^ load_le64(s + 40)) - seed;
+            uint64_t bfh = (load_le64(s + 48) ^ load_le64(s + 56)) + seed;
+            uint64_t ilo = load_le64(p), ihi = load_le64(p + n - 8);
+            __uint128_t m = (__uint128_t)(ilo ^ ihi ^ bfl) * XP1;
+            uint64_t mlo = (uint64_t)m, mhi = (uint64_t)(m >> 64);
+            mlo += (uint64_t)(n - 1) << 54;
+            ihi ^= bfh;
+            mhi += ihi + (uint64_t)(uint32_t)ihi * (XQ32_2 - 1);
+            mlo ^= bswap64(mhi);
+            __uint128_t h = (__uint128_t)mlo * XP2;
+            lo = (uint64_t)h;
+            hi = (uint64_t)(h >> 64) + mhi * XP2;
+            out[0] = x3_avalanche(hi);
+            out[1] = x3_avalanche(lo);
+            return;
+        }
+        if (n >= 4) {
+            uint64_t sd = seed ^ ((uint64_t)bswap32((uint32_t)seed) << 32);
+            uint64_t in64 = ld32(p) + ((uint64_t)ld32(p + n - 4) << 32);
+            uint64_t bf = (load_le64(s + 16) ^ load_le64(s + 24)) + sd;
+            __uint128_t m = (__uint128_t)(in64 ^ bf) * (XP1 + ((uint64_t)n << 2));
+            uint64_t mlo = (uint64_t)m, mhi = (uint64_t)(m >> 64);
+            mhi += mlo << 1;
+            mlo ^= mhi >> 3;
+            mlo ^= mlo >> 35;
+            mlo *= XMX2;
+            mlo ^= mlo >> 28;
+            out[0] = x3_avalanche(mhi);
+            out[1] = mlo;
+            return;
+        }
+        if (n > 0) {
+            uint32_t cl = ((uint32_t)p[0] << 16) | ((uint32_t)p[n >> 1] << 24) | p[n - 1] | ((uint32_t)n << 8);
+            uint32_t sw = bswap32(cl);
+            uint32_t ch = (sw << 13) | (sw >> 19);
+            uint64_t bfl = (uint64_t)(ld32(s) ^ ld32(s + 4)) + seed;
+            uint64_t bfh = (uint64_t)(ld32(s + 8) ^ ld32(s + 12)) - seed;
+            out[0] = x64_avalanche((uint64_t)ch ^ bfh);
+            out[1] = x64_avalanche((uint64_t)cl ^ bfl);
+            return;
+        }
+        out[1] = x64_avalanche(seed ^ (load_le64(s + 64) ^ load_le64(s + 72)));
+        out[0] = x64_avalanche(seed ^ (load_le64(s + 80) ^ load_le64(s + 88)));
+        return;
+    }
+    if (n <= 128) {
+        lo = n * XP1;
+        hi = 0;
+        if (n > 32) {
+            if (n > 64) {
+                if (n > 96) mix32(&lo, &hi, p + 48, p + n - 64, s + 96, seed);
+                mix32(&lo, &hi, p + 32, p + n - 48, s + 64, seed);
+            }
+            mix32(&lo, &hi, p + 16, p + n - 32, s + 32, seed);
+        }
+        mix32(&lo, &hi, p, p + n - 16, s, seed);
+    } else if (n <= 240) {
+        const int rounds = (int)(n / 32);
+        lo = n * XP1;
+        hi = 0;
+        for (int i = 0; i < 4; ++i) mix32(&lo, &hi, p + 32 * i, p + 32 * i + 16, s + 32 * i, seed);
+        lo = x3_avalanche(lo);
+        hi = x3_avalanche(hi);
+        for (int i = 4; i < rounds; ++i) mix32(&lo, &hi, p + 32 * i, p + 32 * i + 16, s + 3 + 32 * (i - 4), seed);
+        mix32(&lo, &hi, p + n - 16, p + n - 32, s + 136 - 17 - 16, 0ull - seed);
+    } else {
+        uint64_t acc[8];
+        uint8_t secbuf[192];
+        const uint8_t *sec;
+        x3_long_acc(acc, p, n, seed, secbuf, &sec);
+        out[1] = x3_merge(acc, sec + 11, n * XP1);
+        out[0] = x3_merge(acc, sec + 192 - 64 - 11, ~(n * XP2));
+        return;
+    }
+    uint64_t rl = lo + hi;
+    uint64_t rh = lo * XP1 + hi * XP4 + (n - seed) * XP2;
+    out[1] = x3_avalanche(rl);
+    out[0] = 0ull - x3_avalanche(rh);
+}
