@@ -15,9 +15,10 @@ from typing import Optional, Sequence
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-crt-cpp-amd.so")
 
-CRC32, CRC32C, CRC64NVME, XXH64 = 0, 1, 2, 3
-ALGORITHMS = {"crc32": CRC32, "crc32c": CRC32C, "crc64nvme": CRC64NVME, "xxh64": XXH64}
-WIDE = {CRC64NVME, XXH64}  # 64-bit results
+CRC32, CRC32C, CRC64NVME, XXH64, XXH3_64, XXH3_128 = 0, 1, 2, 3, 4, 5
+ALGORITHMS = {"crc32": CRC32, "crc32c": CRC32C, "crc64nvme": CRC64NVME, "xxh64": XXH64, "xxh3_64": XXH3_64,
+              "xxh3_128": XXH3_128}
+WIDE = {CRC64NVME, XXH64, XXH3_64, XXH3_128}  # 64-bit result words (XXH3_128: two per buffer)
 
 _lib = None
 
@@ -92,7 +93,7 @@ def checksum_strided(alg: int, base, stride: int, length: int, count: int, seeds
     addr = (base.data_ptr() if hasattr(base, "data_ptr") else int(base)) + base_offset
     dev = base.device if hasattr(base, "device") else torch.device("cuda")
     if out is None:
-        out = torch.empty(count, dtype=_out_dtype(alg), device=dev)
+        out = torch.empty(count * (2 if alg == XXH3_128 else 1), dtype=_out_dtype(alg), device=dev)
     sp = seeds.data_ptr() if seeds is not None else None
     _check(lib().aws_crt_amd_checksum_strided(alg, addr, stride, length, count, sp, out.data_ptr(),
                                               _stream_handle(stream)))
@@ -105,7 +106,7 @@ def checksum_list(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None
 
     n = len(ptrs)
     if out is None:
-        out = torch.empty(n, dtype=_out_dtype(alg), device=device or "cuda")
+        out = torch.empty(n * (2 if alg == XXH3_128 else 1), dtype=_out_dtype(alg), device=device or "cuda")
     P = (ctypes.c_void_p * n)(*ptrs)
     S = (ctypes.c_size_t * n)(*lens)
     sp = seeds.data_ptr() if seeds is not None else None
@@ -132,10 +133,12 @@ def checksum_host(alg: int, buffers: Sequence[bytes], seeds: Optional[Sequence[i
     P = (ctypes.c_void_p * n)(*[ctypes.addressof(k) for k in keep])
     S = (ctypes.c_size_t * n)(*[len(b) for b in buffers])
     T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
-    out = (T * n)()
+    out = (T * (2 * n if alg == XXH3_128 else n))()
     sd = (T * n)(*seeds) if seeds is not None else None
     _check(lib().aws_crt_amd_checksum_host(alg, P, S, n, ctypes.cast(sd, ctypes.c_void_p) if sd else None,
                                            ctypes.cast(out, ctypes.c_void_p)))
+    if alg == XXH3_128:
+        return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
     return list(out)
 
 

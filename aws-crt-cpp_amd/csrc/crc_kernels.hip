@@ -371,7 +371,8 @@ __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
             "s_load_dwordx2 %4, %8, 0x20\n\ts_load_dwordx2 %5, %8, 0x28\n\t"
             "s_load_dwordx2 %6, %8, 0x30\n\ts_load_dwordx2 %7, %8, 0x38\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=s"(k0), "=s"(k1), "=s"(k2), "=s"(k3), "=s"(k4), "=s"(k5), "=s"(k6), "=s"(k7)
+            // early-clobber: a returning load must never overwrite the shared address operand
+            : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
             : "s"(cols + c)
             : "memory");
         const uint64_t k[8] = {k0, k1, k2, k3, k4, k5, k6, k7};

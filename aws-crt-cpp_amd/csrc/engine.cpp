@@ -229,6 +229,14 @@ uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main)
     return (uint32_t)std::max<uint64_t>(seg, kGroupBytes);
 }
 
+inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
+
+int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
+    int e = alg == AWS_CRT_AMD_XXH64 ? amdcrc_launch_xxh64(&xp, s)
+                                     : amdcrc_launch_xxh3(alg == AWS_CRT_AMD_XXH3_64 ? 64 : 128, &xp, s);
+    return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("hash kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+}
+
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, hipStream_t s) {
     const uint64_t tile = (uint64_t)p.seg * kWave;
     int rc = get_kvals(d, alg, p.seg, &p.d_kvals);
@@ -258,7 +266,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
                  uint64_t seed_all, void *d_out, hipStream_t s) {
     if (count == 0) return 0;
     if (!d_out || (len && !base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
-    if (alg == AWS_CRT_AMD_XXH64) {
+    if (is_hash(alg)) {
         XxhParams xp{};
         xp.base = base;
         xp.stride = stride;
@@ -267,8 +275,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         xp.d_seeds = (const uint64_t *)d_seeds;
         xp.seed_all = seed_all;
         xp.d_out = (uint64_t *)d_out;
-        int e = amdcrc_launch_xxh64(&xp, s);
-        return e ? fail(AWS_CRT_AMD_ERR_HIP, "xxh64 launch failed") : 0;
+        return launch_hash(alg, xp, s);
     }
     if (count > 1 && (stride % 16) != 0)
         return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
@@ -337,7 +344,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         mains[i] = main_len((uint64_t)(uintptr_t)ptrs[i], lens[i]);
         total += mains[i];
     }
-    const bool xxh = alg == AWS_CRT_AMD_XXH64;
+    const bool xxh = is_hash(alg);
     uint32_t seg = kGroupBytes;
     uint64_t tile = 0;
     if (!xxh) {
@@ -381,8 +388,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         xp.nbuf = count;
         xp.d_seeds = (const uint64_t *)d_seeds;
         xp.d_out = (uint64_t *)d_out;
-        int e = amdcrc_launch_xxh64(&xp, s);
-        return e ? fail(AWS_CRT_AMD_ERR_HIP, "xxh64 launch failed") : 0;
+        return launch_hash(alg, xp, s);
     }
     ScanParams p{};
     p.seg = seg;
@@ -437,17 +443,17 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
     std::lock_guard<std::mutex> g(d->single_mu);
     if ((rc = ensure_stage(d, std::min(kStageChunk, std::max<size_t>(len, 4096))))) return rc;
     hipStream_t s = d->own_stream;
-    const size_t osz = width_of(alg) == 64 || alg == AWS_CRT_AMD_XXH64 ? 8 : 4;
+    const size_t osz = alg == AWS_CRT_AMD_XXH3_128 ? 16 : (width_of(alg) == 64 || is_hash(alg)) ? 8 : 4;
     char *res = (char *)d->d_small;  // two result slots (ping-pong) + seed slot
     if (len == 0 || !input) {
         // CRC of nothing is the seed itself (state ~seed, complemented back); XXH64 still runs
-        if (alg != AWS_CRT_AMD_XXH64) {
+        if (!is_hash(alg)) {
             *result = seed;
             return 0;
         }
     }
-    if (alg == AWS_CRT_AMD_XXH64) {
-        // XXH64 is not chunkable by seed; stage the whole buffer if it is in host memory
+    if (is_hash(alg)) {
+        // xxHash is not chunkable by seed; stage the whole buffer if it is in host memory
         const void *dp = input;
         DevBuf tmp;
         if (len && !is_device_ptr(input)) {
@@ -457,14 +463,15 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
         }
         uint64_t base = len ? (uint64_t)(uintptr_t)dp : 16;
         rc = strided_impl(d, alg, base, len, len, 1, nullptr, seed, res, s);
-        uint64_t out = 0;
+        uint64_t out[2] = {0, 0};
         if (!rc) {
-            hipError_t e = hipMemcpyAsync(&out, res, 8, hipMemcpyDeviceToHost, s);
+            hipError_t e = hipMemcpyAsync(out, res, osz, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = fail(AWS_CRT_AMD_ERR_HIP, hipGetErrorString(e));
         }
         if (tmp.p) (void)hipFree(tmp.p);
-        *result = out;
+        result[0] = out[0];
+        if (osz == 16) result[1] = out[1];
         return rc;
     }
     if (is_device_ptr(input)) {
@@ -526,7 +533,7 @@ AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void) { return g_last_error.c
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,
                                                  const void *d_seeds, void *d_out, void *hip_stream) {
-    if (alg < 0 || alg > 3) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
     Device *d;
     int rc = get_device(&d);
     if (rc) return rc;
@@ -536,7 +543,7 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, si
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,
                                               const void *d_seeds, void *d_out, void *hip_stream) {
-    if (alg < 0 || alg > 3) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
     Device *d;
     int rc = get_device(&d);
     if (rc) return rc;
@@ -545,18 +552,22 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_host(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                               const void *h_seeds, void *h_out) {
-    if (alg < 0 || alg > 3) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
-    const bool w64 = alg == AWS_CRT_AMD_CRC64NVME || alg == AWS_CRT_AMD_XXH64;
+    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+    const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
     for (size_t i = 0; i < count; ++i) {
         uint64_t seed = 0;
-        if (h_seeds) seed = w64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
-        uint64_t r;
-        int rc = single_impl(alg, h_ptrs[i], lens[i], seed, &r);
+        if (h_seeds) seed = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+        uint64_t r[2] = {0, 0};
+        int rc = single_impl(alg, h_ptrs[i], lens[i], seed, r);
         if (rc) return rc;
-        if (w64)
-            ((uint64_t *)h_out)[i] = r;
-        else
-            ((uint32_t *)h_out)[i] = (uint32_t)r;
+        if (alg == AWS_CRT_AMD_XXH3_128) {
+            ((uint64_t *)h_out)[2 * i] = r[0];
+            ((uint64_t *)h_out)[2 * i + 1] = r[1];
+        } else if (seed64) {
+            ((uint64_t *)h_out)[i] = r[0];
+        } else {
+            ((uint32_t *)h_out)[i] = (uint32_t)r[0];
+        }
     }
     return 0;
 }
@@ -633,8 +644,7 @@ int aws_crt_amd_xxh64_single(const void *input, size_t len, uint64_t seed, uint6
 
 }  // extern "C"
 
-// XXH3 is implemented in a later milestone (xxh3 kernels); until then report unsupported.
-extern "C" int aws_crt_amd_xxh3_single(int, const void *, size_t, uint64_t, uint64_t *) {
-    g_last_error = "xxh3 not yet available on device";
-    return AWS_CRT_AMD_ERR_INVALID_ARG;
+// internal: XXH3-64 / XXH3-128 of one buffer for the xxhash ABI; out = {hash} or {high, low}
+extern "C" int aws_crt_amd_xxh3_single(int bits, const void *input, size_t len, uint64_t seed, uint64_t *out) {
+    return single_impl(bits == 64 ? AWS_CRT_AMD_XXH3_64 : AWS_CRT_AMD_XXH3_128, input, len, seed, out);
 }

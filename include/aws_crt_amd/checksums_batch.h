@@ -18,7 +18,8 @@
  *                XXH64 seed.
  *
  * All pointers named d_* are device addresses on the current HIP device.  Results are written
- * to d_out (uint32_t per buffer for CRC32/CRC32C, uint64_t for CRC64NVME/XXH64).  Calls are
+ * to d_out (uint32_t per buffer for CRC32/CRC32C, uint64_t for CRC64NVME/XXH64/XXH3_64, two uint64_t
+ * {high, low} for XXH3_128).  Calls are
  * asynchronous on `hip_stream` (a hipStream_t; NULL = the legacy default stream).  Inputs must stay
  * valid until the stream reaches the work.  Every call returns 0 on success or a negative
  * aws_crt_amd_status; aws_crt_amd_last_error() describes the last failure on the calling thread.
@@ -42,6 +43,8 @@ enum aws_crt_amd_algorithm {
     AWS_CRT_AMD_CRC32C = 1,
     AWS_CRT_AMD_CRC64NVME = 2,
     AWS_CRT_AMD_XXH64 = 3,
+    AWS_CRT_AMD_XXH3_64 = 4,
+    AWS_CRT_AMD_XXH3_128 = 5, /* 16 bytes per buffer: high 64 bits, then low 64 bits */
 };
 
 enum aws_crt_amd_status {

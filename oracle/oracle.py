@@ -37,6 +37,8 @@ def lib() -> ctypes.CDLL:
             f = getattr(L, f"oracle_{name}_combine")
             f.restype, f.argtypes = t, [t, t, u64]
         L.oracle_xxh64.restype, L.oracle_xxh64.argtypes = u64, [vp, sz, u64]
+        L.oracle_xxh3_64.restype, L.oracle_xxh3_64.argtypes = u64, [vp, sz, u64]
+        L.oracle_xxh3_128.restype, L.oracle_xxh3_128.argtypes = None, [vp, sz, u64, ctypes.POINTER(u64)]
         L.oracle_xpow8n.restype, L.oracle_xpow8n.argtypes = u64, [u64, ctypes.c_int]
         L.oracle_mulmod.restype, L.oracle_mulmod.argtypes = u64, [u64, u64, ctypes.c_int]
         L.oracle_hw_available.restype = ctypes.c_int
@@ -67,8 +69,27 @@ def xxh64(data, seed: int = 0) -> int:
     return lib().oracle_xxh64(p, n, seed)
 
 
+def xxh3_64(data, seed: int = 0) -> int:
+    p, n, keep = _ptr(data)
+    return lib().oracle_xxh3_64(p, n, seed)
+
+
+def xxh3_128(data, seed: int = 0) -> int:
+    """128-bit value, high half first (canonical XXH128 digest order)"""
+    p, n, keep = _ptr(data)
+    out = (ctypes.c_uint64 * 2)()
+    lib().oracle_xxh3_128(p, n, seed, out)
+    return (out[0] << 64) | out[1]
+
+
 def checksum(name: str, data, seed: int = 0) -> int:
-    return xxh64(data, seed) if name == "xxh64" else crc(name, data, seed)
+    if name == "xxh64":
+        return xxh64(data, seed)
+    if name == "xxh3_64":
+        return xxh3_64(data, seed)
+    if name == "xxh3_128":
+        return xxh3_128(data, seed)
+    return crc(name, data, seed)
 
 
 def combine(name: str, c1: int, c2: int, len2: int) -> int:

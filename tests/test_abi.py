@@ -1,0 +1,86 @@
+"""CPU: the C-ABI shared library loads (no device needed) and exports every function the public
+headers under include/ declare -- the drop-in boundary."""
+import ctypes
+import os
+import re
+import subprocess
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
+C_HEADERS = ["include/aws_crt_amd/checksums_batch.h", "include/aws/checksums/crc.h", "include/aws/checksums/xxhash.h",
+             "include/aws/common/allocator.h", "include/aws/common/byte_buf.h", "include/aws/common/error.h"]
+
+
+def declared_c_functions(path):
+    text = open(os.path.join(REPO, path)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(aws_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(n for n in names if not n.endswith("_t")))
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_library_loads_without_gpu():
+    L = ctypes.CDLL(LIB)
+    assert L.aws_crt_amd_device_count() >= 0
+
+
+def test_every_declared_c_symbol_is_exported():
+    syms = exported()
+    missing = []
+    for h in C_HEADERS:
+        for fn in declared_c_functions(h):
+            if fn not in syms:
+                missing.append((h, fn))
+    assert not missing, missing
+
+
+def test_cpp_api_symbols_exported():
+    out = subprocess.run(["nm", "-DC", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    for sig in ["Aws::Crt::Checksum::ComputeCRC32(aws_byte_cursor, unsigned int)",
+                "Aws::Crt::Checksum::ComputeCRC32C(aws_byte_cursor, unsigned int)",
+                "Aws::Crt::Checksum::ComputeCRC64NVME(aws_byte_cursor, unsigned long)",
+                "Aws::Crt::Checksum::CombineCRC32(unsigned int, unsigned int, unsigned long)",
+                "Aws::Crt::Checksum::CombineCRC32C(unsigned int, unsigned int, unsigned long)",
+                "Aws::Crt::Checksum::CombineCRC64NVME(unsigned long, unsigned long, unsigned long)",
+                "Aws::Crt::Checksum::ComputeXXHash64(aws_byte_cursor const&, aws_byte_buf&, unsigned long)",
+                "Aws::Crt::Checksum::ComputeXXHash3_64(aws_byte_cursor const&, aws_byte_buf&, unsigned long)",
+                "Aws::Crt::Checksum::ComputeXXHash3_128(aws_byte_cursor const&, aws_byte_buf&, unsigned long)",
+                "Aws::Crt::Checksum::XXHash::Update(aws_byte_cursor const&)",
+                "Aws::Crt::Checksum::XXHash::Digest(aws_byte_buf&)",
+                "Aws::Crt::ApiHandle::ApiHandle(aws_allocator*)", "Aws::Crt::LastError()"]:
+        assert sig in out, sig
+
+
+def test_no_oracle_in_product():
+    """The product library must not link or embed the test oracle."""
+    out = subprocess.run(["nm", "-D", LIB], capture_output=True, text=True, check=True).stdout
+    assert "oracle_" not in out
+    deps = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True, check=True).stdout
+    assert "liboracle" not in deps
+
+
+def test_combine_scalar_abi_matches_oracle():
+    """aws_checksums_*_combine is scalar GF(2) algebra (no payload) and callable without a device."""
+    from oracle import oracle
+    L = ctypes.CDLL(LIB)
+    for name, t in (("crc32", ctypes.c_uint32), ("crc32c", ctypes.c_uint32), ("crc64nvme", ctypes.c_uint64)):
+        f = getattr(L, f"aws_checksums_{name}_combine")
+        f.restype, f.argtypes = t, [t, t, ctypes.c_uint64]
+        for a, b, n in [(0, 0, 0), (0x12345678, 0x9ABCDEF0, 1), (0xFFFFFFFF, 1, 1 << 33), (7, 11, 123456789)]:
+            assert f(a, b, n) == oracle.combine(name, a, b, n)
+
+
+def test_no_device_fails_loudly():
+    """Without a device the batch ABI returns AWS_CRT_AMD_ERR_NO_DEVICE (no silent CPU fallback)."""
+    L = ctypes.CDLL(LIB)
+    if L.aws_crt_amd_device_count() > 0:
+        import pytest
+        pytest.skip("device present")
+    L.aws_crt_amd_last_error.restype = ctypes.c_char_p
+    rc = L.aws_crt_amd_checksum_strided(1, ctypes.c_void_p(0x1000), 16, 16, 1, None, ctypes.c_void_p(0x2000), None)
+    assert rc == -1
+    assert b"no HIP device" in L.aws_crt_amd_last_error()

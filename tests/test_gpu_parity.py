@@ -19,8 +19,15 @@ from tests.golden.patterns import pattern
 pytestmark = pytest.mark.gpu
 
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "vectors.json")))
-ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3}
-W64 = {"crc64nvme", "xxh64"}
+ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
+W64 = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
+
+
+def results(engine, alg, out):
+    v = engine.as_unsigned(out)
+    if alg == "xxh3_128":
+        return [(v[2 * i] << 64) | v[2 * i + 1] for i in range(len(v) // 2)]
+    return v
 
 
 def dev_random(n, seed):
@@ -61,7 +68,7 @@ def test_single_abi_device_pointer(engine):
         assert engine.crc(alg, t, 77) == oracle.crc(alg, h, 77)
 
 
-@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_golden_vectors_list(engine, alg):
     import torch
 
@@ -81,7 +88,7 @@ def test_golden_vectors_list(engine, alg):
     out = engine.checksum_list(ALG[alg], [base + o for o in offs], [len(b) for b in blobs],
                                seeds=seeds_tensor(alg, [v["seed"] for v in vs]))
     torch.cuda.synchronize()
-    got = engine.as_unsigned(out)
+    got = results(engine, alg, out)
     for v, g in zip(vs, got):
         assert g == v["expect"], v
 
@@ -119,7 +126,7 @@ def test_strided_shapes_with_seeds(engine, alg, L, off, count):
     assert engine.as_unsigned(out) == want
 
 
-@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_ragged_list_random(engine, alg):
     import torch
 
@@ -137,7 +144,7 @@ def test_ragged_list_random(engine, alg):
     torch.cuda.synchronize()
     h = host_bytes(d)
     want = [oracle.checksum(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
-    assert engine.as_unsigned(out) == want
+    assert results(engine, alg, out) == want
 
 
 @pytest.mark.parametrize("alg", ["crc32", "crc32c"])
@@ -185,7 +192,7 @@ def test_combine_batch_device(engine):
 def test_host_path_chunked(engine):
     rng = random.Random(8)
     bufs = [rng.randbytes(n) for n in (0, 1, 5000, (16 << 20) + 77, (40 << 20) + 3)]
-    for alg in ("crc32", "crc32c", "crc64nvme", "xxh64"):
+    for alg in ("crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"):
         seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
         got = engine.checksum_host(ALG[alg], bufs, seeds)
         assert got == [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)]
