@@ -188,6 +188,7 @@ struct EngFor<ALG_CRC64NVME> {
 // fields only) and by the scan cursor (everything); both are pure arithmetic in strided mode.
 struct Tile {
     uint64_t b, k, T;
+    uint64_t tbase;  // global index of the buffer's first tile
     uint64_t vbase;  // device address of this tile's virtual offset 0
     uint64_t H;      // first byte of the 16-aligned main region
     uint64_t ptr, headend, tail;
@@ -225,6 +226,7 @@ __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walke
         d.T = p.tiles_per_buf;
         d.b = t / d.T;
         d.k = t - d.b * d.T;
+        d.tbase = t - d.k;
         ptr = p.base + d.b * p.stride;
         n = p.len;
     } else {
@@ -236,6 +238,7 @@ __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walke
         d.b = wk.b;
         d.k = t - wk.lo;
         d.T = wk.hi - wk.lo;
+        d.tbase = wk.lo;
         ptr = sload64(p.d_ptrs + d.b);
         n = sload64(p.d_lens + d.b);
     }
@@ -548,7 +551,14 @@ __global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p)
     // finish tiles whose groups are all scanned (and empty tiles); false once the wave is done
     auto settle = [&]() -> bool {
         while (gp >= dp.ngroups) {
-            finish_tile(p, dp, s, s_h, eng, lane, pd);
+            if (p.dbg & 1) {
+                if (lane == 0) ((uint32_t *)p.d_out)[dp.b] = (uint32_t)s;  // timing experiment only
+            } else if (p.dbg & 2) {
+                const T r = wave_xor(eng.mulK(s, lane));
+                if (lane == 0) ((uint32_t *)p.d_out)[dp.b] = (uint32_t)r;
+            } else {
+                finish_tile(p, dp, s, s_h, eng, lane, pd);
+            }
             if (++tp >= t1) return false;
             dp = make_tile(p, tp, wp);
             gp = 0;
@@ -584,6 +594,368 @@ __global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p)
         settle();
     }
     resolve(p, pd, eng, lane);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// W = 32 braided scan (CRC32 / CRC32C): the production path for the 32-bit CRCs.
+//
+// A tile of TILE bytes is R = TILE/256 rows of 256 bytes; lane l owns the 4-byte word at 4l of
+// every row, so each wave-wide load reads 256 contiguous bytes (fully coalesced: measured 8.0 TB/s
+// read-only on MI355X, where the lane-contiguous segments above reach about half of that).
+// Lane l's state u is one "braid" of the CRC:
+//     u <- (u ^ w_row) * x^(8*256)       (four lookups in T', whose entries fold in the skip over
+//                                          the other 63 lanes' words of the row)
+// After the R rows u = sum_c w_c * x^(8*256(R-c)), while word (c, l) belongs at x^(8(TILE-256c-4l))
+// relative to the tile end.  So u * x^(-32 l) is lane l's exact share (x is invertible mod P since
+// P(0) = 1): K_l = x^(-32 l), and the tile register is XOR_l u_l * K_l -- the same per-lane matrix
+// and wave reduction as the segment kernel, with no extra lookups per byte.
+constexpr uint32_t kT0Off = kTabBytes + kKmatBytes;  // plain byte table (1 KiB; wave-uniform reads)
+constexpr uint32_t kPcolOff = kT0Off + 1024;         // [m < 32][column j] of x^(8*TILE*m) (4 KiB)
+constexpr uint32_t kBraidLds = kPcolOff + 4096;
+
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+typedef __attribute__((address_space(1))) const uint64_t gu64;
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t c, uint32_t m) {  // acc ^ (c & m)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(acc), "v"(c), "v"(m));
+    return r;
+}
+
+// XOR over the 64 lanes, returned wave-uniform: two quad_perm and two row_ror DPP steps leave each
+// 16-lane row's XOR in all its lanes; four readlanes finish in scalar registers.
+__device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
+                      __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
+}
+
+template <uint32_t POLY>
+struct Braid32 {
+    using T = uint32_t;
+    static constexpr int W = 32;
+    const char *L;
+    uint32_t srcA, srcB;  // per-lane perm constants: copy<<2 (| 1<<16 for tables 2,3)
+
+    __device__ void init(const char *lds, int lane) {
+        L = lds;
+        srcA = (uint32_t)(lane & 31) << 2;
+        srcB = srcA | 0x10000u;
+    }
+    // the four T' lookups of a = u ^ w (same conflict-free LDS layout as Eng32)
+    __device__ __forceinline__ void look(uint32_t a, uint32_t &l3, uint32_t &l2, uint32_t &l1, uint32_t &l0) const {
+        l3 = lds32(L, __builtin_amdgcn_perm(srcB, a, 0x0c060004u) + 128);  // byte0 -> T'3
+        l2 = lds32(L, __builtin_amdgcn_perm(srcB, a, 0x0c060104u));        // byte1 -> T'2
+        l1 = lds32(L, __builtin_amdgcn_perm(srcA, a, 0x0c060204u) + 128);  // byte2 -> T'1
+        l0 = lds32(L, __builtin_amdgcn_perm(srcA, a, 0x0c060304u));        // byte3 -> T'0
+    }
+    // a * x^(8*256)
+    __device__ __forceinline__ uint32_t step(uint32_t a) const {
+        uint32_t l3, l2, l1, l0;
+        look(a, l3, l2, l1, l0);
+        return l3 ^ l2 ^ l1 ^ l0;
+    }
+    // a * x^(8*256) ^ wn  (two 3-input XORs)
+    __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
+        uint32_t l3, l2, l1, l0;
+        look(a, l3, l2, l1, l0);
+        return xor3(xor3(l3, l2, wn), l1, l0);
+    }
+    // plain byte step for head / tail bytes (s is wave-uniform: broadcast reads)
+    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
+        return (s >> 8) ^ lds32(L, kT0Off + 4 * ((s ^ b) & 0xffu));
+    }
+    // r * K_lane : 32 LDS matrix columns
+    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint4 c = *(const uint4 *)(L + kTabBytes + (g * 64 + lane) * 16);
+            acc = xor_and(acc, c.x, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 0), 1));
+            acc = xor_and(acc, c.y, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 1), 1));
+            acc = xor_and(acc, c.z, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 2), 1));
+            acc = xor_and(acc, c.w, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 3), 1));
+        }
+        return acc;
+    }
+};
+
+struct BGroup {
+    uint32_t w[kBraidRowsPerGroup];
+};
+
+// group gi of tile d: rows [16 gi, 16 gi + 16), this lane's word of each (virtual offset
+// gi*4096 + 256 r + 4 lane).  Words in the virtual front pad read a valid address (the main start)
+// and are zeroed by braid_proc.
+__device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi, int lane) {
+    const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
+    if (d.pad == 0) {
+        const uint64_t a = d.vbase + vo0;
+#pragma unroll
+        for (int r = 0; r < kBraidRowsPerGroup; ++r) g.w[r] = *(gu32 *)(a + kBraidRow * r);
+    } else {
+#pragma unroll
+        for (int r = 0; r < kBraidRowsPerGroup; ++r) {
+            const uint32_t vo = vo0 + kBraidRow * r;
+            g.w[r] = *(gu32 *)(vo >= d.pad ? d.vbase + vo : d.H);
+        }
+    }
+}
+
+template <class B>
+__device__ __forceinline__ uint32_t braid_proc(uint32_t u, const BGroup &g, const B &eng, const Tile &d, uint32_t gi,
+                                               int lane, uint32_t s_h) {
+    if (d.pad == 0) {
+        uint32_t a = u ^ g.w[0];
+#pragma unroll
+        for (int r = 0; r + 1 < kBraidRowsPerGroup; ++r) a = eng.step_x(a, g.w[r + 1]);
+        return eng.step(a);
+    }
+    const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
+#pragma unroll
+    for (int r = 0; r < kBraidRowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kBraidRow * r;
+        uint32_t w = vo >= d.pad ? g.w[r] : 0u;
+        if (vo == d.pad) w ^= s_h;  // this braid is still zero here: the head state enters with the word
+        u = eng.step(u ^ w);
+    }
+    return u;
+}
+
+// Cross-tile combine.  Tiles form groups of 32; tile k's register is moved to its group's end
+// (r * x^(8*TILE*m), m < 32: columns in LDS, one per lane).  A wave merges the shares of its own
+// consecutive tiles of one group in registers {arrival bits | XOR} and publishes them with one
+// 64-bit atomic XOR into the group's slot when it moves to another group or runs out of tiles.
+// Whoever completes the slot's arrival bits finishes the buffer (T <= 32), or moves the group value
+// to the buffer end (scalar column table, once per group) and XORs it into the buffer word, counting
+// groups (T > 32).  At most 32 atomics meet on one address, and a wave waits for a returned value
+// only when it publishes its next group (rare) or at its end.
+struct BGroupAcc {
+    uint64_t slot;  // ~0: no open group
+    unsigned long long val;
+    uint64_t b, G, shift, tail;
+    uint32_t n, tail_len;
+};
+struct BPending {
+    bool valid;
+    unsigned long long val, old;
+    BGroupAcc g;
+};
+
+template <class B>
+__device__ void braid_resolve(const ScanParams &p, BPending &pd, const B &eng, int lane) {
+    if (!pd.valid) return;
+    pd.valid = false;
+    const unsigned long long now = rfl64(pd.old) ^ pd.val;
+    const BGroupAcc &g = pd.g;
+    const unsigned long long full = g.n >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << g.n) - 1) << 32);
+    if ((now & 0xFFFFFFFF00000000ull) != full) return;
+    uint32_t grp = (uint32_t)now;
+    if (g.G > 1 && g.shift) grp = mul_pcols<uint32_t, 32>(grp, p.d_pcols + g.shift * 32);
+    if (lane != 0) return;
+    __hip_atomic_exchange(&p.d_acc1[g.slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (g.G == 1) {
+        finalize(p, g.b, grp, g.tail, g.tail_len, eng);
+        return;
+    }
+    const unsigned long long o =
+        __hip_atomic_fetch_xor(&p.d_acc[g.b], (unsigned long long)grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(o) : "memory");  // performed before it is counted
+    const unsigned int c = __hip_atomic_fetch_add(&p.d_cnt[g.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (c == g.G - 1) {
+        const uint32_t fin = (uint32_t)__hip_atomic_exchange(&p.d_acc[g.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.d_cnt[g.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        finalize(p, g.b, fin, g.tail, g.tail_len, eng);
+    }
+}
+
+template <class B>
+__device__ void braid_publish(const ScanParams &p, BGroupAcc &acc, BPending &pd, const B &eng, int lane) {
+    if (acc.slot == ~0ull) return;
+    braid_resolve(p, pd, eng, lane);
+    unsigned long long old = 0;
+    if (lane == 0) old = atomic_xor_ret(&p.d_acc1[acc.slot], acc.val);
+    pd.valid = true;
+    pd.val = acc.val;
+    pd.old = old;
+    pd.g = acc;
+    acc.slot = ~0ull;
+}
+
+template <class B>
+__device__ void braid_finish(const ScanParams &p, const Tile &d, uint32_t u, uint32_t s_h, const B &eng, int lane,
+                             BGroupAcc &acc, BPending &pd) {
+    if (p.dbg & 1) {  // timing experiments only (AMDCRC_DEBUG): results are invalid
+        if (lane == 0) ((uint32_t *)p.d_out)[d.b] = u;
+        return;
+    }
+    const uint32_t r = d.ngroups ? wave_xor_s(eng.mulK(u, lane)) : 0u;
+    if (d.T == 1) {
+        if (lane == 0) finalize(p, d.b, d.ngroups ? r : s_h, d.tail, d.tail_len, eng);
+        return;
+    }
+    // r * x^(8*TILE*m) to the group end: lane j < 32 takes column j if bit (31 - j) of r is set
+    const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
+    const uint32_t m = (uint32_t)(gend - 1 - d.k);
+    const uint32_t colv = lds32(eng.L, kPcolOff + 4 * (m * 32 + (lane & 31)));
+    const uint32_t sel = lane < 32 ? (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - lane, 1) : 0u;
+    const uint32_t v = wave_xor_s(colv & sel);
+    const uint64_t slot = d.tbase + g0;
+    if (slot != acc.slot) {
+        braid_publish(p, acc, pd, eng, lane);
+        acc.slot = slot;
+        acc.val = 0;
+        acc.b = d.b;
+        acc.n = (uint32_t)(gend - g0);
+        acc.G = (d.T + 31) / 32;
+        acc.shift = d.T - gend;
+        acc.tail = d.tail;
+        acc.tail_len = d.tail_len;
+    }
+    acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
+}
+
+template <uint32_t POLY>
+__global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams p) {
+    using B = Braid32<POLY>;
+    __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
+
+    Walker w0{0, 0, 0};
+    if (p.list_mode && t0 < t1) {
+        w0.b = sload64(p.d_wave_buf + gw);
+        w0.lo = sload64(p.d_tile_prefix + w0.b);
+        w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
+    }
+    // ---- prefetch cursor: the next (tile, group) to load; parks on the last group when exhausted
+    Walker wf = w0;
+    uint64_t tf = t0;
+    uint32_t gf = 0;
+    Tile df{};
+    bool any = false;
+    for (; tf < t1; ++tf) {
+        df = make_tile(p, tf, wf);
+        if (df.ngroups) {
+            any = true;
+            break;
+        }
+    }
+    bool pf_done = !any;
+    auto pf_advance = [&]() {
+        if (gf + 1 < df.ngroups) {
+            ++gf;
+            return;
+        }
+        if (pf_done) return;
+        Walker w2 = wf;
+        for (uint64_t t = tf + 1; t < t1; ++t) {
+            Tile d2 = make_tile(p, t, w2);
+            if (d2.ngroups) {
+                df = d2;
+                wf = w2;
+                tf = t;
+                gf = 0;
+                return;
+            }
+        }
+        pf_done = true;
+    };
+    // constants (this thread's K-image word, T' entry and T0 entry), then the first two payload
+    // groups, all before the LDS build so their latency overlaps it
+    const uint32_t *cw = (const uint32_t *)p.d_kvals;
+    const uint64_t kq = *(gu64 *)(p.d_kvals + threadIdx.x);
+    const uint32_t te = *(gu32 *)(cw + 2048 + threadIdx.x);
+    const uint32_t t0e = *(gu32 *)(cw + 3072 + (threadIdx.x & 255));
+    // P columns m < 32 (the host table always holds at least 64 entries when T > 1)
+    const uint32_t pce = *(gu32 *)(p.d_pcols ? (const uint32_t *)(p.d_pcols + threadIdx.x) : cw);
+    // prime unconditionally (a wave without payload reads the constant block) so that the compiler
+    // counts the ring loads exactly instead of draining them before the LDS build
+    BGroup r0, r1, r2;
+    {
+        Tile dz{};
+        dz.vbase = (uint64_t)p.d_kvals;  // 13 KiB: two groups of this lane's words stay inside
+        const Tile &d0 = any ? df : dz;
+        braid_load(r0, d0, any ? gf : 0u, lane);
+        if (any) pf_advance();
+        braid_load(r1, any ? df : dz, any ? gf : 1u, lane);
+        if (any) pf_advance();
+    }
+    {
+        const uint32_t i = threadIdx.x, k = i >> 8, e = i & 255u;
+        const uint32_t base = ((k >> 1) << 16) | (e << 8) | ((k & 1) << 7);
+        const uint4 vv = make_uint4(te, te, te, te);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *(uint4 *)(lds + base + ((j + i) & 7u) * 16) = vv;  // rotated: spread banks
+        *(uint64_t *)(lds + kTabBytes + 8 * i) = kq;
+        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = t0e;
+        *(uint32_t *)(lds + kPcolOff + 4 * i) = pce;
+    }
+    // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched groups
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    if (t0 >= t1) return;
+
+    // ---- scan cursor
+    Walker wp = w0;
+    uint64_t tp = t0;
+    uint32_t gp = 0;
+    Tile dp = make_tile(p, tp, wp);
+    uint32_t s_h = dp.k == 0 ? head_state(p, dp, eng) : 0u;
+    uint32_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
+    BPending pd{};
+    pd.valid = false;
+    BGroupAcc acc{};
+    acc.slot = ~0ull;
+
+    auto settle = [&]() -> bool {
+        while (gp >= dp.ngroups) {
+            braid_finish(p, dp, u, s_h, eng, lane, acc, pd);
+            if (++tp >= t1) return false;
+            dp = make_tile(p, tp, wp);
+            gp = 0;
+            s_h = dp.k == 0 ? head_state(p, dp, eng) : 0u;
+            u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
+        }
+        return true;
+    };
+
+    if (any) {
+        // three-slot ring, prefetch distance two groups (32 dword loads in flight per lane)
+        for (;;) {
+            braid_load(r2, df, gf, lane);
+            pf_advance();
+            if (!settle()) break;
+            u = braid_proc(u, r0, eng, dp, gp++, lane, s_h);
+
+            braid_load(r0, df, gf, lane);
+            pf_advance();
+            if (!settle()) break;
+            u = braid_proc(u, r1, eng, dp, gp++, lane, s_h);
+
+            braid_load(r1, df, gf, lane);
+            pf_advance();
+            if (!settle()) break;
+            u = braid_proc(u, r2, eng, dp, gp++, lane, s_h);
+        }
+    } else {
+        settle();
+    }
+    braid_publish(p, acc, pd, eng, lane);
+    braid_resolve(p, pd, eng, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -693,8 +1065,8 @@ extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stre
 extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     switch (alg) {
-        case ALG_CRC32: hipLaunchKernelGGL(crc_scan_kernel<ALG_CRC32>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
-        case ALG_CRC32C: hipLaunchKernelGGL(crc_scan_kernel<ALG_CRC32C>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
+        case ALG_CRC32: hipLaunchKernelGGL(crc32_braid_kernel<kPoly32>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
+        case ALG_CRC32C: hipLaunchKernelGGL(crc32_braid_kernel<kPoly32C>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
         case ALG_CRC64NVME: hipLaunchKernelGGL(crc_scan_kernel<ALG_CRC64NVME>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
         default: return -1;
     }

@@ -50,9 +50,10 @@ struct DevBuf {
 // Per-stream cross-tile workspace.  Kernels on one stream are serialised, and each launch leaves
 // the words it touched at zero, so a workspace is reusable by the next launch on its stream.
 struct Workspace {
-    unsigned long long *acc = nullptr;
-    unsigned int *cnt = nullptr;
-    size_t cap = 0;
+    unsigned long long *acc = nullptr;   // per buffer
+    unsigned int *cnt = nullptr;         // per buffer
+    unsigned long long *acc1 = nullptr;  // per tile (W=32 group slots)
+    size_t cap = 0, cap_tiles = 0;
 };
 
 struct Device {
@@ -60,6 +61,7 @@ struct Device {
     int cus = 0;
     std::mutex mu;
     std::map<std::pair<int, uint32_t>, DevBuf> kvals;           // (alg, seg) -> 64 x u64
+    std::map<int, DevBuf> braid;                                // alg -> W=32 braided-scan constants
     std::map<std::pair<int, uint64_t>, DevBuf> pcols;           // (alg, tile) -> tmax x W x u64
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
     std::map<hipStream_t, Workspace> ws;
@@ -153,6 +155,37 @@ int get_kvals(Device *d, int alg, uint32_t seg, const uint64_t **out) {
     return 0;
 }
 
+// x^-1 * t : inverse of gf2_mulx (the reflected polynomial's top bit is the x^0 coefficient, 1)
+inline uint32_t inv_mulx32(uint32_t t, uint32_t poly) { return (t & 0x80000000u) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
+
+// W=32 braided-scan constants (layout: engine.h kBraidConstWords)
+int get_braid_consts(Device *d, int alg, const uint64_t **out) {
+    auto it = d->braid.find(alg);
+    if (it == d->braid.end()) {
+        const uint32_t poly = (uint32_t)alg_poly(alg);
+        std::vector<uint32_t> c(kBraidConstWords, 0);
+        uint32_t kl = 0x80000000u;  // x^0, then x^(-32 l)
+        for (int l = 0; l < 64; ++l) {
+            uint32_t col = kl;
+            for (int j = 0; j < 32; ++j) {
+                c[((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
+                col = (uint32_t)gf2_mulx(col, poly);
+            }
+            for (int i = 0; i < 32; ++i) kl = inv_mulx32(kl, poly);
+        }
+        const uint64_t skip = gf2_xpow8n(kBraidRow - 4, poly, 32);
+        for (int i = 0; i < 1024; ++i)
+            c[2048 + i] = (uint32_t)gf2_mulmod(gf2_table_entry(i & 255, i >> 8, poly), skip, poly, 32);
+        for (int e = 0; e < 256; ++e) c[3072 + e] = (uint32_t)gf2_table_entry(e, 0, poly);
+        DevBuf b;
+        int rc = upload(b, c.data(), c.size() * 4);
+        if (rc) return rc;
+        it = d->braid.emplace(alg, b).first;
+    }
+    *out = (const uint64_t *)it->second.p;
+    return 0;
+}
+
 // column j of P_k = x^(8*tile*k) * x^j, k < tmax : moves tile k's partial to its buffer end
 int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t **out) {
     auto key = std::make_pair(alg, tile);
@@ -190,8 +223,20 @@ int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t *
     return 0;
 }
 
-int get_workspace(Device *d, hipStream_t s, size_t nbuf, Workspace **out) {
+int get_workspace(Device *d, hipStream_t s, size_t nbuf, size_t ntiles, Workspace **out) {
     Workspace &w = d->ws[s];
+    if (w.cap_tiles < ntiles) {
+        size_t cap = std::max<size_t>(ntiles, w.cap_tiles * 2);
+        if (w.acc1) {
+            HIP_TRY(hipStreamSynchronize(s));
+            (void)hipFree(w.acc1);
+            w.acc1 = nullptr;
+        }
+        HIP_TRY(hipMalloc((void **)&w.acc1, cap * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(w.acc1, 0, cap * sizeof(unsigned long long)));
+        HIP_TRY(hipDeviceSynchronize());
+        w.cap_tiles = cap;
+    }
     if (w.cap < nbuf) {
         size_t cap = std::max<size_t>(nbuf, w.cap * 2);
         if (w.acc) {
@@ -237,21 +282,33 @@ int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("hash kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
 
+uint32_t debug_flags() {
+    static const uint32_t f = [] {
+        const char *e = std::getenv("AMDCRC_DEBUG");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+    }();
+    return f;
+}
+
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, hipStream_t s) {
+    p.dbg = debug_flags();
     const uint64_t tile = (uint64_t)p.seg * kWave;
-    int rc = get_kvals(d, alg, p.seg, &p.d_kvals);
+    const bool braided = width_of(alg) == 32;
+    int rc = braided ? get_braid_consts(d, alg, &p.d_kvals) : get_kvals(d, alg, p.seg, &p.d_kvals);
     if (rc) return rc;
     p.d_pcols = nullptr;
     p.pcols_tmax = 0;
     p.d_acc = nullptr;
     p.d_cnt = nullptr;
+    p.d_acc1 = nullptr;
     if (tmax > 1) {
         if ((rc = get_pcols(d, alg, tile, tmax, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
         Workspace *w;
-        if ((rc = get_workspace(d, s, nbuf, &w))) return rc;
+        if ((rc = get_workspace(d, s, nbuf, braided ? p.ntiles : 0, &w))) return rc;
         p.d_acc = w->acc;
         p.d_cnt = w->cnt;
+        p.d_acc1 = w->acc1;
     }
     const uint64_t waves = p.ntiles;
     uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;

@@ -38,13 +38,25 @@ struct ScanParams {
     // ---- geometry and constants
     uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
     uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
+    uint32_t dbg;                  // diagnostics only (AMDCRC_DEBUG): bit0 skip tile finish, bit1 skip cross-tile combine
+    uint32_t pad0;
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;
     // ---- cross-tile combine workspace (zero on entry, left zero on exit)
     unsigned long long *d_acc;     // per buffer
     unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
+    unsigned long long *d_acc1;    // W=32 braided scan: per tile (slot of each 32-tile group)
 };
+
+// W=32 braided scan constants (engine.cpp get_braid_consts), u32 words:
+//   [0, 2048)     K-matrix image: columns of K_l = x^(-32 l), [j/4][lane][j%4]
+//   [2048, 3072)  T'_k[e] = e * x^(8(k+1) + 8*252): slice-by-4 step that also skips the other
+//                 63 lanes' words of a 256-byte row
+//   [3072, 3328)  T_0[e] = e * x^8: plain byte step for head / tail bytes
+constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
+constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
+constexpr int kBraidConstWords = 3328;
 
 struct XxhParams {
     const uint64_t *d_ptrs;  // device addresses (list) or null (strided)

@@ -1,0 +1,177 @@
+"""CPU: a Python model of the W=32 braided scan (crc_kernels.hip crc32_braid_kernel), checked
+against the oracle.  It restates the kernel's algebra independently of the C++ host code:
+
+  * rows of 256 bytes; lane l owns the 4-byte word at 4l of every row;
+  * braid step u <- T'(u ^ w) with T'_k[e] = e * x^(8(k+1)) * x^(8*252) (slice-by-4 plus the skip
+    over the other 63 lanes' words);
+  * lane share u * K_l, K_l = x^(-32 l) (x^-1 by inverting the reflected multiply-by-x);
+  * head state injected at virtual offset `pad` of the front-padded first tile;
+  * tiles in groups of 32: a tile moves to its group end (x^(8*TILE*m), m < 32), a group to the
+    buffer end (x^(8*TILE*(T - group_end))).
+
+Rows per tile R is a free parameter here (the kernel uses multiples of 16), so small buffers
+already exercise multi-group buffers.  A failure here is a design bug, not a kernel bug.
+"""
+import random
+
+import pytest
+
+from oracle import oracle
+
+POLY = {"crc32": 0xEDB88320, "crc32c": 0x82F63B78}
+M32 = 0xFFFFFFFF
+ROW = 256
+
+
+def mulx(v, P):
+    return (v >> 1) ^ (P if v & 1 else 0)
+
+
+def inv_mulx(t, P):
+    return ((((t ^ P) << 1) | 1) & M32) if t & 0x80000000 else (t << 1) & M32
+
+
+def mulmod(a, b, P):
+    m, p = 0x80000000, 0
+    while m:
+        if a & m:
+            p ^= b
+        m >>= 1
+        b = mulx(b, P)
+    return p
+
+
+def xpow8n(n, P):
+    r, sq = 0x80000000, 0x00800000  # x^0, x^8
+    while n:
+        if n & 1:
+            r = mulmod(r, sq, P)
+        sq = mulmod(sq, sq, P)
+        n >>= 1
+    return r
+
+
+def table_entry(e, k, P):
+    c = e
+    for _ in range(8 * (k + 1)):
+        c = mulx(c, P)
+    return c
+
+
+class Braid:
+    def __init__(self, alg):
+        P = self.P = POLY[alg]
+        skip = xpow8n(ROW - 4, P)
+        self.Tp = [[mulmod(table_entry(e, k, P), skip, P) for e in range(256)] for k in range(4)]
+        self.T0 = [table_entry(e, 0, P) for e in range(256)]
+        self.K = []
+        kl = 0x80000000
+        for _ in range(64):
+            self.K.append(kl)
+            for _ in range(32):
+                kl = inv_mulx(kl, P)
+
+    def step(self, a):
+        T = self.Tp
+        return T[3][a & 255] ^ T[2][(a >> 8) & 255] ^ T[1][(a >> 16) & 255] ^ T[0][a >> 24]
+
+    def byte(self, s, b):
+        return (s >> 8) ^ self.T0[(s ^ b) & 255]
+
+    def bytes_(self, s, data):
+        for b in data:
+            s = self.byte(s, b)
+        return s
+
+
+def braid_model(br: Braid, data: bytes, addr: int, seed: int, rows: int) -> int:
+    P = br.P
+    n = len(data)
+    ptr, end = addr, addr + n
+    H, Ea = (ptr + 15) & ~15, end & ~15
+    if Ea > H:
+        mainlen, headend, tail = Ea - H, H, Ea
+    else:
+        mainlen, headend, tail = 0, end, end
+    tile = ROW * rows
+    T = -(-mainlen // tile) if mainlen else 1
+    pad = T * tile - mainlen
+    s_h = br.bytes_(~seed & M32, data[: headend - ptr])
+    groups = {}
+    fin = None
+    for k in range(T):
+        r = 0
+        if mainlen:
+            vbase = (H - ptr) - pad + k * tile  # data offset of the tile's virtual byte 0
+            for lane in range(64):
+                u = s_h if (k == 0 and pad == 0 and lane == 0) else 0
+                for c in range(rows):
+                    vo = ROW * c + 4 * lane
+                    if k == 0 and pad and vo < pad:
+                        w = 0
+                    else:
+                        w = int.from_bytes(data[vbase + vo: vbase + vo + 4], "little")
+                    if k == 0 and pad and vo == pad:
+                        w ^= s_h
+                    u = br.step(u ^ w)
+                r ^= mulmod(u, br.K[lane], P)
+        if T == 1:
+            fin = r if mainlen else s_h
+        else:
+            g0 = k & ~31
+            gend = min(g0 + 32, T)
+            groups[g0] = groups.get(g0, 0) ^ mulmod(r, xpow8n(tile * (gend - 1 - k), P), P)
+    if T > 1:
+        fin = 0
+        for g0, v in groups.items():
+            gend = min(g0 + 32, T)
+            fin ^= mulmod(v, xpow8n(tile * (T - gend), P), P)
+    fin = br.bytes_(fin, data[tail - ptr:])
+    return ~fin & M32
+
+
+@pytest.fixture(scope="module", params=["crc32", "crc32c"])
+def braid(request):
+    return request.param, Braid(request.param)
+
+
+def test_inverse_x(braid):
+    alg, br = braid
+    for l in range(64):
+        # K_l * x^(32 l) == 1
+        assert mulmod(br.K[l], xpow8n(4 * l, br.P), br.P) == 0x80000000
+
+
+def test_column_multiply_matches_mulmod(braid):
+    """mul_pcols / the LDS column select: bit (31-j) of r picks column j = X * x^j."""
+    alg, br = braid
+    rnd = random.Random(5)
+    for _ in range(20):
+        X, r = rnd.getrandbits(32), rnd.getrandbits(32)
+        cols, c = [], X
+        for _ in range(32):
+            cols.append(c)
+            c = mulx(c, br.P)
+        acc = 0
+        for j in range(32):
+            if (r >> (31 - j)) & 1:
+                acc ^= cols[j]
+        assert acc == mulmod(r, X, br.P)
+
+
+@pytest.mark.parametrize("rows", [1, 2, 16])
+def test_braid_model_vs_oracle(braid, rows):
+    alg, br = braid
+    rnd = random.Random(hash((alg, rows)) & 0xFFFF)
+    tile = ROW * rows
+    sizes = [0, 1, 15, 16, 17, 255, 256, 4096, tile - 16, tile, tile + 16, 3 * tile + 7, 33 * tile + 48,
+             70 * tile - 32]
+    for n in sizes:
+        for misalign in (0, 3, 9):
+            if n > 20000 and misalign:
+                continue
+            data = bytes(rnd.getrandbits(8) for _ in range(n))
+            seed = rnd.choice([0, rnd.getrandbits(32)])
+            want = oracle.crc(alg, data, seed)
+            got = braid_model(br, data, 0x1000 + misalign, seed, rows)
+            assert got == want, (alg, rows, n, misalign, hex(seed))
