@@ -204,14 +204,18 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 
 // Scalar (SMEM) loads of wave-uniform descriptor words: they retire on lgkmcnt, so waiting for them
 // never drains the vector-memory queue holding the prefetched payload groups.
+// The address is wave-uniform by construction; readfirstlane keeps it in SGPRs even where the
+// compiler cannot prove uniformity (an "s" operand in a VGPR does not assemble).
 __device__ __forceinline__ uint64_t sload64(const void *a) {
     uint64_t v;
-    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+    const uint64_t sa = rfl64((uint64_t)a);
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(sa) : "memory");
     return v;
 }
 __device__ __forceinline__ uint32_t sload32(const void *a) {
     uint32_t v;
-    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+    const uint64_t sa = rfl64((uint64_t)a);
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(sa) : "memory");
     return v;
 }
 
@@ -337,7 +341,8 @@ template <class E>
 __device__ __forceinline__ typename E::T fold_bytes(typename E::T s, uint64_t a, uint64_t end, const E &eng) {
     for (uint64_t blk = a & ~15ull; blk < end; blk += 16) {
         v4u w;
-        asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(blk) : "memory");
+        const uint64_t sblk = rfl64(blk);
+        asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w) : "s"(sblk) : "memory");
         const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
         const uint64_t lo = a > blk ? a : blk, hi = end < blk + 16 ? end : blk + 16;
         for (uint64_t x = lo; x < hi; ++x) {
@@ -368,6 +373,7 @@ __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
 #pragma unroll
     for (int c = 0; c < W; c += 8) {
         uint64_t k0, k1, k2, k3, k4, k5, k6, k7;
+        const uint64_t a = rfl64((uint64_t)(cols + c));  // the table address must live in SGPRs
         asm volatile(
             "s_load_dwordx2 %0, %8, 0x0\n\ts_load_dwordx2 %1, %8, 0x8\n\t"
             "s_load_dwordx2 %2, %8, 0x10\n\ts_load_dwordx2 %3, %8, 0x18\n\t"
@@ -376,7 +382,7 @@ __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
             "s_waitcnt lgkmcnt(0)"
             // early-clobber: a returning load must never overwrite the shared address operand
             : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
-            : "s"(cols + c)
+            : "s"(a)
             : "memory");
         const uint64_t k[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
 #pragma unroll
@@ -401,7 +407,7 @@ __device__ __forceinline__ unsigned long long atomic_xor_ret(unsigned long long 
 }
 
 template <class E>
-__device__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, uint64_t tail, uint32_t tail_len, const E &eng) {
+__device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, uint64_t tail, uint32_t tail_len, const E &eng) {
     if (tail_len) fin = fold_bytes(fin, tail, tail + tail_len, eng);
     fin = ~fin;
     if (E::W == 32)
@@ -411,7 +417,7 @@ __device__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, uin
 }
 
 template <class E>
-__device__ void resolve(const ScanParams &p, Pending &pd, const E &eng, int lane) {
+__device__ __forceinline__ void resolve(const ScanParams &p, Pending &pd, const E &eng, int lane) {
     using T = typename E::T;
     if (!pd.valid) return;
     pd.valid = false;
@@ -426,7 +432,7 @@ __device__ void resolve(const ScanParams &p, Pending &pd, const E &eng, int lane
 }
 
 template <class E>
-__device__ void finish_tile(const ScanParams &p, const Tile &d, typename E::T s, typename E::T s_h, const E &eng,
+__device__ __forceinline__ void finish_tile(const ScanParams &p, const Tile &d, typename E::T s, typename E::T s_h, const E &eng,
                             int lane, Pending &pd) {
     using T = typename E::T;
     constexpr int W = E::W;
@@ -639,7 +645,7 @@ __device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
                       __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
 }
 
-template <uint32_t POLY>
+template <uint32_t POLY, bool BITOP3 = true>
 struct Braid32 {
     using T = uint32_t;
     static constexpr int W = 32;
@@ -668,6 +674,7 @@ struct Braid32 {
     __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
         uint32_t l3, l2, l1, l0;
         look(a, l3, l2, l1, l0);
+        if (!BITOP3) return l3 ^ l2 ^ l1 ^ l0 ^ wn;
         return xor3(xor3(l3, l2, wn), l1, l0);
     }
     // plain byte step for head / tail bytes (s is wave-uniform: broadcast reads)
@@ -698,15 +705,22 @@ struct BGroup {
 // and are zeroed by braid_proc.
 __device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi, int lane) {
     const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
+    // rows go out in order on every path (scheduling barriers), as in braid_fused: the compiler's
+    // vmcnt bookkeeping merges paths, and one path with row 0 issued late would make every wait
+    // for row 0 drain the whole group
     if (d.pad == 0) {
         const uint64_t a = d.vbase + vo0;
 #pragma unroll
-        for (int r = 0; r < kBraidRowsPerGroup; ++r) g.w[r] = *(gu32 *)(a + kBraidRow * r);
+        for (int r = 0; r < kBraidRowsPerGroup; ++r) {
+            g.w[r] = *(gu32 *)(a + kBraidRow * r);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     } else {
 #pragma unroll
         for (int r = 0; r < kBraidRowsPerGroup; ++r) {
             const uint32_t vo = vo0 + kBraidRow * r;
             g.w[r] = *(gu32 *)(vo >= d.pad ? d.vbase + vo : d.H);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -731,6 +745,28 @@ __device__ __forceinline__ uint32_t braid_proc(uint32_t u, const BGroup &g, cons
     return u;
 }
 
+// Steady state (neither the scanned nor the prefetched group in a front-padded tile): scan group g
+// while issuing group g+1's loads, RATE per table step.  Issue and scan share one basic block and a
+// scheduling barrier after every step, so the loads stream out between the table steps instead of in
+// a 16-load burst per wave (measured: a burst-issue loop is 20 % slower at the same work).  With two
+// ring slots the other slot's loads are always the youngest in flight at every loop point, which
+// keeps the compiler's vmcnt bookkeeping exact across the loop.
+template <int RATE, class B>
+__device__ __forceinline__ uint32_t braid_fused(uint32_t u, const BGroup &g, BGroup &dst, uint64_t a, const B &eng) {
+    uint32_t x = u ^ g.w[0];
+#pragma unroll
+    for (int st = 0; st < kBraidRowsPerGroup; ++st) {
+#pragma unroll
+        for (int q = 0; q < RATE; ++q) {
+            const int r = RATE * st + q;
+            if (r < kBraidRowsPerGroup) dst.w[r] = *(gu32 *)(a + kBraidRow * r);
+        }
+        x = st + 1 < kBraidRowsPerGroup ? eng.step_x(x, g.w[st + 1]) : eng.step(x);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return x;
+}
+
 // Cross-tile combine.  Tiles form groups of 32; tile k's register is moved to its group's end
 // (r * x^(8*TILE*m), m < 32: columns in LDS, one per lane).  A wave merges the shares of its own
 // consecutive tiles of one group in registers {arrival bits | XOR} and publishes them with one
@@ -752,7 +788,7 @@ struct BPending {
 };
 
 template <class B>
-__device__ void braid_resolve(const ScanParams &p, BPending &pd, const B &eng, int lane) {
+__device__ __forceinline__ void braid_resolve(const ScanParams &p, BPending &pd, const B &eng, int lane) {
     if (!pd.valid) return;
     pd.valid = false;
     const unsigned long long now = rfl64(pd.old) ^ pd.val;
@@ -779,7 +815,7 @@ __device__ void braid_resolve(const ScanParams &p, BPending &pd, const B &eng, i
 }
 
 template <class B>
-__device__ void braid_publish(const ScanParams &p, BGroupAcc &acc, BPending &pd, const B &eng, int lane) {
+__device__ __forceinline__ void braid_publish(const ScanParams &p, BGroupAcc &acc, BPending &pd, const B &eng, int lane) {
     if (acc.slot == ~0ull) return;
     braid_resolve(p, pd, eng, lane);
     unsigned long long old = 0;
@@ -792,7 +828,7 @@ __device__ void braid_publish(const ScanParams &p, BGroupAcc &acc, BPending &pd,
 }
 
 template <class B>
-__device__ void braid_finish(const ScanParams &p, const Tile &d, uint32_t u, uint32_t s_h, const B &eng, int lane,
+__device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d, uint32_t u, uint32_t s_h, const B &eng, int lane,
                              BGroupAcc &acc, BPending &pd) {
     if (p.dbg & 1) {  // timing experiments only (AMDCRC_DEBUG): results are invalid
         if (lane == 0) ((uint32_t *)p.d_out)[d.b] = u;
@@ -824,9 +860,9 @@ __device__ void braid_finish(const ScanParams &p, const Tile &d, uint32_t u, uin
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY>
+template <uint32_t POLY, bool BITOP3 = true, int RATE = 1>
 __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams p) {
-    using B = Braid32<POLY>;
+    using B = Braid32<POLY, BITOP3>;
     __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
 
     const int lane = threadIdx.x & 63;
@@ -883,14 +919,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     const uint32_t pce = *(gu32 *)(p.d_pcols ? (const uint32_t *)(p.d_pcols + threadIdx.x) : cw);
     // prime unconditionally (a wave without payload reads the constant block) so that the compiler
     // counts the ring loads exactly instead of draining them before the LDS build
-    BGroup r0, r1, r2;
+    BGroup r0, r1;
     {
         Tile dz{};
-        dz.vbase = (uint64_t)p.d_kvals;  // 13 KiB: two groups of this lane's words stay inside
-        const Tile &d0 = any ? df : dz;
-        braid_load(r0, d0, any ? gf : 0u, lane);
-        if (any) pf_advance();
-        braid_load(r1, any ? df : dz, any ? gf : 1u, lane);
+        dz.vbase = (uint64_t)p.d_kvals;  // 13 KiB: one group of this lane's words stays inside
+        braid_load(r0, any ? df : dz, any ? gf : 0u, lane);
         if (any) pf_advance();
     }
     {
@@ -933,23 +966,24 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
         return true;
     };
 
+    // one ring step: scan `cur` (group gp of tile dp) and load `dst` with the prefetch cursor's group
+    auto ring_step = [&](const BGroup &cur, BGroup &dst) {
+        if (dp.pad == 0 && df.pad == 0) {
+            u = braid_fused<RATE>(u, cur, dst, df.vbase + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
+        } else {
+            braid_load(dst, df, gf, lane);
+            u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
+        }
+        ++gp;
+        pf_advance();
+    };
     if (any) {
-        // three-slot ring, prefetch distance two groups (32 dword loads in flight per lane)
+        // two-slot ring: group g+1's loads stream out while group g is scanned
         for (;;) {
-            braid_load(r2, df, gf, lane);
-            pf_advance();
             if (!settle()) break;
-            u = braid_proc(u, r0, eng, dp, gp++, lane, s_h);
-
-            braid_load(r0, df, gf, lane);
-            pf_advance();
+            ring_step(r0, r1);
             if (!settle()) break;
-            u = braid_proc(u, r1, eng, dp, gp++, lane, s_h);
-
-            braid_load(r1, df, gf, lane);
-            pf_advance();
-            if (!settle()) break;
-            u = braid_proc(u, r2, eng, dp, gp++, lane, s_h);
+            ring_step(r1, r0);
         }
     } else {
         settle();
@@ -1066,7 +1100,14 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     hipStream_t s = (hipStream_t)stream;
     switch (alg) {
         case ALG_CRC32: hipLaunchKernelGGL(crc32_braid_kernel<kPoly32>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
-        case ALG_CRC32C: hipLaunchKernelGGL(crc32_braid_kernel<kPoly32C>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
+        case ALG_CRC32C:
+            if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
+                hipLaunchKernelGGL((crc32_braid_kernel<kPoly32C, false>), dim3(nblocks), dim3(kBlock), 0, s, *p);
+            else if (p->dbg & 8)  // diagnostics: two loads per table step (front-loaded issue)
+                hipLaunchKernelGGL((crc32_braid_kernel<kPoly32C, true, 2>), dim3(nblocks), dim3(kBlock), 0, s, *p);
+            else
+                hipLaunchKernelGGL(crc32_braid_kernel<kPoly32C>, dim3(nblocks), dim3(kBlock), 0, s, *p);
+            break;
         case ALG_CRC64NVME: hipLaunchKernelGGL(crc_scan_kernel<ALG_CRC64NVME>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
         default: return -1;
     }

@@ -107,13 +107,15 @@ __global__ __launch_bounds__(1024, 4) void k(const uint8_t *base, uint64_t bytes
         for (int i = 0; i < 4; ++i) r[i] = *(gv4u *)(a + (SEGL > 0 ? 16 : 1024) * i);
     };
     auto proc = [&](const v4u (&r)[4], uint64_t g) {
-        if (MODE == 4 || MODE == 5) {
+        if (MODE == 6) asm volatile("" ::: "memory");  // burst: no load may move into the CRC steps
+        if (MODE == 4 || MODE == 5 || MODE == 6) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 s = crcw<MODE == 5>(s, r[i].x, lds, srcA, srcB);
                 s = crcw<MODE == 5>(s, r[i].y, lds, srcA, srcB);
                 s = crcw<MODE == 5>(s, r[i].z, lds, srcA, srcB);
                 s = crcw<MODE == 5>(s, r[i].w, lds, srcA, srcB);
+                if (MODE == 6 && i == 3) asm volatile("" ::: "memory");
             }
             return;
         }
@@ -232,6 +234,7 @@ int main(int argc, char **argv) {
         run<4, 0>("R coalesced (braid timing)", d, bytes, rotate, out, clk, cus);
         run<1, -1>("M dword braid rows", d, bytes, rotate, out, clk, cus);
         run<4, -1>("R dword braid rows", d, bytes, rotate, out, clk, cus);
+        run<6, -1>("R dword braid, burst issue", d, bytes, rotate, out, clk, cus);
     }
     return 0;
 }
