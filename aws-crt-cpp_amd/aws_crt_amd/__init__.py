@@ -46,6 +46,8 @@ def lib() -> ctypes.CDLL:
         L.aws_crt_amd_checksum_list.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp, vp]
         L.aws_crt_amd_checksum_host.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp]
         L.aws_crt_amd_crc_combine_batch.argtypes = [ctypes.c_int, vp, vp, ctypes.POINTER(u64), sz, vp, vp]
+        L.aws_crt_amd_multipart_crc.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp,
+                                                ctypes.c_char_p, vp]
         for name, rt, st in (("crc32", u32, u32), ("crc32c", u32, u32), ("crc64nvme", u64, u64)):
             f = getattr(L, f"aws_checksums_{name}_ex")
             f.restype, f.argtypes = rt, [vp, sz, st]
@@ -124,6 +126,30 @@ def combine_batch(alg: int, crc1, crc2, len2: Sequence[int], out=None, stream=No
     _check(lib().aws_crt_amd_crc_combine_batch(alg, crc1.data_ptr(), crc2.data_ptr(), L2, n, out.data_ptr(),
                                                _stream_handle(stream)))
     return out
+
+
+def multipart_crc(alg: int, parts, stream=None):
+    """S3 multipart composition (checksums_batch.h aws_crt_amd_multipart_crc): `parts` are device
+    buffers in object order -- torch uint8 tensors or (address, length) pairs.  Returns
+    (part checksums, full-object checksum, its base64 wire form)."""
+    ptrs, lens = [], []
+    for p in parts:
+        if hasattr(p, "data_ptr"):
+            ptrs.append(p.data_ptr())
+            lens.append(p.numel() * p.element_size())
+        else:
+            ptrs.append(int(p[0]))
+            lens.append(int(p[1]))
+    n = len(ptrs)
+    wide = alg == CRC64NVME
+    part_out = (ctypes.c_uint64 * max(n, 1))() if wide else (ctypes.c_uint32 * max(n, 1))()
+    obj = ctypes.c_uint64(0) if wide else ctypes.c_uint32(0)
+    b64 = ctypes.create_string_buffer(16)
+    P = (ctypes.c_void_p * max(n, 1))(*ptrs)
+    Ls = (ctypes.c_size_t * max(n, 1))(*lens)
+    _check(lib().aws_crt_amd_multipart_crc(alg, P, Ls, n, ctypes.addressof(part_out), ctypes.addressof(obj), b64,
+                                           _stream_handle(stream)))
+    return [int(part_out[i]) for i in range(n)], int(obj.value), b64.value.decode()
 
 
 def checksum_host(alg: int, buffers: Sequence[bytes], seeds: Optional[Sequence[int]] = None):

@@ -869,6 +869,12 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
+    // diagnostics: per-wave timeline (start, tables built, scan done, exit) on the 100 MHz clock
+    const bool stamps = p.d_timeline != nullptr;
+    auto stamp = [&](int i) {
+        if (stamps && lane == 0) p.d_timeline[gw * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
     Walker w0{0, 0, 0};
     if (p.list_mode && t0 < t1) {
@@ -940,6 +946,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
+    stamp(1);
     if (t0 >= t1) return;
 
     // ---- scan cursor
@@ -988,8 +995,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     } else {
         settle();
     }
+    stamp(2);
     braid_publish(p, acc, pd, eng, lane);
     braid_resolve(p, pd, eng, lane);
+    stamp(3);
 }
 
 // ------------------------------------------------------------------------------------------

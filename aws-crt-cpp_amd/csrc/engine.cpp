@@ -19,6 +19,8 @@
 #include <tuple>
 #include <vector>
 
+#include <aws/crt/Types.h>
+
 #include "engine.h"
 #include "gf2.h"
 
@@ -290,8 +292,25 @@ uint32_t debug_flags() {
     return f;
 }
 
+// Diagnostics only (AMDCRC_DEBUG bit 4): per-wave timeline of the last braided scan launch.
+struct Timeline {
+    unsigned long long *d = nullptr;
+    size_t cap = 0, waves = 0;
+} g_timeline;
+
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, hipStream_t s) {
     p.dbg = debug_flags();
+    p.d_timeline = nullptr;
+    if (p.dbg & 16) {
+        const size_t waves = (size_t)d->cus * kWavesPerBlock;
+        if (g_timeline.cap < waves) {
+            if (g_timeline.d) (void)hipFree(g_timeline.d);
+            HIP_TRY(hipMalloc((void **)&g_timeline.d, waves * 4 * sizeof(unsigned long long)));
+            g_timeline.cap = waves;
+        }
+        g_timeline.waves = waves;
+        p.d_timeline = g_timeline.d;
+    }
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const bool braided = width_of(alg) == 32;
     int rc = braided ? get_braid_consts(d, alg, &p.d_kvals) : get_kvals(d, alg, p.seg, &p.d_kvals);
@@ -588,6 +607,17 @@ AWS_CRT_AMD_API int aws_crt_amd_device_count(void) { return device_count_noinit(
 
 AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void) { return g_last_error.c_str(); }
 
+// Diagnostics (not part of the public headers): copies the per-wave timeline of the last scan
+// launched with AMDCRC_DEBUG bit 4 set -- 4 x u64 s_memrealtime stamps per wave -- after
+// synchronising the device.  Returns the number of waves written.
+AWS_CRT_AMD_API size_t aws_crt_amd_debug_timeline(unsigned long long *h_out, size_t max_waves) {
+    if (!g_timeline.d || !h_out) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return 0;
+    const size_t n = std::min(max_waves, g_timeline.waves);
+    if (hipMemcpy(h_out, g_timeline.d, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return n;
+}
+
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,
                                                  const void *d_seeds, void *d_out, void *hip_stream) {
     if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
@@ -692,6 +722,57 @@ AWS_CRT_AMD_API uint32_t aws_checksums_crc32c_combine(uint32_t crc1, uint32_t cr
 }
 AWS_CRT_AMD_API uint64_t aws_checksums_crc64nvme_combine(uint64_t crc1, uint64_t crc2, uint64_t len2) {
     return gf2_mulmod(crc1, gf2_xpow8n(len2, kPoly64Nvme, 64), kPoly64Nvme, 64) ^ crc2;
+}
+
+// S3 multipart composition (checksums_batch.h): one batched scan over the parts, then the
+// Combine fold of the part values (4/8-byte scalars, no payload) into the full-object checksum.
+AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_parts, const size_t *lens, size_t count,
+                                              void *h_part_out, void *h_object_out, char *b64_out, void *hip_stream) {
+    if (alg < AWS_CRT_AMD_CRC32 || alg > AWS_CRT_AMD_CRC64NVME || !h_object_out || (count && (!d_parts || !lens)))
+        return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "multipart: CRC32/CRC32C/CRC64NVME, parts and an object result");
+    Device *d;
+    int rc = get_device(&d);
+    if (rc) return rc;
+    const int w = width_of(alg);
+    const uint64_t poly = alg_poly(alg);
+    std::vector<uint64_t> part(count, 0);
+    if (count) {
+        const size_t osz = w / 8;
+        void *d_out = nullptr;
+        HIP_TRY(hipMalloc(&d_out, count * osz));
+        hipStream_t s = (hipStream_t)hip_stream;
+        rc = list_impl(d, alg, d_parts, lens, count, nullptr, d_out, s);
+        std::vector<uint8_t> h(count * osz);
+        if (!rc && hipMemcpyAsync(h.data(), d_out, h.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess) {
+            for (size_t i = 0; i < count; ++i)
+                part[i] = w == 64 ? ((const uint64_t *)h.data())[i] : ((const uint32_t *)h.data())[i];
+        } else if (!rc) {
+            rc = fail(AWS_CRT_AMD_ERR_HIP, "multipart: result copy failed");
+        }
+        (void)hipFree(d_out);
+        if (rc) return rc;
+    }
+    uint64_t obj = 0;  // CRC of zero bytes
+    for (size_t i = 0; i < count; ++i)
+        obj = gf2_mulmod(obj, gf2_xpow8n(lens[i], poly, w), poly, w) ^ part[i];
+    for (size_t i = 0; h_part_out && i < count; ++i) {
+        if (w == 64)
+            ((uint64_t *)h_part_out)[i] = part[i];
+        else
+            ((uint32_t *)h_part_out)[i] = (uint32_t)part[i];
+    }
+    if (w == 64)
+        *(uint64_t *)h_object_out = obj;
+    else
+        *(uint32_t *)h_object_out = (uint32_t)obj;
+    if (b64_out) {
+        uint8_t be[8];
+        for (int i = 0; i < w / 8; ++i) be[i] = (uint8_t)(obj >> (w - 8 * (i + 1)));
+        const Aws::Crt::String b64 = Aws::Crt::Base64Encode(aws_byte_cursor_from_array(be, (size_t)(w / 8)));
+        std::memcpy(b64_out, b64.c_str(), b64.size() + 1);
+    }
+    return 0;
 }
 
 // internal: XXH64 of one buffer (host or device memory) for the xxhash ABI (xxhash.cpp)

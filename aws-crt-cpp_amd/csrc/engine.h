@@ -47,6 +47,7 @@ struct ScanParams {
     unsigned long long *d_acc;     // per buffer
     unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
     unsigned long long *d_acc1;    // W=32 braided scan: per tile (slot of each 32-tile group)
+    unsigned long long *d_timeline; // diagnostics (AMDCRC_DEBUG bit 4): 4 s_memrealtime stamps per wave
 };
 
 // W=32 braided scan constants (engine.cpp get_braid_consts), u32 words:

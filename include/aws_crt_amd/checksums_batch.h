@@ -117,6 +117,29 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_host(
     const void *h_seeds,
     void *h_out);
 
+/*
+ * S3 multipart checksum composition (the aws-c-s3 layer the reference's
+ * S3ChecksumConfig selects, S3.cpp:380-428, default CRC64NVME at S3.cpp:31-36).
+ *
+ * `count` device-resident parts, in object order, are checksummed in one batched scan; the part
+ * values are then folded with Combine (CRC.h:41-51) into the FULL_OBJECT checksum, i.e. the CRC of
+ * the parts' concatenation.  Algorithms: CRC32, CRC32C, CRC64NVME.
+ *   h_part_out    host array of `count` results (u32, or u64 for CRC64NVME); may be null
+ *   h_object_out  host u32 / u64: the full-object checksum
+ *   b64_out       optional (may be null): its S3 wire form, base64 of the big-endian bytes
+ *                 (Types.h:70-75), NUL-terminated; needs 13 bytes of room.
+ * Synchronous on hip_stream.  Returns 0 or a negative status.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(
+    int algorithm,
+    const void *const *d_parts,
+    const size_t *lens,
+    size_t count,
+    void *h_part_out,
+    void *h_object_out,
+    char *b64_out,
+    void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

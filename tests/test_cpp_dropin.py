@@ -52,3 +52,13 @@ def test_reference_test_files_run_on_gpu(engine):
     for name in ("CRC32Piping", "CRC32CPiping", "CRC64NVMEPiping", "XXHash64Piping", "XXHash3_64Piping",
                  "XXHash3_128Piping"):
         assert f"[PASS] {name}" in r.stdout, r.stdout
+
+
+def test_types_base64_cpu():
+    """Base64 of the Types surface (Types.h:70-75): the reference's Base64RoundTrip vector
+    (tests/TypesTest.cpp:17-31), RFC 4648 vectors, S3 wire forms of the CRC check values and
+    malformed inputs.  Host code; no device needed."""
+    _make()
+    r = subprocess.run([os.path.join(CPP, "build", "types_tests")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "4 ran, 0 failed" in r.stdout, r.stdout
