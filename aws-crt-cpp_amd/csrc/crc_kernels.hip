@@ -618,7 +618,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p)
 // and wave reduction as the segment kernel, with no extra lookups per byte.
 constexpr uint32_t kT0Off = kTabBytes + kKmatBytes;  // plain byte table (1 KiB; wave-uniform reads)
 constexpr uint32_t kPcolOff = kT0Off + 1024;         // [m < 32][column j] of x^(8*TILE*m) (4 KiB)
-constexpr uint32_t kBraidLds = kPcolOff + 4096;
+constexpr uint32_t kConstFlagOff = kPcolOff + 4096;   // waves that have published their K / P words
+constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 typedef __attribute__((address_space(1))) const uint64_t gu64;
@@ -643,6 +644,33 @@ __device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
     return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
                       __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
+}
+
+// Compile-time GF(2) bases of the braided scan's byte tables: entry e of a table is the XOR of the
+// basis values of e's set bits (the tables are linear in e), so the tables are built from
+// immediates with no memory traffic -- at launch the constant block is usually evicted by the
+// previous launch's stream and would take several microseconds to arrive.
+//   b[k][i] = T'_k[1 << i] = (1 << i) * x^(8(k+1)) * x^(8*252)     (k < 4)
+//   b[4][i] = T_0[1 << i]  = (1 << i) * x^8
+template <uint32_t POLY>
+struct BraidBasis {
+    uint32_t b[5][8];
+    constexpr BraidBasis() : b() {
+        const uint64_t skip = gf2_xpow8n(kBraidRow - 4, POLY, 32);
+        for (int i = 0; i < 8; ++i) {
+            for (int k = 0; k < 4; ++k) b[k][i] = (uint32_t)gf2_mulmod(gf2_table_entry(1u << i, k, POLY), skip, POLY, 32);
+            b[4][i] = (uint32_t)gf2_table_entry(1u << i, 0, POLY);
+        }
+    }
+};
+
+template <uint32_t POLY, int K>
+__device__ __forceinline__ uint32_t basis_entry(uint32_t e) {
+    constexpr BraidBasis<POLY> B{};
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0u;
+    return v;
 }
 
 template <uint32_t POLY, bool BITOP3 = true>
@@ -722,6 +750,18 @@ __device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi
             g.w[r] = *(gu32 *)(vo >= d.pad ? d.vbase + vo : d.H);
             __builtin_amdgcn_sched_barrier(0);
         }
+    }
+}
+
+// Prologue loads: one code path for padded and unpadded tiles (a per-row address select), so the
+// compiler sees a single load sequence and waits only for the constants before the LDS build.
+__device__ __forceinline__ void braid_prime(BGroup &g, uint64_t vbase, uint64_t H, uint32_t pad, uint32_t gi, int lane) {
+    const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
+#pragma unroll
+    for (int r = 0; r < kBraidRowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kBraidRow * r;
+        g.w[r] = *(gu32 *)(vo >= pad ? vbase + vo : H);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -872,7 +912,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     // diagnostics: per-wave timeline (start, tables built, scan done, exit) on the 100 MHz clock
     const bool stamps = p.d_timeline != nullptr;
     auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 4 + i] = __builtin_amdgcn_s_memrealtime();
+        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
     };
     stamp(0);
 
@@ -915,39 +955,70 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
         }
         pf_done = true;
     };
-    // constants (this thread's K-image word, T' entry and T0 entry), then the first two payload
-    // groups, all before the LDS build so their latency overlaps it
-    const uint32_t *cw = (const uint32_t *)p.d_kvals;
+    // K-image word and P column of this thread: needed only when a tile finishes, so they are
+    // published to LDS after the first group is scanned (see publish_consts), not before the scan
     const uint64_t kq = *(gu64 *)(p.d_kvals + threadIdx.x);
-    const uint32_t te = *(gu32 *)(cw + 2048 + threadIdx.x);
-    const uint32_t t0e = *(gu32 *)(cw + 3072 + (threadIdx.x & 255));
-    // P columns m < 32 (the host table always holds at least 64 entries when T > 1)
-    const uint32_t pce = *(gu32 *)(p.d_pcols ? (const uint32_t *)(p.d_pcols + threadIdx.x) : cw);
-    // prime unconditionally (a wave without payload reads the constant block) so that the compiler
-    // counts the ring loads exactly instead of draining them before the LDS build
+    const uint32_t pce = *(gu32 *)(p.d_pcols ? (const uint32_t *)(p.d_pcols + threadIdx.x) : (const uint32_t *)p.d_kvals);
+    // prime two groups unconditionally (a wave without payload reads the constant block) through one
+    // load path, so the LDS build below waits only for the constants, not for the payload
     BGroup r0, r1;
     {
-        Tile dz{};
-        dz.vbase = (uint64_t)p.d_kvals;  // 13 KiB: one group of this lane's words stays inside
-        braid_load(r0, any ? df : dz, any ? gf : 0u, lane);
+        // field-wise selects (selecting whole Tile structs put them in scratch)
+        const uint64_t zb = (uint64_t)p.d_kvals;  // 13 KiB: two groups of this lane's words stay inside
+        const uint64_t vb0 = any ? df.vbase : zb, h0 = any ? df.H : zb;
+        const uint32_t pad0 = any ? df.pad : 0u, g0 = any ? gf : 0u;
         if (any) pf_advance();
+        const uint64_t vb1 = any ? df.vbase : zb, h1 = any ? df.H : zb;
+        const uint32_t pad1 = any ? df.pad : 0u, g1 = any ? gf : 1u;
+        if (any) pf_advance();
+        braid_prime(r0, vb0, h0, pad0, g0, lane);
+        braid_prime(r1, vb1, h1, pad1, g1, lane);
     }
     {
-        const uint32_t i = threadIdx.x, k = i >> 8, e = i & 255u;
+        // T' (1024 entries, 32 copies each) and T0 from the compile-time bases
+        const uint32_t i = threadIdx.x, e = i & 255u;
+        const uint32_t k = __builtin_amdgcn_readfirstlane(i >> 8);  // wave-uniform
+        const uint32_t te = k == 0   ? basis_entry<POLY, 0>(e)
+                            : k == 1 ? basis_entry<POLY, 1>(e)
+                            : k == 2 ? basis_entry<POLY, 2>(e)
+                                     : basis_entry<POLY, 3>(e);
         const uint32_t base = ((k >> 1) << 16) | (e << 8) | ((k & 1) << 7);
         const uint4 vv = make_uint4(te, te, te, te);
 #pragma unroll
         for (int j = 0; j < 8; ++j) *(uint4 *)(lds + base + ((j + i) & 7u) * 16) = vv;  // rotated: spread banks
-        *(uint64_t *)(lds + kTabBytes + 8 * i) = kq;
-        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = t0e;
-        *(uint32_t *)(lds + kPcolOff + 4 * i) = pce;
+        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(e);
+        if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
     }
+    stamp(4);  // constants arrived, LDS stores issued
     // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched groups
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
     stamp(1);
-    if (t0 >= t1) return;
+    // Every wave publishes its 1/16 of the K image and P columns once its constants have arrived
+    // (after its first group, by which time they have: loads retire in order) and counts itself in
+    // LDS; a wave spins on the count only before its first tile finish.  A wave without work
+    // publishes before leaving, so the count always completes.
+    bool consts_ready = false, published = false;
+    auto publish_consts = [&]() {
+        if (published) return;
+        published = true;
+        *(uint64_t *)(lds + kTabBytes + 8 * threadIdx.x) = kq;
+        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto await_consts = [&]() {
+        if (consts_ready) return;
+        while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+               (uint32_t)kWavesPerBlock)
+            __builtin_amdgcn_s_sleep(1);
+        consts_ready = true;
+    };
+    if (t0 >= t1) {
+        publish_consts();
+        return;
+    }
 
     // ---- scan cursor
     Walker wp = w0;
@@ -963,6 +1034,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
 
     auto settle = [&]() -> bool {
         while (gp >= dp.ngroups) {
+            await_consts();
             braid_finish(p, dp, u, s_h, eng, lane, acc, pd);
             if (++tp >= t1) return false;
             dp = make_tile(p, tp, wp);
@@ -985,16 +1057,26 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
         pf_advance();
     };
     if (any) {
-        // two-slot ring: group g+1's loads stream out while group g is scanned
-        for (;;) {
-            if (!settle()) break;
-            ring_step(r0, r1);
-            if (!settle()) break;
-            ring_step(r1, r0);
+        // two-slot ring: group g+1's loads stream out while group g is scanned.  Both slots start
+        // full (more data in flight while the pipeline fills), so the first group is scanned alone.
+        // leading tiles without payload finish before the primed group is reached: publish first then
+        if (dp.ngroups == 0) publish_consts();
+        if (settle()) {
+            u = braid_proc(u, r0, eng, dp, gp, lane, s_h);
+            ++gp;
+            publish_consts();
+            for (;;) {
+                if (!settle()) break;
+                ring_step(r1, r0);
+                if (!settle()) break;
+                ring_step(r0, r1);
+            }
         }
     } else {
+        publish_consts();
         settle();
     }
+    publish_consts();
     stamp(2);
     braid_publish(p, acc, pd, eng, lane);
     braid_resolve(p, pd, eng, lane);

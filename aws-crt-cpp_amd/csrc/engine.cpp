@@ -305,7 +305,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         const size_t waves = (size_t)d->cus * kWavesPerBlock;
         if (g_timeline.cap < waves) {
             if (g_timeline.d) (void)hipFree(g_timeline.d);
-            HIP_TRY(hipMalloc((void **)&g_timeline.d, waves * 4 * sizeof(unsigned long long)));
+            HIP_TRY(hipMalloc((void **)&g_timeline.d, waves * 8 * sizeof(unsigned long long)));
             g_timeline.cap = waves;
         }
         g_timeline.waves = waves;
@@ -614,7 +614,7 @@ AWS_CRT_AMD_API size_t aws_crt_amd_debug_timeline(unsigned long long *h_out, siz
     if (!g_timeline.d || !h_out) return 0;
     if (hipDeviceSynchronize() != hipSuccess) return 0;
     const size_t n = std::min(max_waves, g_timeline.waves);
-    if (hipMemcpy(h_out, g_timeline.d, n * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    if (hipMemcpy(h_out, g_timeline.d, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return n;
 }
 

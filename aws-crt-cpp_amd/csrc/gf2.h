@@ -12,9 +12,9 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
-#define GF2_HD __host__ __device__ inline
+#define GF2_HD __host__ __device__ constexpr inline
 #else
-#define GF2_HD inline
+#define GF2_HD constexpr inline
 #endif
 
 namespace amdcrc {
