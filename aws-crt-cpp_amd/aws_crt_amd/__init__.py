@@ -86,6 +86,25 @@ def _out_dtype(alg: int):
     return torch.int64 if alg in WIDE else torch.int32
 
 
+def time_next_launch(start_event, stop_event) -> None:
+    """Diagnostics: the next scan launched by this thread stamps its own dispatch start / end into
+    these torch.cuda.Event objects (created with enable_timing=True)."""
+    L = lib()
+    L.aws_crt_amd_debug_time_next_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.aws_crt_amd_debug_time_next_launch(start_event.cuda_event, stop_event.cuda_event)
+
+
+def event_ms(start_event, stop_event) -> float:
+    """Milliseconds between two events stamped by time_next_launch."""
+    L = lib()
+    L.aws_crt_amd_debug_event_ms.restype = ctypes.c_float
+    L.aws_crt_amd_debug_event_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    ms = L.aws_crt_amd_debug_event_ms(start_event.cuda_event, stop_event.cuda_event)
+    if ms < 0:
+        raise EngineError("event timing failed")
+    return ms
+
+
 def checksum_strided(alg: int, base, stride: int, length: int, count: int, seeds=None, out=None, stream=None,
                      base_offset: int = 0):
     """Batch of `count` device buffers [base + i*stride + base_offset, +length).  `base` is a torch

@@ -20,6 +20,7 @@
 //    and XOR-combined per buffer with device-scope atomics; the last tile to arrive finalises.
 //  * No MFMA: this is a byte scan, bounded by HBM read bandwidth.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "engine.h"
 #include "gf2.h"
@@ -616,10 +617,22 @@ __global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p)
 // relative to the tile end.  So u * x^(-32 l) is lane l's exact share (x is invertible mod P since
 // P(0) = 1): K_l = x^(-32 l), and the tile register is XOR_l u_l * K_l -- the same per-lane matrix
 // and wave reduction as the segment kernel, with no extra lookups per byte.
-constexpr uint32_t kT0Off = kTabBytes + kKmatBytes;  // plain byte table (1 KiB; wave-uniform reads)
-constexpr uint32_t kPcolOff = kT0Off + 1024;         // [m < 32][column j] of x^(8*TILE*m) (4 KiB)
-constexpr uint32_t kConstFlagOff = kPcolOff + 4096;   // waves that have published their K / P words
+//
+// LDS (76 KiB, so two 512-thread workgroups share a CU and a launch's prologue overlaps the previous
+// launch's scan on the same CU):
+//   T' tables, 8 copies, quarter-rotated: the 256-byte row of entry e holds the four tables in
+//   quarters of 32 bytes (quarter q = the table indexed by byte q of a, i.e. T'_(3-q)), 8 copies
+//   of 4 bytes each; bytes [128, 256) of every row are unused (v_perm can place the entry byte at
+//   bit 8, not bit 7).  In table slot k, lane quarter j = (lane >> 3) & 3 reads quarter (k + j) & 3
+//   with copy lane & 7, so a ds_read_b32 half-wave touches its 32 banks (bank = 8q + copy) once.
+constexpr uint32_t kBTabBytes = 65536;
+constexpr uint32_t kBKOff = kBTabBytes;               // K image, [j/4][lane][j%4] (8 KiB)
+constexpr uint32_t kPcolOff = kBKOff + 8192;          // [m < 32][column j] of x^(8*TILE*m) (4 KiB)
+constexpr uint32_t kT0Off = kPcolOff + 4096;          // plain byte table (1 KiB; wave-uniform reads)
+constexpr uint32_t kConstFlagOff = kT0Off + 1024;     // waves that have published their K / P words
 constexpr uint32_t kBraidLds = kConstFlagOff + 16;
+constexpr int kBraidBlock = 512;                      // 8 waves; two workgroups per CU
+constexpr int kBraidWaves = kBraidBlock / kWave;
 
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 typedef __attribute__((address_space(1))) const uint64_t gu64;
@@ -664,6 +677,13 @@ struct BraidBasis {
     }
 };
 
+// basis value b[k][bit] for a per-lane (runtime) table index k < 4: four compile-time candidates
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t basis_bit(uint32_t k, int bit) {
+    constexpr BraidBasis<POLY> B{};
+    return k == 0 ? B.b[0][bit] : k == 1 ? B.b[1][bit] : k == 2 ? B.b[2][bit] : B.b[3][bit];
+}
+
 template <uint32_t POLY, int K>
 __device__ __forceinline__ uint32_t basis_entry(uint32_t e) {
     constexpr BraidBasis<POLY> B{};
@@ -678,19 +698,24 @@ struct Braid32 {
     using T = uint32_t;
     static constexpr int W = 32;
     const char *L;
-    uint32_t srcA, srcB;  // per-lane perm constants: copy<<2 (| 1<<16 for tables 2,3)
+    uint32_t cst[4], sel[4];  // per lane and table slot k: quarter<<5 | copy<<2, and the v_perm selector
 
     __device__ void init(const char *lds, int lane) {
         L = lds;
-        srcA = (uint32_t)(lane & 31) << 2;
-        srcB = srcA | 0x10000u;
+        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = (k + j) & 3u;
+            cst[k] = (q << 5) | (cp << 2);
+            sel[k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a, bytes 2-3 <- 0
+        }
     }
-    // the four T' lookups of a = u ^ w (same conflict-free LDS layout as Eng32)
+    // the four T' lookups of a = u ^ w: slot k reads the table of byte (k + j) & 3 (any order: XORed)
     __device__ __forceinline__ void look(uint32_t a, uint32_t &l3, uint32_t &l2, uint32_t &l1, uint32_t &l0) const {
-        l3 = lds32(L, __builtin_amdgcn_perm(srcB, a, 0x0c060004u) + 128);  // byte0 -> T'3
-        l2 = lds32(L, __builtin_amdgcn_perm(srcB, a, 0x0c060104u));        // byte1 -> T'2
-        l1 = lds32(L, __builtin_amdgcn_perm(srcA, a, 0x0c060204u) + 128);  // byte2 -> T'1
-        l0 = lds32(L, __builtin_amdgcn_perm(srcA, a, 0x0c060304u));        // byte3 -> T'0
+        l3 = lds32(L, __builtin_amdgcn_perm(cst[0], a, sel[0]));
+        l2 = lds32(L, __builtin_amdgcn_perm(cst[1], a, sel[1]));
+        l1 = lds32(L, __builtin_amdgcn_perm(cst[2], a, sel[2]));
+        l0 = lds32(L, __builtin_amdgcn_perm(cst[3], a, sel[3]));
     }
     // a * x^(8*256)
     __device__ __forceinline__ uint32_t step(uint32_t a) const {
@@ -714,7 +739,7 @@ struct Braid32 {
         uint32_t acc = 0;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint4 c = *(const uint4 *)(L + kTabBytes + (g * 64 + lane) * 16);
+            const uint4 c = *(const uint4 *)(L + kBKOff + (g * 64 + lane) * 16);
             acc = xor_and(acc, c.x, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 0), 1));
             acc = xor_and(acc, c.y, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 1), 1));
             acc = xor_and(acc, c.z, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 2), 1));
@@ -728,9 +753,17 @@ struct BGroup {
     uint32_t w[kBraidRowsPerGroup];
 };
 
+// one payload word; NT: non-temporal (streamed once, not kept in the caches)
+template <bool NT>
+__device__ __forceinline__ uint32_t ldpay(uint64_t a) {
+    if (NT) return __builtin_nontemporal_load((gu32 *)a);
+    return *(gu32 *)a;
+}
+
 // group gi of tile d: rows [16 gi, 16 gi + 16), this lane's word of each (virtual offset
 // gi*4096 + 256 r + 4 lane).  Words in the virtual front pad read a valid address (the main start)
 // and are zeroed by braid_proc.
+template <bool NT>
 __device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi, int lane) {
     const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
     // rows go out in order on every path (scheduling barriers), as in braid_fused: the compiler's
@@ -740,14 +773,14 @@ __device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi
         const uint64_t a = d.vbase + vo0;
 #pragma unroll
         for (int r = 0; r < kBraidRowsPerGroup; ++r) {
-            g.w[r] = *(gu32 *)(a + kBraidRow * r);
+            g.w[r] = ldpay<NT>(a + kBraidRow * r);
             __builtin_amdgcn_sched_barrier(0);
         }
     } else {
 #pragma unroll
         for (int r = 0; r < kBraidRowsPerGroup; ++r) {
             const uint32_t vo = vo0 + kBraidRow * r;
-            g.w[r] = *(gu32 *)(vo >= d.pad ? d.vbase + vo : d.H);
+            g.w[r] = ldpay<NT>(vo >= d.pad ? d.vbase + vo : d.H);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -755,12 +788,13 @@ __device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi
 
 // Prologue loads: one code path for padded and unpadded tiles (a per-row address select), so the
 // compiler sees a single load sequence and waits only for the constants before the LDS build.
+template <bool NT>
 __device__ __forceinline__ void braid_prime(BGroup &g, uint64_t vbase, uint64_t H, uint32_t pad, uint32_t gi, int lane) {
     const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
 #pragma unroll
     for (int r = 0; r < kBraidRowsPerGroup; ++r) {
         const uint32_t vo = vo0 + kBraidRow * r;
-        g.w[r] = *(gu32 *)(vo >= pad ? vbase + vo : H);
+        g.w[r] = ldpay<NT>(vo >= pad ? vbase + vo : H);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -791,7 +825,7 @@ __device__ __forceinline__ uint32_t braid_proc(uint32_t u, const BGroup &g, cons
 // a 16-load burst per wave (measured: a burst-issue loop is 20 % slower at the same work).  With two
 // ring slots the other slot's loads are always the youngest in flight at every loop point, which
 // keeps the compiler's vmcnt bookkeeping exact across the loop.
-template <int RATE, class B>
+template <int RATE, bool NT, class B>
 __device__ __forceinline__ uint32_t braid_fused(uint32_t u, const BGroup &g, BGroup &dst, uint64_t a, const B &eng) {
     uint32_t x = u ^ g.w[0];
 #pragma unroll
@@ -799,7 +833,7 @@ __device__ __forceinline__ uint32_t braid_fused(uint32_t u, const BGroup &g, BGr
 #pragma unroll
         for (int q = 0; q < RATE; ++q) {
             const int r = RATE * st + q;
-            if (r < kBraidRowsPerGroup) dst.w[r] = *(gu32 *)(a + kBraidRow * r);
+            if (r < kBraidRowsPerGroup) dst.w[r] = ldpay<NT>(a + kBraidRow * r);
         }
         x = st + 1 < kBraidRowsPerGroup ? eng.step_x(x, g.w[st + 1]) : eng.step(x);
         __builtin_amdgcn_sched_barrier(0);
@@ -900,14 +934,14 @@ __device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d,
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY, bool BITOP3 = true, int RATE = 1>
-__global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams p) {
+template <uint32_t POLY, bool BITOP3 = true, int RATE = 1, bool NT = true>
+__global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanParams p) {
     using B = Braid32<POLY, BITOP3>;
     __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
 
     const int lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
     const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
     // diagnostics: per-wave timeline (start, tables built, scan done, exit) on the 100 MHz clock
     const bool stamps = p.d_timeline != nullptr;
@@ -957,36 +991,41 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     };
     // K-image word and P column of this thread: needed only when a tile finishes, so they are
     // published to LDS after the first group is scanned (see publish_consts), not before the scan
-    const uint64_t kq = *(gu64 *)(p.d_kvals + threadIdx.x);
-    const uint32_t pce = *(gu32 *)(p.d_pcols ? (const uint32_t *)(p.d_pcols + threadIdx.x) : (const uint32_t *)p.d_kvals);
-    // prime two groups unconditionally (a wave without payload reads the constant block) through one
-    // load path, so the LDS build below waits only for the constants, not for the payload
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + 4 * threadIdx.x);  // 16 B of the 8 KiB image
+    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
+    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
+    // prime the first group unconditionally (a wave without payload reads the constant block)
     BGroup r0, r1;
     {
         // field-wise selects (selecting whole Tile structs put them in scratch)
-        const uint64_t zb = (uint64_t)p.d_kvals;  // 13 KiB: two groups of this lane's words stay inside
+        const uint64_t zb = (uint64_t)p.d_kvals;  // 13 KiB: a group of this lane's words stays inside
         const uint64_t vb0 = any ? df.vbase : zb, h0 = any ? df.H : zb;
         const uint32_t pad0 = any ? df.pad : 0u, g0 = any ? gf : 0u;
         if (any) pf_advance();
-        const uint64_t vb1 = any ? df.vbase : zb, h1 = any ? df.H : zb;
-        const uint32_t pad1 = any ? df.pad : 0u, g1 = any ? gf : 1u;
-        if (any) pf_advance();
-        braid_prime(r0, vb0, h0, pad0, g0, lane);
-        braid_prime(r1, vb1, h1, pad1, g1, lane);
+        // Only the first group is primed, before the table build: issuing a load stalls the wave
+        // while the memory system is saturated (every CU primes at once), so priming two groups
+        // kept the first scan waiting for 8 KiB per wave to be accepted.  The ring scans group 0
+        // while group 1's loads go out between its table steps.
+        braid_prime<NT>(r0, vb0, h0, pad0, g0, lane);
     }
     {
-        // T' (1024 entries, 32 copies each) and T0 from the compile-time bases
-        const uint32_t i = threadIdx.x, e = i & 255u;
-        const uint32_t k = __builtin_amdgcn_readfirstlane(i >> 8);  // wave-uniform
-        const uint32_t te = k == 0   ? basis_entry<POLY, 0>(e)
-                            : k == 1 ? basis_entry<POLY, 1>(e)
-                            : k == 2 ? basis_entry<POLY, 2>(e)
-                                     : basis_entry<POLY, 3>(e);
-        const uint32_t base = ((k >> 1) << 16) | (e << 8) | ((k & 1) << 7);
-        const uint4 vv = make_uint4(te, te, te, te);
+        // T' (4 tables x 256 entries, 8 copies each) and T0 from the compile-time bases.  One 16-byte
+        // store = 4 copies of one (table, entry); the 8 lanes of a ds_write_b128 group take the 8
+        // (quarter, half) slots of a row, so each group fills 128 distinct bytes (no bank conflict).
+        const uint32_t i = threadIdx.x;
+        const uint32_t q = (i >> 1) & 3u, h = i & 1u;
+        uint32_t bq[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) *(uint4 *)(lds + base + ((j + i) & 7u) * 16) = vv;  // rotated: spread banks
-        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(e);
+        for (int b = 0; b < 8; ++b) bq[b] = basis_bit<POLY>(3 - q, b);  // quarter q holds T'_(3-q)
+#pragma unroll
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint32_t e = (i >> 3) + 64u * pass;
+            uint32_t te = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) te ^= ((e >> b) & 1u) ? bq[b] : 0u;
+            *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
+        }
+        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
         if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
     }
     stamp(4);  // constants arrived, LDS stores issued
@@ -1003,15 +1042,16 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     auto publish_consts = [&]() {
         if (published) return;
         published = true;
-        *(uint64_t *)(lds + kTabBytes + 8 * threadIdx.x) = kq;
-        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce;
+        *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
+        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
+        *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     auto await_consts = [&]() {
         if (consts_ready) return;
         while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)kWavesPerBlock)
+               (uint32_t)kBraidWaves)
             __builtin_amdgcn_s_sleep(1);
         consts_ready = true;
     };
@@ -1046,24 +1086,26 @@ __global__ __launch_bounds__(kBlock, 1) void crc32_braid_kernel(const ScanParams
     };
 
     // one ring step: scan `cur` (group gp of tile dp) and load `dst` with the prefetch cursor's group
+    // (once the prefetch cursor is parked on the wave's last group that group is already in flight:
+    // a second load of it would be pure extra traffic -- non-temporal loads do not leave it in L2)
     auto ring_step = [&](const BGroup &cur, BGroup &dst) {
-        if (dp.pad == 0 && df.pad == 0) {
-            u = braid_fused<RATE>(u, cur, dst, df.vbase + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
+        if (pf_done) {
+            u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
+        } else if (dp.pad == 0 && df.pad == 0) {
+            u = braid_fused<RATE, NT>(u, cur, dst, df.vbase + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
         } else {
-            braid_load(dst, df, gf, lane);
+            braid_load<NT>(dst, df, gf, lane);
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
         }
         ++gp;
         pf_advance();
     };
     if (any) {
-        // two-slot ring: group g+1's loads stream out while group g is scanned.  Both slots start
-        // full (more data in flight while the pipeline fills), so the first group is scanned alone.
+        // two-slot ring: group g+1's loads stream out while group g is scanned
         // leading tiles without payload finish before the primed group is reached: publish first then
         if (dp.ngroups == 0) publish_consts();
         if (settle()) {
-            u = braid_proc(u, r0, eng, dp, gp, lane, s_h);
-            ++gp;
+            ring_step(r0, r1);
             publish_consts();
             for (;;) {
                 if (!settle()) break;
@@ -1187,19 +1229,29 @@ extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stre
     return (int)hipGetLastError();
 }
 
-extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, void *stream) {
+// Scan launch.  ev[0] / ev[1] (diagnostics, may be null): HIP events stamped with the dispatch's own
+// start / end time (hipExtLaunchKernel), i.e. the interval a kernel-trace profiler reports.
+template <typename K>
+static void launch(K kernel, int nblocks, int threads, hipStream_t s, const ScanParams *p, void *const *ev) {
+    if (ev && (ev[0] || ev[1]))
+        hipExtLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+    else
+        hipLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, *p);
+}
+
+extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, void *stream, void *const *ev) {
     hipStream_t s = (hipStream_t)stream;
     switch (alg) {
-        case ALG_CRC32: hipLaunchKernelGGL(crc32_braid_kernel<kPoly32>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
+        case ALG_CRC32: launch(crc32_braid_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev); break;
         case ALG_CRC32C:
             if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
-                hipLaunchKernelGGL((crc32_braid_kernel<kPoly32C, false>), dim3(nblocks), dim3(kBlock), 0, s, *p);
-            else if (p->dbg & 8)  // diagnostics: two loads per table step (front-loaded issue)
-                hipLaunchKernelGGL((crc32_braid_kernel<kPoly32C, true, 2>), dim3(nblocks), dim3(kBlock), 0, s, *p);
+                launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
+            else if (p->dbg & 1024)  // diagnostics: cached (temporal) payload loads
+                launch(crc32_braid_kernel<kPoly32C, true, 1, false>, nblocks, kBraidBlock, s, p, ev);
             else
-                hipLaunchKernelGGL(crc32_braid_kernel<kPoly32C>, dim3(nblocks), dim3(kBlock), 0, s, *p);
+                launch(crc32_braid_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             break;
-        case ALG_CRC64NVME: hipLaunchKernelGGL(crc_scan_kernel<ALG_CRC64NVME>, dim3(nblocks), dim3(kBlock), 0, s, *p); break;
+        case ALG_CRC64NVME: launch(crc_scan_kernel<ALG_CRC64NVME>, nblocks, kBlock, s, p, ev); break;
         default: return -1;
     }
     return (int)hipGetLastError();

@@ -32,6 +32,8 @@ using namespace amdcrc;
 namespace {
 
 thread_local std::string g_last_error;
+// diagnostics (aws_crt_amd_debug_time_next_launch): events stamped by the next scan dispatch
+thread_local void *g_time_events[2] = {nullptr, nullptr};
 
 int fail(int code, const std::string &msg) {
     g_last_error = msg;
@@ -278,6 +280,18 @@ uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main)
 
 inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 
+// Launch geometry of the scan kernels: the W=32 braided scan runs two 512-thread workgroups per CU
+// (8 waves each), the W=64 scan one 1024-thread workgroup per CU.  Either way 16 wave slots per CU.
+struct ScanGeometry {
+    uint64_t blocks, waves_per_block;
+};
+ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles) {
+    const uint64_t wpb = width_of(alg) == 32 ? 8 : (uint64_t)kWavesPerBlock;
+    const uint64_t per_cu = (uint64_t)kWavesPerBlock / wpb;
+    const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)d->cus * per_cu);
+    return {blocks, wpb};
+}
+
 int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
     int e = alg == AWS_CRT_AMD_XXH64 ? amdcrc_launch_xxh64(&xp, s)
                                      : amdcrc_launch_xxh3(alg == AWS_CRT_AMD_XXH3_64 ? 64 : 128, &xp, s);
@@ -329,11 +343,10 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_cnt = w->cnt;
         p.d_acc1 = w->acc1;
     }
-    const uint64_t waves = p.ntiles;
-    uint64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    blocks = std::min<uint64_t>(blocks, (uint64_t)d->cus);
+    const uint64_t blocks = scan_geometry(d, alg, p.ntiles).blocks;
     if (blocks == 0) return 0;
-    int e = amdcrc_launch_scan(alg, &p, (int)blocks, s);
+    int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
+    g_time_events[0] = g_time_events[1] = nullptr;
     if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString((hipError_t)e));
     return 0;
 }
@@ -438,8 +451,8 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         prefix[i + 1] = prefix[i] + T;
     }
     const uint64_t ntiles = prefix[count];
-    uint64_t blocks = std::min<uint64_t>((ntiles + kWavesPerBlock - 1) / kWavesPerBlock, (uint64_t)d->cus);
-    const uint64_t nw = std::max<uint64_t>(blocks, 1) * kWavesPerBlock;
+    const ScanGeometry geo = scan_geometry(d, xxh ? ALG_CRC32 : alg, ntiles);
+    const uint64_t nw = std::max<uint64_t>(geo.blocks, 1) * geo.waves_per_block;
     const size_t words = count * 2 + (count + 1) + nw;
     uint64_t *h;
     int rc0 = stage_begin(d, s, words * 8, (void **)&h);
@@ -616,6 +629,23 @@ AWS_CRT_AMD_API size_t aws_crt_amd_debug_timeline(unsigned long long *h_out, siz
     const size_t n = std::min(max_waves, g_timeline.waves);
     if (hipMemcpy(h_out, g_timeline.d, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
     return n;
+}
+
+// Diagnostics (not part of the public headers): the next scan launched by this thread records the
+// dispatch's own start / end timestamps into these hipEvent_t (hipExtLaunchKernel), the interval a
+// kernel-trace profiler reports, without the marker packets of a hipEventRecord pair.
+AWS_CRT_AMD_API void aws_crt_amd_debug_time_next_launch(void *start_event, void *stop_event) {
+    g_time_events[0] = start_event;
+    g_time_events[1] = stop_event;
+}
+
+// Diagnostics: elapsed milliseconds between two events stamped by aws_crt_amd_debug_time_next_launch
+// (torch's Event.elapsed_time refuses events it did not record itself).
+AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_event) {
+    float ms = -1.0f;
+    if (hipEventSynchronize((hipEvent_t)stop_event) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, (hipEvent_t)start_event, (hipEvent_t)stop_event) != hipSuccess) return -1.0f;
+    return ms;
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,

@@ -10,11 +10,18 @@ Each rank scans its own batches (buffers shard across GPUs with no collective: w
 Steps rotate over --batches distinct batches (default 8 = 512 MiB per GPU, twice the 256 MiB
 Infinity Cache) so every launch streams from HBM, not from the on-die cache.
 
-Timed region: the K launches are replayed from a captured HIP graph (one launch per batch, the
-batches split over --branches independent graph branches so consecutive launches overlap their
-ramp-up and tail); any K % batches remainder is launched eagerly.  Kernel duration for the
-roofline: a separate pass queues --timing-launches eager launches bracketed by HIP events behind a
-GPU-side hold (so host launch latency never sits between an event pair).
+Timed region: K eager launches, alternating over --branches HIP streams so that a launch's
+workgroups start on CUs as the previous launch's workgroups retire (its prologue overlaps the other
+launch's tail; measured best at 2 streams).  --mode graph replays a captured HIP graph instead (one
+launch per batch, batches split over graph branches; measured slower on ROCm 7.2: every replay
+starts with a ~20 us bubble).  Kernel duration for the roofline: a separate pass queues
+--timing-launches eager launches on one stream behind a GPU-side hold; each launch stamps HIP
+events with its own dispatch start / end (hipExtLaunchKernel through the engine's diagnostics
+hook), the interval rocprofv3's kernel trace reports for the same dispatches.
+
+End-to-end (PCIe-inclusive): the same batches start in pinned host memory; H2D copies
+on a copy stream overlap the scans on a compute stream through a 3-slot device ring, results come
+back D2H.  Reported as `e2e_pinned` next to `value`, never as `value`.
 
 Prints one JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per launch (1 byte read per
 payload byte) / mean kernel duration from HIP events recorded on the launch stream.
@@ -46,11 +53,12 @@ def parse():
     ap.add_argument("--buffer-bytes", type=int, default=65536)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--branches", type=int, default=2)
-    ap.add_argument("--mode", default="graph", choices=["graph", "eager"])
+    ap.add_argument("--mode", default="eager", choices=["graph", "eager"])
     ap.add_argument("--timing-launches", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
     return ap.parse_args()
 
 
@@ -82,6 +90,53 @@ def cpu_baseline(alg, host_batch, count, L, gpu_results, seconds, threads):
                       f"copied to host, {threads} threads, oracle SSE4.2 crc32q 3-way "
                       f"({'PCLMUL fold' if alg != 'crc32c' else 'crc32q'}) tier",
             "single_thread_gibs": round(rate1, 3), "parity_with_gpu": parity}
+
+
+def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
+    """Pinned host -> device -> scan -> results to host, copies overlapped with scans (3-slot ring)."""
+    import torch
+
+    step = count * L
+    host = torch.empty(nb * step, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev_data[: nb * step])
+    odt = torch.int64 if wide else torch.int32
+    slots = [torch.empty(step, dtype=torch.uint8, device=dev_data.device) for _ in range(3)]
+    outs = [torch.empty(count, dtype=odt, device=dev_data.device) for _ in range(3)]
+    hres = torch.empty((iters, count), dtype=odt, pin_memory=True)
+    cs, ks = torch.cuda.Stream(device=dev_data.device), torch.cuda.Stream(device=dev_data.device)
+    copied = [torch.cuda.Event() for _ in range(3)]
+    freed = [torch.cuda.Event() for _ in range(3)]
+
+    def run(n):
+        for i in range(n):
+            k, b = i % 3, i % nb
+            with torch.cuda.stream(cs):
+                if i >= 3:
+                    cs.wait_event(freed[k])
+                slots[k].copy_(host[b * step:(b + 1) * step], non_blocking=True)
+                copied[k].record(cs)
+            ks.wait_event(copied[k])
+            eng.checksum_strided(alg_id, slots[k], L, L, count, out=outs[k], stream=ks)
+            with torch.cuda.stream(ks):
+                hres[i].copy_(outs[k], non_blocking=True)
+            freed[k].record(ks)
+
+    run(min(iters, 6))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(iters)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # H2D alone through the same pinned buffers (the PCIe ceiling of this pipeline)
+    t1 = time.perf_counter()
+    with torch.cuda.stream(cs):
+        for i in range(iters):
+            slots[i % 3].copy_(host[(i % nb) * step:((i % nb) + 1) * step], non_blocking=True)
+    torch.cuda.synchronize()
+    el_h2d = time.perf_counter() - t1
+    return {"value": round(iters * step / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(iters * step / el_h2d / 2**30, 2),
+            "sample": f"{iters} batches of {count} x {L // 1024} KiB from {nb * step >> 20} MiB pinned host memory, "
+                      f"H2D on a copy stream overlapped with the scans, results D2H"}
 
 
 def main():
@@ -117,8 +172,11 @@ def main():
         eng.checksum_strided(ALG[alg], data, L, L, count, out=outs[b], stream=st, base_offset=b * step_bytes)
 
     torch.cuda.synchronize()
-    for i in range(max(args.warmup, 2 * nb)):  # every (batch, stream) pair once: caches + workspaces
-        launch(i)
+    # every batch once and, when there is a timed region, every stream (per-stream workspaces are
+    # allocated on first use); with --steps 0 (profiling the timing pass) stream 0 only, so every
+    # launch of the run is a serialized one
+    for i in range(max(args.warmup, nb if args.steps == 0 else 2 * nb)):
+        launch(i, streams[0] if args.steps == 0 else None)
     torch.cuda.synchronize()
 
     graph = None
@@ -168,11 +226,12 @@ def main():
     with torch.cuda.stream(st):
         torch.cuda._sleep(int(40e6))
     for i in range(nt):
-        starts[i].record(st)
-        launch(i, st)
+        starts[i].record(st)  # creates the events; the launch below re-stamps them
         ends[i].record(st)
+        eng.time_next_launch(starts[i], ends[i])  # hipExtLaunchKernel: the dispatch's own timestamps
+        launch(i, st)
     torch.cuda.synchronize()
-    durs = sorted(s_.elapsed_time(e_) for s_, e_ in zip(starts, ends))
+    durs = sorted(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends))
     kernel_ms = sum(durs) / nt
     achieved_gbs = step_bytes / (kernel_ms * 1e-3) / 1e9
 
@@ -185,6 +244,10 @@ def main():
                 traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_batches > 0:
+        e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -203,7 +266,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -213,7 +276,7 @@ def main():
                                    f"device-resident, per GPU per step",
                        "buffers_per_step": count, "buffer_bytes": L, "rotating_batches": nb,
                        "resident_bytes_per_gpu": nb * step_bytes, "launch": args.mode,
-                       "graph_branches": len(streams) if graph is not None else 1,
+                       "streams": len(streams),
                        "parallelism": f"buffers sharded over {world} GPU(s), no collective"},
             "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -221,6 +284,7 @@ def main():
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_median": round(durs[nt // 2], 5),
                          "bytes_per_launch": step_bytes, "timing_launches": nt},
             "cpu_baseline": cpu,
+            "e2e_pinned": e2e,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

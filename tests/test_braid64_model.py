@@ -1,0 +1,203 @@
+"""CPU: a Python model of the W=64 braided scan (crc_kernels.hip crc64_braid_kernel, CRC64NVME),
+checked against the oracle.  It restates the kernel's algebra independently of the C++ host code:
+
+  * rows of 512 bytes; lane l owns the 8-byte word at 8l of every row;
+  * braid step u <- T'(u ^ w) with T'_t[e] = e * x^(8(t+1)) * x^(8*504): slice-by-8 plus the skip
+    over the other 63 lanes' words; byte i of the 64-bit a indexes T'_(7-i);
+  * the kernel's LDS layout: region r = dword r of a, quarter q = byte q of that dword, copy c;
+    lane quarter j reads quarter (k + j) & 3 in table slot k (conflict-free bank pairs);
+  * lane share u * K_l, K_l = x^(-64 l);
+  * head state injected at virtual offset `pad` of the front-padded first tile;
+  * tiles in groups of 32: a tile moves to its group end (x^(8*TILE*m), m < 32), a group to the
+    buffer end (x^(8*TILE*(T - group_end))), arrivals counted per group and per buffer.
+
+Rows per tile R is a free parameter here (the kernel uses multiples of 8), so small buffers already
+exercise multi-group buffers.  A failure here is a design bug, not a kernel bug.
+"""
+import random
+
+import pytest
+
+from oracle import oracle
+
+P64 = 0x9A6C9329AC4BC9B5
+M64 = (1 << 64) - 1
+ROW = 512
+
+
+def mulx(v):
+    return (v >> 1) ^ (P64 if v & 1 else 0)
+
+
+def inv_mulx(t):
+    return ((((t ^ P64) << 1) | 1) & M64) if t >> 63 else (t << 1) & M64
+
+
+def mulmod(a, b):
+    m, p = 1 << 63, 0
+    while m:
+        if a & m:
+            p ^= b
+        m >>= 1
+        b = mulx(b)
+    return p
+
+
+def xpow8n(n):
+    r, sq = 1 << 63, 1 << 55  # x^0, x^8
+    while n:
+        if n & 1:
+            r = mulmod(r, sq)
+        sq = mulmod(sq, sq)
+        n >>= 1
+    return r
+
+
+def table_entry(e, t):
+    c = e
+    for _ in range(8 * (t + 1)):
+        c = mulx(c)
+    return c
+
+
+class Braid64:
+    def __init__(self):
+        skip = xpow8n(ROW - 8)
+        self.Tp = [[mulmod(table_entry(e, t), skip) for e in range(256)] for t in range(8)]
+        self.T0 = [table_entry(e, 0) for e in range(256)]
+        # the kernel's LDS image: byte address -> value (only the written entries)
+        self.lds = {}
+        for r in range(2):
+            for q in range(4):
+                t = 7 - q if r == 0 else 3 - q
+                for e in range(256):
+                    for c in range(8):
+                        self.lds[(r << 16) | (e << 8) | (q << 6) | (c << 3)] = self.Tp[t][e]
+        self.K = []
+        kl = 1 << 63
+        for _ in range(64):
+            self.K.append(kl)
+            for _ in range(64):
+                kl = inv_mulx(kl)
+
+    def step(self, a):
+        v = 0
+        for i in range(8):
+            v ^= self.Tp[7 - i][(a >> (8 * i)) & 255]
+        return v
+
+    def step_lds(self, a, lane):
+        """the kernel's lookup schedule: slot k, lane quarter j -> byte (k+j)&3 of each dword"""
+        j, c = (lane >> 3) & 3, lane & 7
+        v = 0
+        for k in range(4):
+            q = (k + j) & 3
+            for r in range(2):
+                e = (a >> (32 * r + 8 * q)) & 255
+                v ^= self.lds[(r << 16) | (e << 8) | (q << 6) | (c << 3)]
+        return v
+
+    def bytes_(self, s, data):
+        for b in data:
+            s = (s >> 8) ^ self.T0[(s ^ b) & 255]
+        return s
+
+
+@pytest.fixture(scope="module")
+def br():
+    return Braid64()
+
+
+def braid64_model(br, data, addr, seed, rows):
+    n = len(data)
+    ptr, end = addr, addr + n
+    H, Ea = (ptr + 15) & ~15, end & ~15
+    if Ea > H:
+        mainlen, headend, tail = Ea - H, H, Ea
+    else:
+        mainlen, headend, tail = 0, end, end
+    tile = ROW * rows
+    T = -(-mainlen // tile) if mainlen else 1
+    pad = T * tile - mainlen
+    s_h = br.bytes_(~seed & M64, data[: headend - ptr])
+    group_val, group_cnt, buf_val, buf_cnt = {}, {}, 0, 0
+    G = -(-T // 32)
+    fin = None
+    for k in range(T):
+        r = 0
+        if mainlen:
+            vbase = (H - ptr) - pad + k * tile
+            for lane in range(64):
+                u = s_h if (k == 0 and pad == 0 and lane == 0) else 0
+                for c in range(rows):
+                    vo = ROW * c + 8 * lane
+                    w = 0 if (k == 0 and pad and vo < pad) else int.from_bytes(data[vbase + vo: vbase + vo + 8], "little")
+                    if k == 0 and pad and vo == pad:
+                        w ^= s_h
+                    u = br.step(u ^ w)
+                r ^= mulmod(u, br.K[lane])
+        if T == 1:
+            fin = r if mainlen else s_h
+            break
+        g0 = k & ~31
+        gend = min(g0 + 32, T)
+        group_val[g0] = group_val.get(g0, 0) ^ mulmod(r, xpow8n(tile * (gend - 1 - k)))
+        group_cnt[g0] = group_cnt.get(g0, 0) + 1
+        if group_cnt[g0] == gend - g0:  # the group's last arrival
+            gv = group_val.pop(g0)
+            if G == 1:
+                fin = gv
+            else:
+                buf_val ^= mulmod(gv, xpow8n(tile * (T - gend)))
+                buf_cnt += 1
+                if buf_cnt == G:
+                    fin = buf_val
+    fin = br.bytes_(fin, data[tail - ptr:])
+    return ~fin & M64
+
+
+def test_inverse_x(br):
+    for l in range(64):
+        assert mulmod(br.K[l], xpow8n(8 * l)) == 1 << 63
+
+
+def test_lds_schedule_is_conflict_free_and_complete(br):
+    """in every slot the 32 lanes of a ds_read_b64 group hit 32 distinct bank pairs, and over the
+    four slots each lane reads each byte of both dwords once"""
+    for k in range(4):
+        for r in range(2):
+            pairs = set()
+            for lane in range(32):
+                j, c = (lane >> 3) & 3, lane & 7
+                q = (k + j) & 3
+                addr = (r << 16) | (0xA5 << 8) | (q << 6) | (c << 3)
+                pairs.add((addr >> 3) & 31)
+            assert len(pairs) == 32
+    rnd = random.Random(3)
+    for _ in range(200):
+        a = rnd.getrandbits(64)
+        assert br.step_lds(a, rnd.randrange(64)) == br.step(a)
+
+
+def test_step_is_multiply_by_x4096(br):
+    rnd = random.Random(4)
+    for _ in range(20):
+        a = rnd.getrandbits(64)
+        assert br.step(a) == mulmod(a, xpow8n(ROW))
+
+
+@pytest.mark.parametrize("rows", [1, 2, 8])
+def test_braid64_model_vs_oracle(br, rows):
+    rnd = random.Random(rows * 7 + 1)
+    tile = ROW * rows
+    sizes = [0, 1, 15, 16, 17, 511, 512, 4096, tile - 16, tile, tile + 16, 3 * tile + 7, 33 * tile + 48,
+             70 * tile - 32]
+    for n in sizes:
+        for misalign in (0, 3, 9):
+            if n > 20000 and misalign:
+                continue
+            data = bytes(rnd.getrandbits(8) for _ in range(n))
+            seed = rnd.choice([0, rnd.getrandbits(64)])
+            want = oracle.crc("crc64nvme", data, seed)
+            got = braid64_model(br, data, 0x1000 + misalign, seed, rows)
+            assert got == want, (rows, n, misalign, hex(seed))
