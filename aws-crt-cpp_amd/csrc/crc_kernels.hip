@@ -1126,6 +1126,348 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
 }
 
 // ------------------------------------------------------------------------------------------
+// W = 64 braided scan (CRC64NVME): the production path for the 64-bit CRC.
+//
+// The W=32 braid with 8-byte words: a row is 512 bytes, lane l owns the word at 8l (one
+// global_load_dwordx2 per row, 512 contiguous bytes per wave instruction), and
+//     u <- (u ^ w_row) * x^(8*512)
+// is one slice-by-8 step whose tables T'_t[e] = e * x^(8(t+1)) * x^(8*504) fold in the skip over the
+// other 63 words (byte i of a = u ^ w indexes T'_(7-i)): eight lookups per 8-byte word, one per byte.
+// Lane l's share of the tile register is u * x^(-64 l).
+//
+// LDS: the eight 64-bit tables in 8 copies, quarter-rotated (128 KiB; 32 copies would need 512 KiB).
+// Region r (= dword r of a) holds, in the 256-byte row of entry e, the four tables indexed by the
+// bytes of that dword: quarter q (64 bytes) = byte q, 8 copies x 8 bytes.  In table slot k, lane
+// quarter j = (lane >> 3) & 3 reads quarter (k + j) & 3 with copy lane & 7, so the 32 lanes of a
+// ds_read_b64 half-wave cover the 32 bank pairs of the row exactly once (tests/test_braid64_model.py
+// checks the schedule).  Tiles are combined in groups of 32 (slot value + arrival count per group),
+// then per buffer, so at most 32 atomics meet on one address.
+constexpr uint32_t kB64Row = 512;
+constexpr int kB64RowsPerGroup = 8;                 // 4 KiB per wave per ring slot (= 64 B per lane)
+constexpr uint32_t kB64TabBytes = 131072;
+constexpr uint32_t kB64T0Off = kB64TabBytes;        // plain byte table, 256 x u64 (head / tail)
+constexpr uint32_t kB64Lds = kB64T0Off + 2048;
+
+typedef __attribute__((address_space(1))) const uint64_t gu64c;
+
+template <uint64_t POLY>
+struct Braid64Basis {
+    uint64_t b[9][8];  // b[t][i] = T'_t[1 << i] (t < 8); b[8][i] = T_0[1 << i]
+    constexpr Braid64Basis() : b() {
+        const uint64_t skip = gf2_xpow8n(kB64Row - 8, POLY, 64);
+        for (int i = 0; i < 8; ++i) {
+            for (int t = 0; t < 8; ++t) b[t][i] = gf2_mulmod(gf2_table_entry(1u << i, t, POLY), skip, POLY, 64);
+            b[8][i] = gf2_table_entry(1u << i, 0, POLY);
+        }
+    }
+};
+
+template <uint64_t POLY, int K>
+__device__ __forceinline__ uint64_t basis64(uint32_t e) {
+    constexpr Braid64Basis<POLY> B{};
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0ull;
+    return v;
+}
+
+template <uint64_t POLY>
+__device__ __forceinline__ uint64_t basis64_rt(uint32_t t, uint32_t e) {  // t wave-uniform
+    switch (t) {
+        case 0: return basis64<POLY, 0>(e);
+        case 1: return basis64<POLY, 1>(e);
+        case 2: return basis64<POLY, 2>(e);
+        case 3: return basis64<POLY, 3>(e);
+        case 4: return basis64<POLY, 4>(e);
+        case 5: return basis64<POLY, 5>(e);
+        case 6: return basis64<POLY, 6>(e);
+        default: return basis64<POLY, 7>(e);
+    }
+}
+
+template <uint64_t POLY>
+struct Braid64 {
+    using T = uint64_t;
+    static constexpr int W = 64;
+    const char *L;
+    uint32_t cst[4], csth[4], sel[4];
+    uint64_t kl;  // K_l = x^(-64 l)
+
+    __device__ void init(const char *lds, int lane) {
+        L = lds;
+        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = (k + j) & 3u;
+            cst[k] = (q << 6) | (cp << 3);
+            csth[k] = cst[k] | 0x10000u;
+            sel[k] = 0x0c060004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a, byte2 <- region
+        }
+    }
+    // a * x^(8*512) ^ wn
+    __device__ __forceinline__ uint64_t step_x(uint64_t a, uint64_t wn) const {
+        const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = lds64(L, __builtin_amdgcn_perm(cst[k], lo, sel[k]));
+            v[4 + k] = lds64(L, __builtin_amdgcn_perm(csth[k], hi, sel[k]));
+        }
+        uint32_t rl = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]), (uint32_t)v[3], (uint32_t)v[4]);
+        rl = xor3(xor3(rl, (uint32_t)v[5], (uint32_t)v[6]), (uint32_t)v[7], (uint32_t)wn);
+        uint32_t rh = xor3(xor3((uint32_t)(v[0] >> 32), (uint32_t)(v[1] >> 32), (uint32_t)(v[2] >> 32)),
+                           (uint32_t)(v[3] >> 32), (uint32_t)(v[4] >> 32));
+        rh = xor3(xor3(rh, (uint32_t)(v[5] >> 32), (uint32_t)(v[6] >> 32)), (uint32_t)(v[7] >> 32), (uint32_t)(wn >> 32));
+        return ((uint64_t)rh << 32) | rl;
+    }
+    __device__ __forceinline__ uint64_t step(uint64_t a) const { return step_x(a, 0); }
+    // plain byte step for head / tail bytes (s wave-uniform: broadcast reads)
+    __device__ __forceinline__ uint64_t byte(uint64_t s, uint32_t b) const {
+        return (s >> 8) ^ lds64(L, kB64T0Off + 8 * (((uint32_t)s ^ b) & 0xffu));
+    }
+    // r * K_l, bit-serial (once per tile)
+    __device__ __forceinline__ uint64_t mulK(uint64_t r) const {
+        uint64_t b = kl, acc = 0;
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) {
+            acc ^= b & (uint64_t)((int64_t)(r << j) >> 63);
+            b = gf2_mulx(b, POLY);
+        }
+        return acc;
+    }
+};
+
+struct B64Group {
+    uint64_t w[kB64RowsPerGroup];
+};
+
+template <bool NT>
+__device__ __forceinline__ uint64_t ldpay64(uint64_t a) {
+    if (NT) return __builtin_nontemporal_load((gu64c *)a);
+    return *(gu64c *)a;
+}
+
+// group gi of tile d: rows [8 gi, 8 gi + 8), this lane's word of each (virtual offset
+// gi*4096 + 512 r + 8 lane); words in the virtual front pad read the main start and are zeroed later
+template <bool NT>
+__device__ __forceinline__ void b64_load(B64Group &g, uint64_t vbase, uint64_t H, uint32_t pad, uint32_t gi, int lane) {
+    const uint32_t vo0 = gi * (kB64Row * kB64RowsPerGroup) + 8u * lane;
+#pragma unroll
+    for (int r = 0; r < kB64RowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kB64Row * r;
+        g.w[r] = ldpay64<NT>(vo >= pad ? vbase + vo : H);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <class B>
+__device__ __forceinline__ uint64_t b64_proc(uint64_t u, const B64Group &g, const B &eng, const Tile &d, uint32_t gi,
+                                             int lane, uint64_t s_h) {
+    if (d.pad == 0) {
+        uint64_t a = u ^ g.w[0];
+#pragma unroll
+        for (int r = 0; r + 1 < kB64RowsPerGroup; ++r) a = eng.step_x(a, g.w[r + 1]);
+        return eng.step(a);
+    }
+    const uint32_t vo0 = gi * (kB64Row * kB64RowsPerGroup) + 8u * lane;
+#pragma unroll
+    for (int r = 0; r < kB64RowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kB64Row * r;
+        uint64_t w = vo >= d.pad ? g.w[r] : 0ull;
+        if (vo == d.pad) w ^= s_h;  // this braid is still zero here: the head state enters with the word
+        u = eng.step(u ^ w);
+    }
+    return u;
+}
+
+// steady state: scan group g while issuing group g+1's loads, one per table step
+template <bool NT, class B>
+__device__ __forceinline__ uint64_t b64_fused(uint64_t u, const B64Group &g, B64Group &dst, uint64_t a, const B &eng) {
+    uint64_t x = u ^ g.w[0];
+#pragma unroll
+    for (int st = 0; st < kB64RowsPerGroup; ++st) {
+        dst.w[st] = ldpay64<NT>(a + kB64Row * st);
+        x = st + 1 < kB64RowsPerGroup ? eng.step_x(x, g.w[st + 1]) : eng.step(x);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t wave_xor64_s(uint64_t v) {
+    const uint32_t lo = wave_xor_s((uint32_t)v), hi = wave_xor_s((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Tile finish: lane shares -> tile register -> its 32-tile group slot (value XOR, then arrival
+// count); the group's last arrival moves the group value to the buffer end and XORs it into the
+// buffer word (count of groups); the buffer's last group finalises.
+template <class B>
+__device__ __forceinline__ void b64_finish(const ScanParams &p, const Tile &d, uint64_t u, uint64_t s_h, const B &eng, int lane) {
+    const uint64_t r = d.ngroups ? wave_xor64_s(eng.mulK(u)) : 0ull;
+    if (d.T == 1) {
+        if (lane == 0) finalize(p, d.b, d.ngroups ? r : s_h, d.tail, d.tail_len, eng);
+        return;
+    }
+    const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
+    const uint64_t v = mul_pcols<uint64_t, 64>(r, p.d_pcols + (gend - 1 - d.k) * 64);
+    const uint64_t slot = d.tbase + g0;
+    unsigned int c = 0;
+    if (lane == 0) {
+        const unsigned long long o =
+            __hip_atomic_fetch_xor(&p.d_acc1[slot], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(o) : "memory");  // performed before it is counted
+        c = __hip_atomic_fetch_add(&p.d_cnt1[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (c != (unsigned int)(gend - g0 - 1)) return;
+    unsigned long long gv = 0;
+    if (lane == 0) {
+        gv = __hip_atomic_exchange(&p.d_acc1[slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.d_cnt1[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gv = rfl64(gv);
+    const uint64_t G = (d.T + 31) / 32;
+    if (G == 1) {
+        if (lane == 0) finalize(p, d.b, (uint64_t)gv, d.tail, d.tail_len, eng);
+        return;
+    }
+    const uint64_t gs = d.T > gend ? mul_pcols<uint64_t, 64>((uint64_t)gv, p.d_pcols + (d.T - gend) * 64) : (uint64_t)gv;
+    if (lane == 0) {
+        const unsigned long long o =
+            __hip_atomic_fetch_xor(&p.d_acc[d.b], (unsigned long long)gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(o) : "memory");
+        const unsigned int c2 = __hip_atomic_fetch_add(&p.d_cnt[d.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c2 == (unsigned int)(G - 1)) {
+            const uint64_t fin = __hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&p.d_cnt[d.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            finalize(p, d.b, fin, d.tail, d.tail_len, eng);
+        }
+    }
+}
+
+template <uint64_t POLY, bool NT = true>
+__global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams p) {
+    using B = Braid64<POLY>;
+    __shared__ __attribute__((aligned(16))) char lds[kB64Lds];
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
+
+    Walker w0{0, 0, 0};
+    if (p.list_mode && t0 < t1) {
+        w0.b = sload64(p.d_wave_buf + gw);
+        w0.lo = sload64(p.d_tile_prefix + w0.b);
+        w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
+    }
+    // ---- prefetch cursor: the next (tile, group) to load; pf_done once every group is in flight
+    Walker wf = w0;
+    uint64_t tf = t0;
+    uint32_t gf = 0;
+    Tile df{};
+    bool any = false;
+    for (; tf < t1; ++tf) {
+        df = make_tile(p, tf, wf);
+        if (df.ngroups) {
+            any = true;
+            break;
+        }
+    }
+    bool pf_done = !any;
+    auto pf_advance = [&]() {
+        if (gf + 1 < df.ngroups) {
+            ++gf;
+            return;
+        }
+        if (pf_done) return;
+        Walker w2 = wf;
+        for (uint64_t t = tf + 1; t < t1; ++t) {
+            Tile d2 = make_tile(p, t, w2);
+            if (d2.ngroups) {
+                df = d2;
+                wf = w2;
+                tf = t;
+                gf = 0;
+                return;
+            }
+        }
+        pf_done = true;
+    };
+    const uint64_t kl = *(gu64c *)(p.d_kvals + lane);
+    // prime the first group (a wave without payload reads the 16 KiB constant block)
+    B64Group r0, r1;
+    {
+        const uint64_t zb = (uint64_t)p.d_kvals;
+        b64_load<NT>(r0, any ? df.vbase : zb, any ? df.H : zb, any ? df.pad : 0u, any ? gf : 0u, lane);
+        if (any) pf_advance();
+    }
+    {
+        // T'_t: two waves per table (t wave-uniform), each thread two entries x 8 copies; T0
+        const uint32_t i = threadIdx.x, wv = i >> 6;
+        const uint32_t t = __builtin_amdgcn_readfirstlane(wv >> 1);
+        const uint32_t reg = t >= 4 ? 0u : 1u, q = t >= 4 ? 7u - t : 3u - t;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const uint32_t e = ((wv & 1u) << 7) | ((uint32_t)n << 6) | (i & 63u);
+            const uint64_t v = basis64_rt<POLY>(t, e);
+            const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
+            char *row = lds + (reg << 16) + (e << 8) + (q << 6);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) *(v4u *)(row + (((h + i) & 3u) << 4)) = vv;  // rotated: spread banks
+        }
+        if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    if (t0 >= t1) return;
+
+    // ---- scan cursor
+    Walker wp = w0;
+    uint64_t tp = t0;
+    uint32_t gp = 0;
+    Tile dp = make_tile(p, tp, wp);
+    uint64_t s_h = dp.k == 0 ? head_state(p, dp, eng) : 0ull;
+    uint64_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
+
+    auto settle = [&]() -> bool {
+        while (gp >= dp.ngroups) {
+            b64_finish(p, dp, u, s_h, eng, lane);
+            if (++tp >= t1) return false;
+            dp = make_tile(p, tp, wp);
+            gp = 0;
+            s_h = dp.k == 0 ? head_state(p, dp, eng) : 0ull;
+            u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
+        }
+        return true;
+    };
+    auto ring_step = [&](const B64Group &cur, B64Group &dst) {
+        if (pf_done) {
+            u = b64_proc(u, cur, eng, dp, gp, lane, s_h);
+        } else if (dp.pad == 0 && df.pad == 0) {
+            u = b64_fused<NT>(u, cur, dst, df.vbase + gf * (kB64Row * kB64RowsPerGroup) + 8u * lane, eng);
+        } else {
+            b64_load<NT>(dst, df.vbase, df.H, df.pad, gf, lane);
+            u = b64_proc(u, cur, eng, dp, gp, lane, s_h);
+        }
+        ++gp;
+        pf_advance();
+    };
+    if (any) {
+        for (;;) {
+            if (!settle()) break;
+            ring_step(r0, r1);
+            if (!settle()) break;
+            ring_step(r1, r0);
+        }
+    } else {
+        settle();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // xxHash64 (aws_xxhash64_compute, XXHash.cpp:17): one lane per buffer; the published
 // algorithm is a serial chain per buffer, so parallelism comes only from the batch.
 constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull, XP2 = 0xC2B2AE3D27D4EB4Full, XP3 = 0x165667B19E3779F9ull,
@@ -1251,7 +1593,12 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             else
                 launch(crc32_braid_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             break;
-        case ALG_CRC64NVME: launch(crc_scan_kernel<ALG_CRC64NVME>, nblocks, kBlock, s, p, ev); break;
+        case ALG_CRC64NVME:
+            if (p->dbg & 2048)  // diagnostics: the first-generation lane-segment scan
+                launch(crc_scan_kernel<ALG_CRC64NVME>, nblocks, kBlock, s, p, ev);
+            else
+                launch(crc64_braid_kernel<kPoly64Nvme>, nblocks, kBlock, s, p, ev);
+            break;
         default: return -1;
     }
     return (int)hipGetLastError();

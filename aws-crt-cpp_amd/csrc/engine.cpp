@@ -56,7 +56,8 @@ struct DevBuf {
 struct Workspace {
     unsigned long long *acc = nullptr;   // per buffer
     unsigned int *cnt = nullptr;         // per buffer
-    unsigned long long *acc1 = nullptr;  // per tile (W=32 group slots)
+    unsigned long long *acc1 = nullptr;  // per tile (32-tile group slots of the braided scans)
+    unsigned int *cnt1 = nullptr;        // per tile (W=64 group arrival counts)
     size_t cap = 0, cap_tiles = 0;
 };
 
@@ -190,6 +191,29 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
     return 0;
 }
 
+// W=64 braided-scan constants: K_l = x^(-64 l), l < 64, then zeros to 16 KiB (a wave without
+// payload primes its ring from this block: two groups of its words stay inside)
+inline uint64_t inv_mulx64(uint64_t t, uint64_t poly) { return (t >> 63) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
+int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
+    auto key = std::make_pair(alg, 0u);
+    auto it = d->kvals.find(key);
+    if (it == d->kvals.end()) {
+        const uint64_t poly = alg_poly(alg);
+        std::vector<uint64_t> c(2048, 0);
+        uint64_t kl = 1ull << 63;  // x^0
+        for (int l = 0; l < 64; ++l) {
+            c[l] = kl;
+            for (int i = 0; i < 64; ++i) kl = inv_mulx64(kl, poly);
+        }
+        DevBuf b;
+        int rc = upload(b, c.data(), c.size() * 8);
+        if (rc) return rc;
+        it = d->kvals.emplace(key, b).first;
+    }
+    *out = (const uint64_t *)it->second.p;
+    return 0;
+}
+
 // column j of P_k = x^(8*tile*k) * x^j, k < tmax : moves tile k's partial to its buffer end
 int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t **out) {
     auto key = std::make_pair(alg, tile);
@@ -234,10 +258,14 @@ int get_workspace(Device *d, hipStream_t s, size_t nbuf, size_t ntiles, Workspac
         if (w.acc1) {
             HIP_TRY(hipStreamSynchronize(s));
             (void)hipFree(w.acc1);
+            (void)hipFree(w.cnt1);
             w.acc1 = nullptr;
+            w.cnt1 = nullptr;
         }
         HIP_TRY(hipMalloc((void **)&w.acc1, cap * sizeof(unsigned long long)));
         HIP_TRY(hipMemset(w.acc1, 0, cap * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc((void **)&w.cnt1, cap * sizeof(unsigned int)));
+        HIP_TRY(hipMemset(w.cnt1, 0, cap * sizeof(unsigned int)));
         HIP_TRY(hipDeviceSynchronize());
         w.cap_tiles = cap;
     }
@@ -326,14 +354,17 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_timeline = g_timeline.d;
     }
     const uint64_t tile = (uint64_t)p.seg * kWave;
-    const bool braided = width_of(alg) == 32;
-    int rc = braided ? get_braid_consts(d, alg, &p.d_kvals) : get_kvals(d, alg, p.seg, &p.d_kvals);
+    const bool braided = width_of(alg) == 32 || !(p.dbg & 2048);  // dbg 2048: first-generation W=64 scan
+    int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals)
+             : braided           ? get_braid64_consts(d, alg, &p.d_kvals)
+                                 : get_kvals(d, alg, p.seg, &p.d_kvals);
     if (rc) return rc;
     p.d_pcols = nullptr;
     p.pcols_tmax = 0;
     p.d_acc = nullptr;
     p.d_cnt = nullptr;
     p.d_acc1 = nullptr;
+    p.d_cnt1 = nullptr;
     if (tmax > 1) {
         if ((rc = get_pcols(d, alg, tile, tmax, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
@@ -342,6 +373,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_acc = w->acc;
         p.d_cnt = w->cnt;
         p.d_acc1 = w->acc1;
+        p.d_cnt1 = w->cnt1;
     }
     const uint64_t blocks = scan_geometry(d, alg, p.ntiles).blocks;
     if (blocks == 0) return 0;

@@ -46,7 +46,8 @@ struct ScanParams {
     // ---- cross-tile combine workspace (zero on entry, left zero on exit)
     unsigned long long *d_acc;     // per buffer
     unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
-    unsigned long long *d_acc1;    // W=32 braided scan: per tile (slot of each 32-tile group)
+    unsigned long long *d_acc1;    // braided scans: per tile (slot of each 32-tile group)
+    unsigned int *d_cnt1;          // W=64 braided scan: per tile (arrivals of each 32-tile group)
     unsigned long long *d_timeline; // diagnostics (AMDCRC_DEBUG bit 4): 4 s_memrealtime stamps per wave
 };
 
