@@ -1,23 +1,19 @@
-// Batched CRC32 / CRC32C / CRC64NVME scan for gfx950 (MI355X, CDNA4).
+// Batched CRC32 / CRC32C / CRC64NVME scans for gfx950 (MI355X, CDNA4).
 //
 // Replaces the CPU loop behind aws_checksums_crc32_ex / crc32c_ex / crc64nvme_ex
 // (reference call sites source/checksum/CRC.cpp:17,22,27) for batches of device-resident
 // buffers.  Design notes: DESIGN.md "Kernels".  In short:
 //
-//  * One persistent workgroup of 1024 threads per CU.  The slice tables are built in LDS at
-//    launch and replicated 32x so that lane (l mod 32) always reads bank (l mod 32): a
-//    ds_read_b32 wave instruction is conflict-free whatever bytes it indexes.
-//      W=32: slice-by-4, 4 tables x 256 entries x 32 copies x 4 B = 128 KiB
-//      W=64: slice-by-2, 2 tables x 256 entries x 32 copies x 8 B = 128 KiB
-//    LDS byte address = table-pair<<16 | entry<<8 | table-in-pair<<7 | copy<<2 (W=32), which one
-//    v_perm_b32 builds from the state register (entry byte) and a per-lane constant (copy,
-//    pair): one VALU op per table lookup.
-//  * A wavefront owns a tile = 64 lanes x seg bytes of one buffer; lane l scans its contiguous
-//    seg bytes with 16-byte loads (8 in flight per prefetch group, one group ahead).
-//  * Lane partials are moved to the tile end with a per-lane GF(2) matrix (x^(8*seg*(63-l)),
-//    32 columns in LDS, W=32) or bit-serial multiply (W=64), XOR-reduced across the wave, then
-//    moved to the buffer end with x^(8*TILE*(T-1-k)) (column table in HBM, one column per lane)
-//    and XOR-combined per buffer with device-scope atomics; the last tile to arrive finalises.
+//  * Braided scans.  A buffer's 16-aligned main region is cut into tiles; a wavefront scans a tile
+//    row by row, lane l owning word l of every row (one fully coalesced wave load per row).  Each
+//    lane's state is one "braid" of the CRC: u <- (u ^ w) * x^(8*row), one slice-by-4 (W=32) or
+//    slice-by-8 (W=64) step whose byte tables fold in the skip over the other 63 lanes' words.
+//  * Byte tables live in LDS in 8 copies, quarter-rotated so that every ds_read of a half-wave
+//    touches distinct banks whatever bytes it indexes (76 KiB for W=32, 130 KiB for W=64).
+//  * A lane's state times x^(-w*l) is its share of the tile register (K_l); the wave XOR-reduces
+//    the shares, moves the tile register to its 32-tile group's end and then to the buffer end with
+//    column tables, and device-scope atomics combine the tiles of a buffer; the last arrival
+//    finalises (tail bytes, complement, store).
 //  * No MFMA: this is a byte scan, bounded by HBM read bandwidth.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -29,174 +25,13 @@ using namespace amdcrc;
 
 namespace {
 
-constexpr uint32_t kTabBytes = 131072;
-constexpr uint32_t kKmatBytes = 8192;  // W=32 only: 64 lanes x 32 columns x 4 B
-constexpr uint32_t kLdsBytes = kTabBytes + kKmatBytes;
-
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
-
+typedef __attribute__((address_space(1))) const v4u gv4u;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+typedef __attribute__((address_space(1))) const uint64_t gu64;
 
 __device__ __forceinline__ uint32_t lds32(const char *L, uint32_t a) { return *(const uint32_t *)(L + a); }
 __device__ __forceinline__ uint64_t lds64(const char *L, uint32_t a) { return *(const uint64_t *)(L + a); }
-
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v ^= __shfl_xor(v, off);
-    return v;
-}
-__device__ __forceinline__ uint64_t wave_xor(uint64_t v) {
-    uint32_t lo = wave_xor((uint32_t)v), hi = wave_xor((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// ------------------------------------------------------------------------------------------
-// W = 32: slice-by-4
-template <uint32_t POLY>
-struct Eng32 {
-    using T = uint32_t;
-    static constexpr int W = 32;
-    const char *L;
-    uint32_t srcA, srcB;  // per-lane perm constants: copy<<2 (| 1<<16 for tables 2,3)
-
-    __device__ void init(const char *lds, int lane, const ScanParams &) {
-        L = lds;
-        srcA = (uint32_t)(lane & 31) << 2;
-        srcB = srcA | 0x10000u;
-    }
-    uint64_t kl;  // unused (K in LDS)
-
-    static __device__ void build(char *L, const ScanParams &p) {
-        for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
-            const int k = (int)(i >> 8);
-            const uint32_t e = i & 255u;
-            const uint32_t v = (uint32_t)gf2_table_entry(e, k, POLY);
-            const uint32_t base = ((uint32_t)(k >> 1) << 16) | (e << 8) | ((uint32_t)(k & 1) << 7);
-            const uint4 vv = make_uint4(v, v, v, v);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t m = (j + i) & 7u;  // rotate so a wave's 16-B stores spread over banks
-                *(uint4 *)(L + base + m * 16) = vv;
-            }
-        }
-    }
-    // the host-built K-matrix image (engine.cpp get_kvals) arrives 8 bytes per thread
-    static constexpr bool kKmatInLds = true;
-
-    // s <- (s ^ w) * x^32 mod P : four conflict-free lookups
-    __device__ __forceinline__ uint32_t word(uint32_t s, uint32_t w) const {
-        s ^= w;
-        const uint32_t a3 = __builtin_amdgcn_perm(srcB, s, 0x0c060004u);  // byte0 -> T3
-        const uint32_t a2 = __builtin_amdgcn_perm(srcB, s, 0x0c060104u);  // byte1 -> T2
-        const uint32_t a1 = __builtin_amdgcn_perm(srcA, s, 0x0c060204u);  // byte2 -> T1
-        const uint32_t a0 = __builtin_amdgcn_perm(srcA, s, 0x0c060304u);  // byte3 -> T0
-        return lds32(L, a3 + 128) ^ lds32(L, a2) ^ lds32(L, a1 + 128) ^ lds32(L, a0);
-    }
-    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-        const uint32_t e = (s ^ b) & 0xffu;
-        return (s >> 8) ^ lds32(L, (e << 8) | srcA);
-    }
-    // r * x^(8*seg*(63-lane)) : 32 LDS matrix columns
-    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint4 c = *(const uint4 *)(L + kTabBytes + (g * 64 + lane) * 16);
-            acc ^= c.x & (uint32_t)((int32_t)(r << (4 * g + 0)) >> 31);
-            acc ^= c.y & (uint32_t)((int32_t)(r << (4 * g + 1)) >> 31);
-            acc ^= c.z & (uint32_t)((int32_t)(r << (4 * g + 2)) >> 31);
-            acc ^= c.w & (uint32_t)((int32_t)(r << (4 * g + 3)) >> 31);
-        }
-        return acc;
-    }
-};
-
-// ------------------------------------------------------------------------------------------
-// W = 64: slice-by-2 (two 64 KiB tables)
-template <uint64_t POLY>
-struct Eng64 {
-    using T = uint64_t;
-    static constexpr int W = 64;
-    const char *L;
-    uint32_t src0, src1;  // copy<<3 | table<<16
-    uint64_t kl;          // K_l = x^(8*seg*(63-lane))
-
-    static constexpr bool kKmatInLds = false;
-
-    __device__ void init(const char *lds, int lane, const ScanParams &) {
-        L = lds;
-        src0 = (uint32_t)(lane & 31) << 3;
-        src1 = src0 | 0x10000u;
-    }
-
-    static __device__ void build(char *L, const ScanParams &) {
-        for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) {
-            const int k = (int)(i >> 8);
-            const uint32_t e = i & 255u;
-            const uint64_t v = gf2_table_entry(e, k, POLY);
-            const uint32_t base = ((uint32_t)k << 16) | (e << 8);
-            const uint4 vv = make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32));
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t m = (j + i) & 15u;
-                *(uint4 *)(L + base + m * 16) = vv;
-            }
-        }
-    }
-
-    __device__ __forceinline__ uint64_t half(uint64_t s, uint32_t h) const {
-        s ^= h;
-        const uint32_t lo = (uint32_t)s;
-        const uint32_t a1 = __builtin_amdgcn_perm(src1, lo, 0x0c060004u);  // byte0 -> T1
-        const uint32_t a0 = __builtin_amdgcn_perm(src0, lo, 0x0c060104u);  // byte1 -> T0
-        return (s >> 16) ^ lds64(L, a1) ^ lds64(L, a0);
-    }
-    __device__ __forceinline__ uint64_t word(uint64_t s, uint32_t w) const {
-        s = half(s, w & 0xffffu);
-        return half(s, w >> 16);
-    }
-    __device__ __forceinline__ uint64_t byte(uint64_t s, uint32_t b) const {
-        const uint32_t e = ((uint32_t)s ^ b) & 0xffu;
-        return (s >> 8) ^ lds64(L, (e << 8) | src0);
-    }
-    __device__ __forceinline__ uint64_t mulK(uint64_t r, int) const {
-        uint64_t b = kl, acc = 0;
-#pragma unroll 8
-        for (int j = 0; j < 64; ++j) {
-            acc ^= b & (uint64_t)((int64_t)(r << j) >> 63);
-            b = gf2_mulx(b, POLY);
-        }
-        return acc;
-    }
-};
-
-template <int ALG>
-struct EngFor;
-template <>
-struct EngFor<ALG_CRC32> {
-    using E = Eng32<kPoly32>;
-};
-template <>
-struct EngFor<ALG_CRC32C> {
-    using E = Eng32<kPoly32C>;
-};
-template <>
-struct EngFor<ALG_CRC64NVME> {
-    using E = Eng64<kPoly64Nvme>;
-};
-
-// ------------------------------------------------------------------------------------------
-// Tile descriptor (wave-uniform, SGPRs).  Built twice per tile: by the prefetch cursor (address
-// fields only) and by the scan cursor (everything); both are pure arithmetic in strided mode.
-struct Tile {
-    uint64_t b, k, T;
-    uint64_t tbase;  // global index of the buffer's first tile
-    uint64_t vbase;  // device address of this tile's virtual offset 0
-    uint64_t H;      // first byte of the 16-aligned main region
-    uint64_t ptr, headend, tail;
-    uint32_t pad;  // virtual zero bytes in front of main (k == 0 only)
-    uint32_t ngroups;
-    uint32_t tail_len;
-};
 
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
@@ -220,20 +55,73 @@ __device__ __forceinline__ uint32_t sload32(const void *a) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t c, uint32_t m) {  // acc ^ (c & m)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(acc), "v"(c), "v"(m));
+    return r;
+}
+
+// XOR over the 64 lanes, returned wave-uniform: two quad_perm and two row_ror DPP steps leave each
+// 16-lane row's XOR in all its lanes; four readlanes finish in scalar registers.
+__device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
+                      __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
+}
+__device__ __forceinline__ uint64_t wave_xor64_s(uint64_t v) {
+    const uint32_t lo = wave_xor_s((uint32_t)v), hi = wave_xor_s((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ------------------------------------------------------------------------------------------
+// Work decomposition (engine.h): buffer b = [ptr, end) is head [ptr, H) (H = ptr rounded up to 16),
+// main [H, Ea) (Ea = end rounded down to 16) and tail [Ea, end).  Main is front-padded virtually
+// with zeros to T tiles of TILE = 64 * seg bytes (free for a raw CRC); tile k starts at virtual
+// offset k * TILE.  LIST = ragged batch (descriptors by SMEM), else uniform (pure arithmetic).
+struct Tile {        // wave-uniform (SGPRs): everything the scan needs per tile
+    uint64_t b, k, T;
+    uint64_t tbase;  // global index of the buffer's first tile
+    uint64_t vbase;  // device address of this tile's virtual offset 0; main starts at vbase + pad
+    uint32_t pad;    // virtual zero bytes in front of main (k == 0 only)
+    uint32_t ngroups;
+};
+struct Edges {       // head / tail of a buffer, recomputed where needed instead of kept in SGPRs
+    uint64_t ptr, headend, tail, end;
+};
 struct Walker {  // list mode: running position in the tile prefix
     uint64_t b, lo, hi;
 };
 
+template <bool LIST>
+__device__ __forceinline__ Edges buffer_edges(const ScanParams &p, uint64_t b) {
+    uint64_t ptr, n;
+    if (LIST) {
+        ptr = sload64(p.d_ptrs + b);
+        n = sload64(p.d_lens + b);
+    } else {
+        ptr = p.base + b * p.stride;
+        n = p.len;
+    }
+    const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
+    return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
+}
+
+template <bool LIST>
 __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walker &wk) {
     Tile d;
-    uint64_t ptr, n;
-    if (!p.list_mode) {
+    if (!LIST) {
         d.T = p.tiles_per_buf;
         d.b = t / d.T;
         d.k = t - d.b * d.T;
         d.tbase = t - d.k;
-        ptr = p.base + d.b * p.stride;
-        n = p.len;
     } else {
         while (t >= wk.hi) {
             ++wk.b;
@@ -244,97 +132,15 @@ __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walke
         d.k = t - wk.lo;
         d.T = wk.hi - wk.lo;
         d.tbase = wk.lo;
-        ptr = sload64(p.d_ptrs + d.b);
-        n = sload64(p.d_lens + d.b);
     }
-    const uint64_t end = ptr + n;
-    const uint64_t H = (ptr + 15) & ~15ull;
-    const uint64_t Ea = end & ~15ull;
+    const Edges e = buffer_edges<LIST>(p, d.b);
+    const uint64_t mainlen = e.tail - e.headend;  // 0 when there is no 16-aligned main region
     const uint64_t tile_bytes = (uint64_t)p.seg * kWave;
-    uint64_t mainlen;
-    if (Ea > H) {
-        mainlen = Ea - H;
-        d.headend = H;
-        d.tail = Ea;
-        d.tail_len = (uint32_t)(end - Ea);
-    } else {
-        mainlen = 0;
-        d.headend = end;
-        d.tail = end;
-        d.tail_len = 0;
-    }
     const uint64_t pad = d.T * tile_bytes - mainlen;
-    d.ptr = ptr;
     d.pad = d.k == 0 ? (uint32_t)pad : 0u;
-    d.H = H;
-    d.vbase = H - pad + d.k * tile_bytes;
+    d.vbase = e.headend - pad + d.k * tile_bytes;
     d.ngroups = mainlen ? p.seg / kGroupBytes : 0u;
     return d;
-}
-
-// Payload groups are plain global loads (address space 1) into registers.  Everything else the
-// loop reads -- descriptors, seeds, head/tail bytes, the P columns -- is a scalar (SMEM) load that
-// retires on lgkmcnt, so the compiler's vmcnt accounting sees only the ring loads (and the combine
-// atomic) and can keep two groups in flight across tile boundaries.
-struct Group {
-    v4u v[kVecPerGroup];
-};
-typedef __attribute__((address_space(1))) const v4u gv4u;
-
-__device__ __forceinline__ void issue_group(Group &g, uint64_t a) {
-#pragma unroll
-    for (int i = 0; i < kVecPerGroup; ++i) g.v[i] = ((gv4u *)a)[i];
-}
-__device__ __forceinline__ void issue_group4(Group &g, uint64_t a0, uint64_t a1, uint64_t a2, uint64_t a3) {
-    g.v[0] = *(gv4u *)a0;
-    g.v[1] = *(gv4u *)a1;
-    g.v[2] = *(gv4u *)a2;
-    g.v[3] = *(gv4u *)a3;
-}
-template <int N>
-__device__ __forceinline__ void wait_group(Group &) {}
-
-__device__ __forceinline__ void load_group(Group &grp, const Tile &d, uint32_t g, uint32_t seg, int lane) {
-    const uint32_t vo0 = (uint32_t)lane * seg + g * kGroupBytes;
-    if (d.pad == 0) {
-        issue_group(grp, d.vbase + vo0);
-    } else {
-        // virtual zero bytes [0, pad): read a valid address (the main start) and zero in proc_group
-        uint64_t a[kVecPerGroup];
-#pragma unroll
-        for (int i = 0; i < kVecPerGroup; ++i) {
-            const uint32_t vo = vo0 + 16u * i;
-            a[i] = vo >= d.pad ? d.vbase + vo : d.H;
-        }
-        issue_group4(grp, a[0], a[1], a[2], a[3]);
-    }
-}
-
-template <class E>
-__device__ __forceinline__ typename E::T proc_group(typename E::T s, const Group &grp, const E &eng, const Tile &d,
-                                                   uint32_t g, uint32_t seg, int lane, typename E::T s_h) {
-    if (d.pad == 0) {
-#pragma unroll
-        for (int i = 0; i < kVecPerGroup; ++i) {
-            s = eng.word(s, grp.v[i].x);
-            s = eng.word(s, grp.v[i].y);
-            s = eng.word(s, grp.v[i].z);
-            s = eng.word(s, grp.v[i].w);
-        }
-    } else {
-        const uint32_t vo0 = (uint32_t)lane * seg + g * kGroupBytes;
-#pragma unroll
-        for (int i = 0; i < kVecPerGroup; ++i) {
-            const uint32_t vo = vo0 + 16u * i;
-            const uint32_t keep = vo >= d.pad ? ~0u : 0u;
-            if (vo == d.pad) s ^= s_h;  // lane state is 0 here: inject the head state
-            s = eng.word(s, grp.v[i].x & keep);
-            s = eng.word(s, grp.v[i].y & keep);
-            s = eng.word(s, grp.v[i].z & keep);
-            s = eng.word(s, grp.v[i].w & keep);
-        }
-    }
-    return s;
 }
 
 // bytes [a, end) folded into state s (a < end, both inside 16-aligned blocks read by SMEM)
@@ -355,16 +161,29 @@ __device__ __forceinline__ typename E::T fold_bytes(typename E::T s, uint64_t a,
     return s;
 }
 
-// head state of a buffer: ~seed advanced over the unaligned head bytes [ptr, headend)
-template <class E>
-__device__ __forceinline__ typename E::T head_state(const ScanParams &p, const Tile &d, const E &eng) {
+// head state of buffer b: ~seed advanced over the unaligned head bytes [ptr, headend)
+template <bool LIST, class E>
+__device__ __forceinline__ typename E::T head_state(const ScanParams &p, uint64_t b, const E &eng) {
     using T = typename E::T;
     uint64_t seed = p.seed_all;
     if (p.d_seeds)
-        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)p.d_seeds + d.b) : sload64((const uint64_t *)p.d_seeds + d.b);
+        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)p.d_seeds + b) : sload64((const uint64_t *)p.d_seeds + b);
     T s = (T)~seed;
-    if (d.headend > d.ptr) s = fold_bytes(s, d.ptr, d.headend, eng);
+    const Edges e = buffer_edges<LIST>(p, b);
+    if (e.headend > e.ptr) s = fold_bytes(s, e.ptr, e.headend, eng);
     return s;
+}
+
+// buffer b's register after its main region -> tail bytes, complement, store
+template <bool LIST, class E>
+__device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, const E &eng) {
+    const Edges e = buffer_edges<LIST>(p, b);
+    if (e.end > e.tail) fin = fold_bytes(fin, e.tail, e.end, eng);
+    fin = ~fin;
+    if (E::W == 32)
+        ((uint32_t *)p.d_out)[b] = (uint32_t)fin;
+    else
+        ((uint64_t *)p.d_out)[b] = (uint64_t)fin;
 }
 
 // r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time
@@ -393,232 +212,22 @@ __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
     return acc;
 }
 
-// A tile's contribution to the per-buffer accumulator is published with one device-scope atomic;
-// its returned value (who arrived last) is examined at the next tile boundary, by which time at
-// least one more payload group (4 loads) has been issued behind it: vmcnt(4) then covers it.
-struct Pending {
-    bool valid;
-    unsigned long long val, old;
-    uint64_t b, T_, tail;
-    uint32_t tail_len;
-};
-
 __device__ __forceinline__ unsigned long long atomic_xor_ret(unsigned long long *a, unsigned long long v) {
     return __hip_atomic_fetch_xor(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <class E>
-__device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, uint64_t tail, uint32_t tail_len, const E &eng) {
-    if (tail_len) fin = fold_bytes(fin, tail, tail + tail_len, eng);
-    fin = ~fin;
-    if (E::W == 32)
-        ((uint32_t *)p.d_out)[b] = (uint32_t)fin;
-    else
-        ((uint64_t *)p.d_out)[b] = (uint64_t)fin;
-}
-
-template <class E>
-__device__ __forceinline__ void resolve(const ScanParams &p, Pending &pd, const E &eng, int lane) {
-    using T = typename E::T;
-    if (!pd.valid) return;
-    pd.valid = false;
-    const unsigned long long old = rfl64(pd.old);  // lane 0 issued the atomic
-    const unsigned long long now = old ^ pd.val;
-    const unsigned long long full = pd.T_ == 32 ? 0xFFFFFFFF00000000ull : (((1ull << pd.T_) - 1) << 32);
-    if ((now & 0xFFFFFFFF00000000ull) == full) {
-        if (lane == 0) __hip_atomic_exchange(&p.d_acc[pd.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const T fin = (T)(uint32_t)now;
-        if (lane == 0) finalize(p, pd.b, fin, pd.tail, pd.tail_len, eng);
-    }
-}
-
-template <class E>
-__device__ __forceinline__ void finish_tile(const ScanParams &p, const Tile &d, typename E::T s, typename E::T s_h, const E &eng,
-                            int lane, Pending &pd) {
-    using T = typename E::T;
-    constexpr int W = E::W;
-    T r = 0;
-    if (d.ngroups) r = wave_xor(eng.mulK(s, lane));
-    if (d.T == 1) {
-        const T fin = d.ngroups ? r : s_h;
-        if (lane == 0) finalize(p, d.b, fin, d.tail, d.tail_len, eng);
-        return;
-    }
-    // move the (wave-uniform) tile partial to the buffer end: r * x^(8*TILE*(T-1-k))
-    const T v = mul_pcols<T, W>((T)rfl64((uint64_t)r), p.d_pcols + (d.T - 1 - d.k) * W);
-    resolve(p, pd, eng, lane);
-    if (W == 32 && d.T <= 32) {
-        // one 64-bit word per buffer: {arrival bit of each tile | XOR of the tile partials}
-        const unsigned long long val = (unsigned long long)(uint32_t)v | (1ull << (32 + d.k));
-        unsigned long long old = 0;
-        if (lane == 0) old = atomic_xor_ret(&p.d_acc[d.b], val);
-        pd.valid = true;
-        pd.val = val;
-        pd.old = old;
-        pd.b = d.b;
-        pd.T_ = d.T;
-        pd.tail = d.tail;
-        pd.tail_len = d.tail_len;
-    } else if (lane == 0) {
-        // wide state or more than 32 tiles: XOR, wait for it to be performed, then count arrivals
-        const unsigned long long old =
-            __hip_atomic_fetch_xor(&p.d_acc[d.b], (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::"v"(old) : "memory");
-        const unsigned int c = __hip_atomic_fetch_add(&p.d_cnt[d.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c == d.T - 1) {
-            const T fin = (T)__hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.d_cnt[d.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            finalize(p, d.b, fin, d.tail, d.tail_len, eng);
-        }
-    }
-}
-
-template <int ALG>
-__global__ __launch_bounds__(kBlock, 1) void crc_scan_kernel(const ScanParams p) {
-    using E = typename EngFor<ALG>::E;
-    using T = typename E::T;
-    __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
-    const uint32_t seg = p.seg;
-
-    Walker w0{0, 0, 0};
-    if (p.list_mode && t0 < t1) {
-        w0.b = sload64(p.d_wave_buf + gw);
-        w0.lo = sload64(p.d_tile_prefix + w0.b);
-        w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
-    }
-    // ---- prefetch cursor: the next (tile, group) to load; parks on the last group when exhausted
-    Walker wf = w0;
-    uint64_t tf = t0;
-    uint32_t gf = 0;
-    Tile df{};
-    bool any = false;
-    for (; tf < t1; ++tf) {
-        df = make_tile(p, tf, wf);
-        if (df.ngroups) {
-            any = true;
-            break;
-        }
-    }
-    bool pf_done = !any;
-    auto pf_advance = [&]() {
-        if (gf + 1 < df.ngroups) {
-            ++gf;
-            return;
-        }
-        if (pf_done) return;
-        Walker w2 = wf;
-        for (uint64_t t = tf + 1; t < t1; ++t) {
-            Tile d2 = make_tile(p, t, w2);
-            if (d2.ngroups) {
-                df = d2;
-                wf = w2;
-                tf = t;
-                gf = 0;
-                return;
-            }
-        }
-        pf_done = true;
-    };
-    // K data first (W=32: 8 bytes of the LDS K-matrix image per thread; W=64: this lane's K_l),
-    // then the first two payload groups, all before the LDS table build so their latency overlaps it
-    const uint64_t kq = *(const __attribute__((address_space(1))) uint64_t *)(E::kKmatInLds ? p.d_kvals + threadIdx.x
-                                                                                        : p.d_kvals + lane);
-    Group r0, r1, r2;
-    if (any) {
-        load_group(r0, df, gf, seg, lane);
-        pf_advance();
-        load_group(r1, df, gf, seg, lane);
-        pf_advance();
-    }
-
-    E::build(lds, p);
-    if (E::kKmatInLds) *(uint64_t *)(lds + kTabBytes + 8 * threadIdx.x) = kq;
-    // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched groups
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    E eng;
-    eng.init(lds, lane, p);
-    eng.kl = kq;
-    if (t0 >= t1) return;
-
-    // ---- scan cursor
-    Walker wp = w0;
-    uint64_t tp = t0;
-    uint32_t gp = 0;
-    Tile dp = make_tile(p, tp, wp);
-    T s_h = dp.k == 0 ? head_state(p, dp, eng) : (T)0;
-    T s = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : (T)0;
-    Pending pd{};
-    pd.valid = false;
-
-    // finish tiles whose groups are all scanned (and empty tiles); false once the wave is done
-    auto settle = [&]() -> bool {
-        while (gp >= dp.ngroups) {
-            if (p.dbg & 1) {
-                if (lane == 0) ((uint32_t *)p.d_out)[dp.b] = (uint32_t)s;  // timing experiment only
-            } else if (p.dbg & 2) {
-                const T r = wave_xor(eng.mulK(s, lane));
-                if (lane == 0) ((uint32_t *)p.d_out)[dp.b] = (uint32_t)r;
-            } else {
-                finish_tile(p, dp, s, s_h, eng, lane, pd);
-            }
-            if (++tp >= t1) return false;
-            dp = make_tile(p, tp, wp);
-            gp = 0;
-            s_h = dp.k == 0 ? head_state(p, dp, eng) : (T)0;
-            s = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : (T)0;
-        }
-        return true;
-    };
-
-    if (any) {
-        // three-slot ring, prefetch distance two groups; each step issues 4 loads, then waits
-        // for the oldest group with 8 younger loads allowed in flight
-        for (;;) {
-            load_group(r2, df, gf, seg, lane);
-            pf_advance();
-            if (!settle()) break;
-            wait_group<8>(r0);
-            s = proc_group(s, r0, eng, dp, gp++, seg, lane, s_h);
-
-            load_group(r0, df, gf, seg, lane);
-            pf_advance();
-            if (!settle()) break;
-            wait_group<8>(r1);
-            s = proc_group(s, r1, eng, dp, gp++, seg, lane, s_h);
-
-            load_group(r1, df, gf, seg, lane);
-            pf_advance();
-            if (!settle()) break;
-            wait_group<8>(r2);
-            s = proc_group(s, r2, eng, dp, gp++, seg, lane, s_h);
-        }
-    } else {
-        settle();
-    }
-    resolve(p, pd, eng, lane);
-}
-
-
 // ------------------------------------------------------------------------------------------
-// W = 32 braided scan (CRC32 / CRC32C): the production path for the 32-bit CRCs.
+// W = 32 braided scan (CRC32 / CRC32C).
 //
 // A tile of TILE bytes is R = TILE/256 rows of 256 bytes; lane l owns the 4-byte word at 4l of
-// every row, so each wave-wide load reads 256 contiguous bytes (fully coalesced: measured 8.0 TB/s
-// read-only on MI355X, where the lane-contiguous segments above reach about half of that).
-// Lane l's state u is one "braid" of the CRC:
+// every row, so each wave-wide load reads 256 contiguous bytes.  Lane l's state u is one braid:
 //     u <- (u ^ w_row) * x^(8*256)       (four lookups in T', whose entries fold in the skip over
 //                                          the other 63 lanes' words of the row)
 // After the R rows u = sum_c w_c * x^(8*256(R-c)), while word (c, l) belongs at x^(8(TILE-256c-4l))
 // relative to the tile end.  So u * x^(-32 l) is lane l's exact share (x is invertible mod P since
-// P(0) = 1): K_l = x^(-32 l), and the tile register is XOR_l u_l * K_l -- the same per-lane matrix
-// and wave reduction as the segment kernel, with no extra lookups per byte.
+// P(0) = 1): K_l = x^(-32 l), and the tile register is XOR_l u_l * K_l.
 //
-// LDS (76 KiB, so two 512-thread workgroups share a CU and a launch's prologue overlaps the previous
+// LDS (77 KiB, so two 512-thread workgroups share a CU and a launch's prologue overlaps the previous
 // launch's scan on the same CU):
 //   T' tables, 8 copies, quarter-rotated: the 256-byte row of entry e holds the four tables in
 //   quarters of 32 bytes (quarter q = the table indexed by byte q of a, i.e. T'_(3-q)), 8 copies
@@ -630,39 +239,14 @@ constexpr uint32_t kBKOff = kBTabBytes;               // K image, [j/4][lane][j%
 constexpr uint32_t kPcolOff = kBKOff + 8192;          // [m < 32][column j] of x^(8*TILE*m) (4 KiB)
 constexpr uint32_t kT0Off = kPcolOff + 4096;          // plain byte table (1 KiB; wave-uniform reads)
 constexpr uint32_t kConstFlagOff = kT0Off + 1024;     // waves that have published their K / P words
+constexpr uint32_t kPoolOff = kConstFlagOff + 4;      // workgroup tile pool: tiles claimed so far
 constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 constexpr int kBraidBlock = 512;                      // 8 waves; two workgroups per CU
 constexpr int kBraidWaves = kBraidBlock / kWave;
 
-typedef __attribute__((address_space(1))) const uint32_t gu32;
-typedef __attribute__((address_space(1))) const uint64_t gu64;
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ uint32_t xor_and(uint32_t acc, uint32_t c, uint32_t m) {  // acc ^ (c & m)
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(acc), "v"(c), "v"(m));
-    return r;
-}
-
-// XOR over the 64 lanes, returned wave-uniform: two quad_perm and two row_ror DPP steps leave each
-// 16-lane row's XOR in all its lanes; four readlanes finish in scalar registers.
-__device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
-    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
-                      __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
-}
-
 // Compile-time GF(2) bases of the braided scan's byte tables: entry e of a table is the XOR of the
 // basis values of e's set bits (the tables are linear in e), so the tables are built from
-// immediates with no memory traffic -- at launch the constant block is usually evicted by the
-// previous launch's stream and would take several microseconds to arrive.
+// immediates with no memory traffic.
 //   b[k][i] = T'_k[1 << i] = (1 << i) * x^(8(k+1)) * x^(8*252)     (k < 4)
 //   b[4][i] = T_0[1 << i]  = (1 << i) * x^8
 template <uint32_t POLY>
@@ -760,41 +344,18 @@ __device__ __forceinline__ uint32_t ldpay(uint64_t a) {
     return *(gu32 *)a;
 }
 
-// group gi of tile d: rows [16 gi, 16 gi + 16), this lane's word of each (virtual offset
+// group gi of a tile: rows [16 gi, 16 gi + 16), this lane's word of each (virtual offset
 // gi*4096 + 256 r + 4 lane).  Words in the virtual front pad read a valid address (the main start)
-// and are zeroed by braid_proc.
+// and are zeroed by braid_proc.  Rows go out in order on every path (scheduling barriers): the
+// compiler's vmcnt bookkeeping merges paths, and one path with row 0 issued late would make every
+// wait for row 0 drain the whole group.
 template <bool NT>
-__device__ __forceinline__ void braid_load(BGroup &g, const Tile &d, uint32_t gi, int lane) {
-    const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
-    // rows go out in order on every path (scheduling barriers), as in braid_fused: the compiler's
-    // vmcnt bookkeeping merges paths, and one path with row 0 issued late would make every wait
-    // for row 0 drain the whole group
-    if (d.pad == 0) {
-        const uint64_t a = d.vbase + vo0;
-#pragma unroll
-        for (int r = 0; r < kBraidRowsPerGroup; ++r) {
-            g.w[r] = ldpay<NT>(a + kBraidRow * r);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < kBraidRowsPerGroup; ++r) {
-            const uint32_t vo = vo0 + kBraidRow * r;
-            g.w[r] = ldpay<NT>(vo >= d.pad ? d.vbase + vo : d.H);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-}
-
-// Prologue loads: one code path for padded and unpadded tiles (a per-row address select), so the
-// compiler sees a single load sequence and waits only for the constants before the LDS build.
-template <bool NT>
-__device__ __forceinline__ void braid_prime(BGroup &g, uint64_t vbase, uint64_t H, uint32_t pad, uint32_t gi, int lane) {
+__device__ __forceinline__ void braid_load(BGroup &g, uint64_t vbase, uint32_t pad, uint32_t gi, int lane) {
     const uint32_t vo0 = gi * (kBraidRow * kBraidRowsPerGroup) + 4u * lane;
 #pragma unroll
     for (int r = 0; r < kBraidRowsPerGroup; ++r) {
         const uint32_t vo = vo0 + kBraidRow * r;
-        g.w[r] = ldpay<NT>(vo >= pad ? vbase + vo : H);
+        g.w[r] = ldpay<NT>(vbase + (vo >= pad ? vo : pad));
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -843,17 +404,17 @@ __device__ __forceinline__ uint32_t braid_fused(uint32_t u, const BGroup &g, BGr
 
 // Cross-tile combine.  Tiles form groups of 32; tile k's register is moved to its group's end
 // (r * x^(8*TILE*m), m < 32: columns in LDS, one per lane).  A wave merges the shares of its own
-// consecutive tiles of one group in registers {arrival bits | XOR} and publishes them with one
-// 64-bit atomic XOR into the group's slot when it moves to another group or runs out of tiles.
-// Whoever completes the slot's arrival bits finishes the buffer (T <= 32), or moves the group value
-// to the buffer end (scalar column table, once per group) and XORs it into the buffer word, counting
-// groups (T > 32).  At most 32 atomics meet on one address, and a wave waits for a returned value
-// only when it publishes its next group (rare) or at its end.
+// tiles of one group in registers {arrival bits | XOR} and publishes them with one 64-bit atomic XOR
+// into the group's slot when it moves to another group or runs out of tiles.  Whoever completes the
+// slot's arrival bits finishes the buffer (T <= 32), or moves the group value to the buffer end
+// (scalar column table, once per group) and XORs it into the buffer word, counting groups (T > 32).
+// At most 32 atomics meet on one address, and a wave waits for a returned value only when it
+// publishes its next group (rare) or at its end.
 struct BGroupAcc {
     uint64_t slot;  // ~0: no open group
     unsigned long long val;
-    uint64_t b, G, shift, tail;
-    uint32_t n, tail_len;
+    uint64_t b, T;
+    uint32_t g0;  // first tile of the group within its buffer
 };
 struct BPending {
     bool valid;
@@ -861,37 +422,38 @@ struct BPending {
     BGroupAcc g;
 };
 
-template <class B>
+template <bool LIST, class B>
 __device__ __forceinline__ void braid_resolve(const ScanParams &p, BPending &pd, const B &eng, int lane) {
     if (!pd.valid) return;
     pd.valid = false;
     const unsigned long long now = rfl64(pd.old) ^ pd.val;
     const BGroupAcc &g = pd.g;
-    const unsigned long long full = g.n >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << g.n) - 1) << 32);
+    const uint64_t n = g.T - g.g0 < 32 ? g.T - g.g0 : 32, G = (g.T + 31) / 32, shift = g.T - g.g0 - n;
+    const unsigned long long full = n >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << n) - 1) << 32);
     if ((now & 0xFFFFFFFF00000000ull) != full) return;
     uint32_t grp = (uint32_t)now;
-    if (g.G > 1 && g.shift) grp = mul_pcols<uint32_t, 32>(grp, p.d_pcols + g.shift * 32);
+    if (G > 1 && shift) grp = mul_pcols<uint32_t, 32>(grp, p.d_pcols + shift * 32);
     if (lane != 0) return;
     __hip_atomic_exchange(&p.d_acc1[g.slot], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (g.G == 1) {
-        finalize(p, g.b, grp, g.tail, g.tail_len, eng);
+    if (G == 1) {
+        finalize<LIST>(p, g.b, grp, eng);
         return;
     }
     const unsigned long long o =
         __hip_atomic_fetch_xor(&p.d_acc[g.b], (unsigned long long)grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::"v"(o) : "memory");  // performed before it is counted
     const unsigned int c = __hip_atomic_fetch_add(&p.d_cnt[g.b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c == g.G - 1) {
+    if (c == G - 1) {
         const uint32_t fin = (uint32_t)__hip_atomic_exchange(&p.d_acc[g.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&p.d_cnt[g.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        finalize(p, g.b, fin, g.tail, g.tail_len, eng);
+        finalize<LIST>(p, g.b, fin, eng);
     }
 }
 
-template <class B>
+template <bool LIST, class B>
 __device__ __forceinline__ void braid_publish(const ScanParams &p, BGroupAcc &acc, BPending &pd, const B &eng, int lane) {
     if (acc.slot == ~0ull) return;
-    braid_resolve(p, pd, eng, lane);
+    braid_resolve<LIST>(p, pd, eng, lane);
     unsigned long long old = 0;
     if (lane == 0) old = atomic_xor_ret(&p.d_acc1[acc.slot], acc.val);
     pd.valid = true;
@@ -901,16 +463,12 @@ __device__ __forceinline__ void braid_publish(const ScanParams &p, BGroupAcc &ac
     acc.slot = ~0ull;
 }
 
-template <class B>
+template <bool LIST, class B>
 __device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d, uint32_t u, uint32_t s_h, const B &eng, int lane,
-                             BGroupAcc &acc, BPending &pd) {
-    if (p.dbg & 1) {  // timing experiments only (AMDCRC_DEBUG): results are invalid
-        if (lane == 0) ((uint32_t *)p.d_out)[d.b] = u;
-        return;
-    }
+                                             BGroupAcc &acc, BPending &pd) {
     const uint32_t r = d.ngroups ? wave_xor_s(eng.mulK(u, lane)) : 0u;
     if (d.T == 1) {
-        if (lane == 0) finalize(p, d.b, d.ngroups ? r : s_h, d.tail, d.tail_len, eng);
+        if (lane == 0) finalize<LIST>(p, d.b, d.ngroups ? r : s_h, eng);
         return;
     }
     // r * x^(8*TILE*m) to the group end: lane j < 32 takes column j if bit (31 - j) of r is set
@@ -921,28 +479,45 @@ __device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d,
     const uint32_t v = wave_xor_s(colv & sel);
     const uint64_t slot = d.tbase + g0;
     if (slot != acc.slot) {
-        braid_publish(p, acc, pd, eng, lane);
+        braid_publish<LIST>(p, acc, pd, eng, lane);
         acc.slot = slot;
         acc.val = 0;
         acc.b = d.b;
-        acc.n = (uint32_t)(gend - g0);
-        acc.G = (d.T + 31) / 32;
-        acc.shift = d.T - gend;
-        acc.tail = d.tail;
-        acc.tail_len = d.tail_len;
+        acc.T = d.T;
+        acc.g0 = (uint32_t)g0;
     }
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY, bool BITOP3 = true, int RATE = 1, bool NT = true>
-__global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanParams p) {
+template <uint32_t POLY, bool LIST, bool BITOP3 = true, bool NT = true>
+__global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanParams p) {
     using B = Braid32<POLY, BITOP3>;
     __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
 
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
-    const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
+    // Tiles.  Static: an even split of [0, ntiles) over the waves.  Workgroup pool (p.nstatic != 0,
+    // uniform batches): the workgroup's even share [wb0, wb1) is split into one static tile per wave
+    // and a pool the waves claim from an LDS counter as they run dry, so a wave the memory system
+    // serves late scans less of its workgroup's share.
+    const bool dyn = !LIST && p.nstatic != 0;
+    uint64_t t0, t1, pool_base = 0, pool_size = 0;
+    if (dyn) {
+        const uint64_t wb0 = (uint64_t)blockIdx.x * p.ntiles / gridDim.x, wb1 = ((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x;
+        const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
+        t0 = wb0 + wv < wb1 ? wb0 + wv : wb1;
+        t1 = wb0 + wv < wb1 ? t0 + 1 : wb1;
+        pool_base = wb0 + kBraidWaves;
+        pool_size = pool_base < wb1 ? wb1 - pool_base : 0;
+    } else {
+        t0 = gw * p.ntiles / nw;
+        t1 = (gw + 1) * p.ntiles / nw;
+    }
+    t0 = rfl64(t0), t1 = rfl64(t1);
+    // tiles entered by the prefetch cursor from the pool, in order, for the scan cursor
+    uint64_t fifo0 = 0, fifo1 = 0;
+    uint32_t fifo_n = 0;
     // diagnostics: per-wave timeline (start, tables built, scan done, exit) on the 100 MHz clock
     const bool stamps = p.d_timeline != nullptr;
     auto stamp = [&](int i) {
@@ -951,39 +526,56 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
     stamp(0);
 
     Walker w0{0, 0, 0};
-    if (p.list_mode && t0 < t1) {
+    if (LIST && t0 < t1) {
         w0.b = sload64(p.d_wave_buf + gw);
         w0.lo = sload64(p.d_tile_prefix + w0.b);
         w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
     }
-    // ---- prefetch cursor: the next (tile, group) to load; parks on the last group when exhausted
+    // ---- prefetch cursor: the next (tile, group) to load; pf_done once every group is in flight
     Walker wf = w0;
     uint64_t tf = t0;
     uint32_t gf = 0;
-    Tile df{};
+    uint64_t fvb = 0;  // the cursor tile's vbase, pad and group count
+    uint32_t fpad = 0, fng = 0;
     bool any = false;
     for (; tf < t1; ++tf) {
-        df = make_tile(p, tf, wf);
-        if (df.ngroups) {
+        const Tile d = make_tile<LIST>(p, tf, wf);
+        if (d.ngroups) {
+            fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
             any = true;
             break;
         }
     }
     bool pf_done = !any;
     auto pf_advance = [&]() {
-        if (gf + 1 < df.ngroups) {
+        if (gf + 1 < fng) {
             ++gf;
             return;
         }
         if (pf_done) return;
         Walker w2 = wf;
         for (uint64_t t = tf + 1; t < t1; ++t) {
-            Tile d2 = make_tile(p, t, w2);
-            if (d2.ngroups) {
-                df = d2;
+            const Tile d = make_tile<LIST>(p, t, w2);
+            if (d.ngroups) {
+                fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
                 wf = w2;
                 tf = t;
                 gf = 0;
+                return;
+            }
+        }
+        if (pool_size) {
+            uint32_t v = 0;
+            if (lane == 0) v = __hip_atomic_fetch_add((uint32_t *)(lds + kPoolOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            v = __builtin_amdgcn_readfirstlane(v);
+            if (v < pool_size) {
+                const uint64_t t = pool_base + v;
+                const Tile d = make_tile<LIST>(p, t, w2);
+                fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
+                tf = t;
+                gf = 0;
+                if (fifo_n == 0) fifo0 = t; else fifo1 = t;
+                ++fifo_n;
                 return;
             }
         }
@@ -994,20 +586,14 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
     const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + 4 * threadIdx.x);  // 16 B of the 8 KiB image
     const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
     const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
-    // prime the first group unconditionally (a wave without payload reads the constant block)
+    // prime the first group unconditionally (a wave without payload reads the 13 KiB constant block).
+    // Only one group is primed, before the table build: issuing a load stalls the wave while the
+    // memory system is saturated (every CU primes at once), so priming two groups kept the first scan
+    // waiting for 8 KiB per wave to be accepted.  The ring scans group 0 while group 1's loads go out
+    // between its table steps.
     BGroup r0, r1;
-    {
-        // field-wise selects (selecting whole Tile structs put them in scratch)
-        const uint64_t zb = (uint64_t)p.d_kvals;  // 13 KiB: a group of this lane's words stays inside
-        const uint64_t vb0 = any ? df.vbase : zb, h0 = any ? df.H : zb;
-        const uint32_t pad0 = any ? df.pad : 0u, g0 = any ? gf : 0u;
-        if (any) pf_advance();
-        // Only the first group is primed, before the table build: issuing a load stalls the wave
-        // while the memory system is saturated (every CU primes at once), so priming two groups
-        // kept the first scan waiting for 8 KiB per wave to be accepted.  The ring scans group 0
-        // while group 1's loads go out between its table steps.
-        braid_prime<NT>(r0, vb0, h0, pad0, g0, lane);
-    }
+    braid_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
+    if (any && !dyn) pf_advance();  // pool mode: after the barrier, where the pool counter is set up
     {
         // T' (4 tables x 256 entries, 8 copies each) and T0 from the compile-time bases.  One 16-byte
         // store = 4 copies of one (table, entry); the 8 lanes of a ds_write_b128 group take the 8
@@ -1027,14 +613,18 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
         }
         if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
         if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
+        if (i == 0) *(uint32_t *)(lds + kPoolOff) = 0u;
     }
-    stamp(4);  // constants arrived, LDS stores issued
-    // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched groups
+    stamp(4);  // LDS stores issued
+    // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched group
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
+    // pool mode: the prefetch cursor may reach the pool only now (the host gives every wave of a
+    // pooled launch a static tile with payload, so a wave's pool tiles always follow it)
+    if (dyn && any) pf_advance();
     stamp(1);
-    // Every wave publishes its 1/16 of the K image and P columns once its constants have arrived
+    // Every wave publishes its 1/8 of the K image and P columns once its constants have arrived
     // (after its first group, by which time they have: loads retire in order) and counts itself in
     // LDS; a wave spins on the count only before its first tile finish.  A wave without work
     // publishes before leaving, so the count always completes.
@@ -1064,22 +654,38 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
     Walker wp = w0;
     uint64_t tp = t0;
     uint32_t gp = 0;
-    Tile dp = make_tile(p, tp, wp);
-    uint32_t s_h = dp.k == 0 ? head_state(p, dp, eng) : 0u;
+    Tile dp = make_tile<LIST>(p, tp, wp);
+    uint32_t s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0u;
     uint32_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
     BPending pd{};
     pd.valid = false;
     BGroupAcc acc{};
     acc.slot = ~0ull;
 
+    // the scan cursor's next tile: the static range, then the pool tiles the prefetch cursor entered
+    bool scan_pool = false;
+    auto next_scan = [&]() -> bool {
+        if (!scan_pool) {
+            if (++tp < t1) {
+                dp = make_tile<LIST>(p, tp, wp);
+                return true;
+            }
+            scan_pool = true;
+        }
+        if (fifo_n == 0) return false;
+        tp = fifo0;
+        fifo0 = fifo1;
+        --fifo_n;
+        dp = make_tile<LIST>(p, tp, wp);
+        return true;
+    };
     auto settle = [&]() -> bool {
         while (gp >= dp.ngroups) {
             await_consts();
-            braid_finish(p, dp, u, s_h, eng, lane, acc, pd);
-            if (++tp >= t1) return false;
-            dp = make_tile(p, tp, wp);
+            braid_finish<LIST>(p, dp, u, s_h, eng, lane, acc, pd);
+            if (!next_scan()) return false;
             gp = 0;
-            s_h = dp.k == 0 ? head_state(p, dp, eng) : 0u;
+            s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0u;
             u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
         }
         return true;
@@ -1091,10 +697,10 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
     auto ring_step = [&](const BGroup &cur, BGroup &dst) {
         if (pf_done) {
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
-        } else if (dp.pad == 0 && df.pad == 0) {
-            u = braid_fused<RATE, NT>(u, cur, dst, df.vbase + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
+        } else if (dp.pad == 0 && fpad == 0) {
+            u = braid_fused<1, NT>(u, cur, dst, fvb + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
         } else {
-            braid_load<NT>(dst, df, gf, lane);
+            braid_load<NT>(dst, fvb, fpad, gf, lane);
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
         }
         ++gp;
@@ -1120,13 +726,13 @@ __global__ __launch_bounds__(kBraidBlock, 2) void crc32_braid_kernel(const ScanP
     }
     publish_consts();
     stamp(2);
-    braid_publish(p, acc, pd, eng, lane);
-    braid_resolve(p, pd, eng, lane);
+    braid_publish<LIST>(p, acc, pd, eng, lane);
+    braid_resolve<LIST>(p, pd, eng, lane);
     stamp(3);
 }
 
 // ------------------------------------------------------------------------------------------
-// W = 64 braided scan (CRC64NVME): the production path for the 64-bit CRC.
+// W = 64 braided scan (CRC64NVME).
 //
 // The W=32 braid with 8-byte words: a row is 512 bytes, lane l owns the word at 8l (one
 // global_load_dwordx2 per row, 512 contiguous bytes per wave instruction), and
@@ -1147,8 +753,6 @@ constexpr int kB64RowsPerGroup = 8;                 // 4 KiB per wave per ring s
 constexpr uint32_t kB64TabBytes = 131072;
 constexpr uint32_t kB64T0Off = kB64TabBytes;        // plain byte table, 256 x u64 (head / tail)
 constexpr uint32_t kB64Lds = kB64T0Off + 2048;
-
-typedef __attribute__((address_space(1))) const uint64_t gu64c;
 
 template <uint64_t POLY>
 struct Braid64Basis {
@@ -1243,19 +847,19 @@ struct B64Group {
 
 template <bool NT>
 __device__ __forceinline__ uint64_t ldpay64(uint64_t a) {
-    if (NT) return __builtin_nontemporal_load((gu64c *)a);
-    return *(gu64c *)a;
+    if (NT) return __builtin_nontemporal_load((gu64 *)a);
+    return *(gu64 *)a;
 }
 
-// group gi of tile d: rows [8 gi, 8 gi + 8), this lane's word of each (virtual offset
+// group gi of a tile: rows [8 gi, 8 gi + 8), this lane's word of each (virtual offset
 // gi*4096 + 512 r + 8 lane); words in the virtual front pad read the main start and are zeroed later
 template <bool NT>
-__device__ __forceinline__ void b64_load(B64Group &g, uint64_t vbase, uint64_t H, uint32_t pad, uint32_t gi, int lane) {
+__device__ __forceinline__ void b64_load(B64Group &g, uint64_t vbase, uint32_t pad, uint32_t gi, int lane) {
     const uint32_t vo0 = gi * (kB64Row * kB64RowsPerGroup) + 8u * lane;
 #pragma unroll
     for (int r = 0; r < kB64RowsPerGroup; ++r) {
         const uint32_t vo = vo0 + kB64Row * r;
-        g.w[r] = ldpay64<NT>(vo >= pad ? vbase + vo : H);
+        g.w[r] = ldpay64<NT>(vbase + (vo >= pad ? vo : pad));
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -1293,19 +897,14 @@ __device__ __forceinline__ uint64_t b64_fused(uint64_t u, const B64Group &g, B64
     return x;
 }
 
-__device__ __forceinline__ uint64_t wave_xor64_s(uint64_t v) {
-    const uint32_t lo = wave_xor_s((uint32_t)v), hi = wave_xor_s((uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
 // Tile finish: lane shares -> tile register -> its 32-tile group slot (value XOR, then arrival
 // count); the group's last arrival moves the group value to the buffer end and XORs it into the
 // buffer word (count of groups); the buffer's last group finalises.
-template <class B>
+template <bool LIST, class B>
 __device__ __forceinline__ void b64_finish(const ScanParams &p, const Tile &d, uint64_t u, uint64_t s_h, const B &eng, int lane) {
     const uint64_t r = d.ngroups ? wave_xor64_s(eng.mulK(u)) : 0ull;
     if (d.T == 1) {
-        if (lane == 0) finalize(p, d.b, d.ngroups ? r : s_h, d.tail, d.tail_len, eng);
+        if (lane == 0) finalize<LIST>(p, d.b, d.ngroups ? r : s_h, eng);
         return;
     }
     const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
@@ -1328,7 +927,7 @@ __device__ __forceinline__ void b64_finish(const ScanParams &p, const Tile &d, u
     gv = rfl64(gv);
     const uint64_t G = (d.T + 31) / 32;
     if (G == 1) {
-        if (lane == 0) finalize(p, d.b, (uint64_t)gv, d.tail, d.tail_len, eng);
+        if (lane == 0) finalize<LIST>(p, d.b, (uint64_t)gv, eng);
         return;
     }
     const uint64_t gs = d.T > gend ? mul_pcols<uint64_t, 64>((uint64_t)gv, p.d_pcols + (d.T - gend) * 64) : (uint64_t)gv;
@@ -1340,12 +939,12 @@ __device__ __forceinline__ void b64_finish(const ScanParams &p, const Tile &d, u
         if (c2 == (unsigned int)(G - 1)) {
             const uint64_t fin = __hip_atomic_exchange(&p.d_acc[d.b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&p.d_cnt[d.b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            finalize(p, d.b, fin, d.tail, d.tail_len, eng);
+            finalize<LIST>(p, d.b, fin, eng);
         }
     }
 }
 
-template <uint64_t POLY, bool NT = true>
+template <uint64_t POLY, bool LIST, bool NT = true>
 __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams p) {
     using B = Braid64<POLY>;
     __shared__ __attribute__((aligned(16))) char lds[kB64Lds];
@@ -1356,7 +955,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
 
     Walker w0{0, 0, 0};
-    if (p.list_mode && t0 < t1) {
+    if (LIST && t0 < t1) {
         w0.b = sload64(p.d_wave_buf + gw);
         w0.lo = sload64(p.d_tile_prefix + w0.b);
         w0.hi = sload64(p.d_tile_prefix + w0.b + 1);
@@ -1365,27 +964,29 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     Walker wf = w0;
     uint64_t tf = t0;
     uint32_t gf = 0;
-    Tile df{};
+    uint64_t fvb = 0;
+    uint32_t fpad = 0, fng = 0;
     bool any = false;
     for (; tf < t1; ++tf) {
-        df = make_tile(p, tf, wf);
-        if (df.ngroups) {
+        const Tile d = make_tile<LIST>(p, tf, wf);
+        if (d.ngroups) {
+            fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
             any = true;
             break;
         }
     }
     bool pf_done = !any;
     auto pf_advance = [&]() {
-        if (gf + 1 < df.ngroups) {
+        if (gf + 1 < fng) {
             ++gf;
             return;
         }
         if (pf_done) return;
         Walker w2 = wf;
         for (uint64_t t = tf + 1; t < t1; ++t) {
-            Tile d2 = make_tile(p, t, w2);
-            if (d2.ngroups) {
-                df = d2;
+            const Tile d = make_tile<LIST>(p, t, w2);
+            if (d.ngroups) {
+                fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
                 wf = w2;
                 tf = t;
                 gf = 0;
@@ -1394,14 +995,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
         }
         pf_done = true;
     };
-    const uint64_t kl = *(gu64c *)(p.d_kvals + lane);
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
     // prime the first group (a wave without payload reads the 16 KiB constant block)
     B64Group r0, r1;
-    {
-        const uint64_t zb = (uint64_t)p.d_kvals;
-        b64_load<NT>(r0, any ? df.vbase : zb, any ? df.H : zb, any ? df.pad : 0u, any ? gf : 0u, lane);
-        if (any) pf_advance();
-    }
+    b64_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
+    if (any) pf_advance();
     {
         // T'_t: two waves per table (t wave-uniform), each thread two entries x 8 copies; T0
         const uint32_t i = threadIdx.x, wv = i >> 6;
@@ -1428,17 +1026,17 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     Walker wp = w0;
     uint64_t tp = t0;
     uint32_t gp = 0;
-    Tile dp = make_tile(p, tp, wp);
-    uint64_t s_h = dp.k == 0 ? head_state(p, dp, eng) : 0ull;
+    Tile dp = make_tile<LIST>(p, tp, wp);
+    uint64_t s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0ull;
     uint64_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
 
     auto settle = [&]() -> bool {
         while (gp >= dp.ngroups) {
-            b64_finish(p, dp, u, s_h, eng, lane);
+            b64_finish<LIST>(p, dp, u, s_h, eng, lane);
             if (++tp >= t1) return false;
-            dp = make_tile(p, tp, wp);
+            dp = make_tile<LIST>(p, tp, wp);
             gp = 0;
-            s_h = dp.k == 0 ? head_state(p, dp, eng) : 0ull;
+            s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0ull;
             u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
         }
         return true;
@@ -1446,10 +1044,10 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     auto ring_step = [&](const B64Group &cur, B64Group &dst) {
         if (pf_done) {
             u = b64_proc(u, cur, eng, dp, gp, lane, s_h);
-        } else if (dp.pad == 0 && df.pad == 0) {
-            u = b64_fused<NT>(u, cur, dst, df.vbase + gf * (kB64Row * kB64RowsPerGroup) + 8u * lane, eng);
+        } else if (dp.pad == 0 && fpad == 0) {
+            u = b64_fused<NT>(u, cur, dst, fvb + gf * (kB64Row * kB64RowsPerGroup) + 8u * lane, eng);
         } else {
-            b64_load<NT>(dst, df.vbase, df.H, df.pad, gf, lane);
+            b64_load<NT>(dst, fvb, fpad, gf, lane);
             u = b64_proc(u, cur, eng, dp, gp, lane, s_h);
         }
         ++gp;
@@ -1583,21 +1181,29 @@ static void launch(K kernel, int nblocks, int threads, hipStream_t s, const Scan
 
 extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, void *stream, void *const *ev) {
     hipStream_t s = (hipStream_t)stream;
+    const bool list = p->list_mode != 0;
     switch (alg) {
-        case ALG_CRC32: launch(crc32_braid_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev); break;
-        case ALG_CRC32C:
-            if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
-                launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->dbg & 1024)  // diagnostics: cached (temporal) payload loads
-                launch(crc32_braid_kernel<kPoly32C, true, 1, false>, nblocks, kBraidBlock, s, p, ev);
+        case ALG_CRC32:
+            if (list)
+                launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
-                launch(crc32_braid_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
+                launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
+            break;
+        case ALG_CRC32C:
+            if (list)
+                launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
+            else if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
+                launch(crc32_braid_kernel<kPoly32C, false, false>, nblocks, kBraidBlock, s, p, ev);
+            else if (p->dbg & 1024)  // diagnostics: cached (temporal) payload loads
+                launch(crc32_braid_kernel<kPoly32C, false, true, false>, nblocks, kBraidBlock, s, p, ev);
+            else
+                launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (p->dbg & 2048)  // diagnostics: the first-generation lane-segment scan
-                launch(crc_scan_kernel<ALG_CRC64NVME>, nblocks, kBlock, s, p, ev);
+            if (list)
+                launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);
             else
-                launch(crc64_braid_kernel<kPoly64Nvme>, nblocks, kBlock, s, p, ev);
+                launch(crc64_braid_kernel<kPoly64Nvme, false>, nblocks, kBlock, s, p, ev);
             break;
         default: return -1;
     }

@@ -58,6 +58,7 @@ struct Workspace {
     unsigned int *cnt = nullptr;         // per buffer
     unsigned long long *acc1 = nullptr;  // per tile (32-tile group slots of the braided scans)
     unsigned int *cnt1 = nullptr;        // per tile (W=64 group arrival counts)
+    unsigned int *claim = nullptr;       // dynamic tile pool: 2 words per shard
     size_t cap = 0, cap_tiles = 0;
 };
 
@@ -269,6 +270,12 @@ int get_workspace(Device *d, hipStream_t s, size_t nbuf, size_t ntiles, Workspac
         HIP_TRY(hipDeviceSynchronize());
         w.cap_tiles = cap;
     }
+    if (!w.claim) {
+        const size_t words = 2 * 1024;  // >= 2 x (max workgroups / kShardBlocks)
+        HIP_TRY(hipMalloc((void **)&w.claim, words * sizeof(unsigned int)));
+        HIP_TRY(hipMemset(w.claim, 0, words * sizeof(unsigned int)));
+        HIP_TRY(hipDeviceSynchronize());
+    }
     if (w.cap < nbuf) {
         size_t cap = std::max<size_t>(nbuf, w.cap * 2);
         if (w.acc) {
@@ -298,8 +305,9 @@ inline uint64_t main_len(uint64_t ptr, uint64_t n) {
 // Bytes per lane per tile.  A tile is 64*seg bytes; pick the largest seg (fewest partials to
 // combine) that still gives every wavefront slot on the chip a tile and does not exceed the
 // typical buffer.
-uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main) {
-    const uint64_t slots = (uint64_t)d->cus * kWavesPerBlock;
+// typical buffer.  per_slot: tiles wanted per wave slot (2 when a dynamic pool balances the waves).
+uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main, uint64_t per_slot = 1) {
+    const uint64_t slots = (uint64_t)d->cus * kWavesPerBlock * per_slot;
     uint64_t seg = 4096;
     while (seg > kGroupBytes && (total_main / (seg * kWave) < slots || seg * kWave > std::max<uint64_t>(typical_main, 1)))
         seg >>= 1;
@@ -365,7 +373,8 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     p.d_cnt = nullptr;
     p.d_acc1 = nullptr;
     p.d_cnt1 = nullptr;
-    if (tmax > 1) {
+    p.d_claim = nullptr;
+    if (tmax > 1 || p.nstatic) {
         if ((rc = get_pcols(d, alg, tile, tmax, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
         Workspace *w;
@@ -374,6 +383,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_cnt = w->cnt;
         p.d_acc1 = w->acc1;
         p.d_cnt1 = w->cnt1;
+        p.d_claim = w->claim;
     }
     const uint64_t blocks = scan_geometry(d, alg, p.ntiles).blocks;
     if (blocks == 0) return 0;
@@ -403,7 +413,13 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     std::lock_guard<std::mutex> g(d->mu);
     const uint64_t ml = main_len(base, len);
     ScanParams p{};
-    p.seg = choose_seg(d, ml * count, ml);
+    // W=32: every wave scans one static tile, then claims tiles from its shard's pool, so waves the
+    // memory system serves late take less of the batch (dynamic tile pool)
+    // Only where the pool does not shrink the tiles: smaller tiles cost a tile finish per 8 KiB and
+    // measured slower on 1024 x 64 KiB (3704 vs 4380 GiB/s), while on 16 x 256 MiB and 131072 x 8 KiB
+    // the pool gains 3-4 % at equal tiles.
+    p.seg = choose_seg(d, ml * count, ml, 1);
+    const bool pool = width_of(alg) == 32 && ml > 0 && !(debug_flags() & 4096) && choose_seg(d, ml * count, ml, 2) == p.seg;
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const uint64_t T = ml ? (ml + tile - 1) / tile : 1;
     p.base = base;
@@ -415,6 +431,11 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     p.d_seeds = d_seeds;
     p.seed_all = seed_all;
     p.d_out = d_out;
+    if (pool) {
+        // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
+        const ScanGeometry geo = scan_geometry(d, alg, p.ntiles);
+        if (p.ntiles >= 2 * geo.blocks * geo.waves_per_block) p.nstatic = geo.blocks * geo.waves_per_block;
+    }
     return launch_scan(d, alg, p, count, T, s);
 }
 

@@ -49,6 +49,12 @@ struct ScanParams {
     unsigned long long *d_acc1;    // braided scans: per tile (slot of each 32-tile group)
     unsigned int *d_cnt1;          // W=64 braided scan: per tile (arrivals of each 32-tile group)
     unsigned long long *d_timeline; // diagnostics (AMDCRC_DEBUG bit 4): 4 s_memrealtime stamps per wave
+    // ---- dynamic tile pool (W=32 braided scan, strided batches): tiles [0, nstatic) are split
+    // statically over the waves; tiles [nstatic, ntiles) are claimed at run time, per shard of
+    // kShardBlocks workgroups, from d_claim[2 * shard] (claims) / [2 * shard + 1] (waves done)
+    uint64_t nstatic;               // 0: no dynamic pool (every tile static)
+    uint64_t dyn_chunk;             // pool tiles per shard
+    unsigned int *d_claim;          // 2 words per shard, zero on entry, left zero on exit
 };
 
 // W=32 braided scan constants (engine.cpp get_braid_consts), u32 words:
@@ -56,6 +62,7 @@ struct ScanParams {
 //   [2048, 3072)  T'_k[e] = e * x^(8(k+1) + 8*252): slice-by-4 step that also skips the other
 //                 63 lanes' words of a 256-byte row
 //   [3072, 3328)  T_0[e] = e * x^8: plain byte step for head / tail bytes
+constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
 constexpr int kBraidConstWords = 3328;
