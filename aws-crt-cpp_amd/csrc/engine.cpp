@@ -316,15 +316,27 @@ uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main,
 
 inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 
-// Launch geometry of the scan kernels: the W=32 braided scan runs two 512-thread workgroups per CU
-// (8 waves each), the W=64 scan one 1024-thread workgroup per CU.  Either way 16 wave slots per CU.
+// Launch geometry of the scan kernels.  The W=32 braided scan runs 512-thread workgroups (8 waves,
+// 77 KiB LDS), two of which fit a CU.  A small batch (under 256 MiB of main bytes) launches one per
+// CU: a single launch then takes 6 % longer (19.0 vs 17.9 us for 1024 x 64 KiB), but launches queued
+// on other streams find a free workgroup slot on every CU, so one launch's prologue and drain
+// overlap another's streaming (4950 vs 4290 GiB/s with 3 streams).  Large batches
+// are long enough to amortise their own ramp and use both slots.  The W=64 scan runs one
+// 1024-thread workgroup per CU (130 KiB LDS).
+constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
-ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles) {
+ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main) {
     const uint64_t wpb = width_of(alg) == 32 ? 8 : (uint64_t)kWavesPerBlock;
-    const uint64_t per_cu = (uint64_t)kWavesPerBlock / wpb;
-    const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)d->cus * per_cu);
+    const uint64_t per_cu = width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
+    uint64_t cap = (uint64_t)d->cus * per_cu;
+    static const double frac = [] {  // diagnostics: AMDCRC_GRID_FRAC caps the grid at a share of the slots
+        const char *e = std::getenv("AMDCRC_GRID_FRAC");
+        return e ? std::atof(e) : 1.0;
+    }();
+    if (frac > 0 && frac < 1) cap = std::max<uint64_t>(1, (uint64_t)(cap * frac));
+    const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, cap);
     return {blocks, wpb};
 }
 
@@ -348,7 +360,7 @@ struct Timeline {
     size_t cap = 0, waves = 0;
 } g_timeline;
 
-int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, hipStream_t s) {
+int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, uint64_t total_main, hipStream_t s) {
     p.dbg = debug_flags();
     p.d_timeline = nullptr;
     if (p.dbg & 16) {
@@ -385,7 +397,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_cnt1 = w->cnt1;
         p.d_claim = w->claim;
     }
-    const uint64_t blocks = scan_geometry(d, alg, p.ntiles).blocks;
+    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main).blocks;
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
@@ -433,10 +445,10 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     p.d_out = d_out;
     if (pool) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
-        const ScanGeometry geo = scan_geometry(d, alg, p.ntiles);
+        const ScanGeometry geo = scan_geometry(d, alg, p.ntiles, ml * count);
         if (p.ntiles >= 2 * geo.blocks * geo.waves_per_block) p.nstatic = geo.blocks * geo.waves_per_block;
     }
-    return launch_scan(d, alg, p, count, T, s);
+    return launch_scan(d, alg, p, count, T, ml * count, s);
 }
 
 // Per-stream pinned -> device descriptor staging.  stage_begin returns host memory to fill;
@@ -504,7 +516,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         prefix[i + 1] = prefix[i] + T;
     }
     const uint64_t ntiles = prefix[count];
-    const ScanGeometry geo = scan_geometry(d, xxh ? ALG_CRC32 : alg, ntiles);
+    const ScanGeometry geo = scan_geometry(d, xxh ? ALG_CRC32 : alg, ntiles, total);
     const uint64_t nw = std::max<uint64_t>(geo.blocks, 1) * geo.waves_per_block;
     const size_t words = count * 2 + (count + 1) + nw;
     uint64_t *h;
@@ -543,7 +555,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     p.ntiles = ntiles;
     p.d_seeds = d_seeds;
     p.d_out = d_out;
-    return launch_scan(d, alg, p, count, tmax, s);
+    return launch_scan(d, alg, p, count, tmax, total, s);
 }
 
 int ensure_stage(Device *d, size_t bytes) {

@@ -12,7 +12,7 @@ Infinity Cache) so every launch streams from HBM, not from the on-die cache.
 
 Timed region: K eager launches, alternating over --branches HIP streams so that a launch's
 workgroups start on CUs as the previous launch's workgroups retire (its prologue overlaps the other
-launch's tail; measured best at 2 streams).  --mode graph replays a captured HIP graph instead (one
+launch.s tail; 3 streams by default).  --mode graph replays a captured HIP graph instead (one
 launch per batch, batches split over graph branches; measured slower on ROCm 7.2: every replay
 starts with a ~20 us bubble).  Kernel duration for the roofline: a separate pass queues
 --timing-launches eager launches on one stream behind a GPU-side hold; each launch stamps HIP
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--buffers", type=int, default=1024)
     ap.add_argument("--buffer-bytes", type=int, default=65536)
     ap.add_argument("--batches", type=int, default=8)
-    ap.add_argument("--branches", type=int, default=2)
+    ap.add_argument("--branches", type=int, default=3)
     ap.add_argument("--mode", default="eager", choices=["graph", "eager"])
     ap.add_argument("--timing-launches", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -175,7 +175,7 @@ def main():
     # every batch once and, when there is a timed region, every stream (per-stream workspaces are
     # allocated on first use); with --steps 0 (profiling the timing pass) stream 0 only, so every
     # launch of the run is a serialized one
-    for i in range(max(args.warmup, nb if args.steps == 0 else 2 * nb)):
+    for i in range(max(args.warmup, nb if args.steps == 0 else nb * len(streams))):
         launch(i, streams[0] if args.steps == 0 else None)
     torch.cuda.synchronize()
 
