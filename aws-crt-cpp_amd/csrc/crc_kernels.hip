@@ -1066,8 +1066,9 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
 }
 
 // ------------------------------------------------------------------------------------------
-// xxHash64 (aws_xxhash64_compute, XXHash.cpp:17): one lane per buffer; the published
-// algorithm is a serial chain per buffer, so parallelism comes only from the batch.
+// xxHash64 (aws_xxhash64_compute, XXHash.cpp:17).  The published algorithm is four serial chains
+// per buffer (nonlinear: add, rotate, multiply mod 2^64), so a buffer has at most four lanes of
+// parallelism; the batch supplies the rest.
 constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull, XP2 = 0xC2B2AE3D27D4EB4Full, XP3 = 0x165667B19E3779F9ull,
                    XP4 = 0x85EBCA77C2B2AE63ull, XP5 = 0x27D4EB2F165667C5ull;
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
@@ -1079,34 +1080,70 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void xxh64_kernel(const XxhParams p) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.nbuf) return;
-    const uint8_t *ptr = (const uint8_t *)(p.d_ptrs ? p.d_ptrs[i] : p.base + i * p.stride);
-    const uint64_t n = p.d_ptrs ? p.d_lens[i] : p.len;
-    const uint64_t seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
-    const uint8_t *end = ptr + n;
-    uint64_t h;
-    if (n >= 32) {
-        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
-        if (((uintptr_t)ptr & 15) == 0) {
-            while (ptr + 32 <= end) {
-                const ulonglong2 a = *(const ulonglong2 *)ptr, b = *(const ulonglong2 *)(ptr + 16);
-                v1 = xround(v1, a.x);
-                v2 = xround(v2, a.y);
-                v3 = xround(v3, b.x);
-                v4 = xround(v4, b.y);
-                ptr += 32;
-            }
-        } else {
-            while (ptr + 32 <= end) {
-                v1 = xround(v1, ld64u(ptr));
-                v2 = xround(v2, ld64u(ptr + 8));
-                v3 = xround(v3, ld64u(ptr + 16));
-                v4 = xround(v4, ld64u(ptr + 24));
-                ptr += 32;
+// XXH64 with one quad (4 lanes) per buffer: lane j owns accumulator v_(j+1), i.e. word j of every
+// 32-byte stripe, so a buffer's four independent serial chains run on four lanes instead of
+// interleaving in one (the per-lane chain, not issue, then bounds a buffer: 8 B per round latency).
+// Each lane loads its words of four stripes per iteration, the next four in flight while these are
+// mixed in.  Lane 0 of the quad finishes (merge, remaining < 32 bytes, avalanche).
+__device__ __forceinline__ uint64_t ldw(const uint8_t *p, bool aligned) {
+    if (aligned) return *(const __attribute__((address_space(1))) uint64_t *)p;
+    return ld64u(p);
+}
+
+// lane k of each quad, broadcast to the quad (DPP quad_perm [k,k,k,k])
+template <int K>
+__device__ __forceinline__ uint64_t quad_bcast(uint64_t v) {
+    constexpr int sel = K | (K << 2) | (K << 4) | (K << 6);
+    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, sel, 0xF, 0xF, false);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), sel, 0xF, 0xF, false);
+    return ((uint64_t)h << 32) | l;
+}
+
+__global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+    const int j = (int)(threadIdx.x & 3);
+    const bool valid = i < p.nbuf;
+    const uint8_t *ptr = nullptr;
+    uint64_t n = 0, seed = 0;
+    if (valid) {
+        ptr = (const uint8_t *)(p.d_ptrs ? p.d_ptrs[i] : p.base + i * p.stride);
+        n = p.d_ptrs ? p.d_lens[i] : p.len;
+        seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
+    }
+    const uint64_t ns = n >= 32 ? n / 32 : 0;
+    const bool aligned = ((uintptr_t)ptr & 7) == 0;
+    uint64_t v = seed + (j == 0 ? XP1 + XP2 : j == 1 ? XP2 : j == 2 ? 0ull : 0ull - XP1);
+    const uint8_t *q = ptr + 8 * j;
+    // kXxSlots x 4 stripes in flight per lane: an HBM load takes ~2 us, a round ~60-80 cycles of
+    // dependent 64-bit arithmetic; the kernel runs a few waves per CU, so registers are plentiful
+    constexpr int kXxSlots = 12;
+    uint64_t s = 0;
+    if (ns >= 4 * kXxSlots) {
+        uint64_t w[kXxSlots][4];
+#pragma unroll
+        for (int k = 0; k < kXxSlots; ++k)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) w[k][m] = ldw(q + 32 * (4 * k + m), aligned);
+        for (s = 4 * kXxSlots; s + 4 * kXxSlots <= ns; s += 4 * kXxSlots) {
+#pragma unroll
+            for (int k = 0; k < kXxSlots; ++k) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) v = xround(v, w[k][m]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[k][m] = ldw(q + 32 * (s + 4 * k + m), aligned);
             }
         }
+#pragma unroll
+        for (int k = 0; k < kXxSlots; ++k)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) v = xround(v, w[k][m]);
+    }
+    for (; s < ns; ++s) v = xround(v, ldw(q + 32 * s, aligned));
+    // lane 0 of the quad gathers v1..v4 (quad_perm DPP broadcasts of lanes 1..3)
+    const uint64_t v1 = quad_bcast<0>(v), v2 = quad_bcast<1>(v), v3 = quad_bcast<2>(v), v4 = quad_bcast<3>(v);
+    if (!valid || j != 0) return;
+    uint64_t h;
+    if (n >= 32) {
         h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
         h = xmerge(h, v1);
         h = xmerge(h, v2);
@@ -1116,20 +1153,21 @@ __global__ __launch_bounds__(256) void xxh64_kernel(const XxhParams p) {
         h = seed + XP5;
     }
     h += n;
-    while (ptr + 8 <= end) {
-        h ^= xround(0, ld64u(ptr));
+    const uint8_t *t = ptr + 32 * ns, *end = ptr + n;
+    while (t + 8 <= end) {
+        h ^= xround(0, ld64u(t));
         h = rotl64(h, 27) * XP1 + XP4;
-        ptr += 8;
+        t += 8;
     }
-    if (ptr + 4 <= end) {
-        uint32_t v;
-        __builtin_memcpy(&v, ptr, 4);
-        h ^= (uint64_t)v * XP1;
+    if (t + 4 <= end) {
+        uint32_t w;
+        __builtin_memcpy(&w, t, 4);
+        h ^= (uint64_t)w * XP1;
         h = rotl64(h, 23) * XP2 + XP3;
-        ptr += 4;
+        t += 4;
     }
-    while (ptr < end) {
-        h ^= (*ptr++) * XP5;
+    while (t < end) {
+        h ^= (*t++) * XP5;
         h = rotl64(h, 11) * XP1;
     }
     h ^= h >> 33;
@@ -1171,8 +1209,8 @@ extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stre
 
 // Scan launch.  ev[0] / ev[1] (diagnostics, may be null): HIP events stamped with the dispatch's own
 // start / end time (hipExtLaunchKernel), i.e. the interval a kernel-trace profiler reports.
-template <typename K>
-static void launch(K kernel, int nblocks, int threads, hipStream_t s, const ScanParams *p, void *const *ev) {
+template <typename K, typename P>
+static void launch(K kernel, int nblocks, int threads, hipStream_t s, const P *p, void *const *ev) {
     if (ev && (ev[0] || ev[1]))
         hipExtLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
     else
@@ -1210,10 +1248,10 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     return (int)hipGetLastError();
 }
 
-extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream) {
+extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream, void *const *ev) {
     const int threads = 256;
-    const uint64_t blocks = (p->nbuf + threads - 1) / threads;
+    const uint64_t blocks = (p->nbuf * 4 + threads - 1) / threads;  // a quad per buffer
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(xxh64_kernel, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, *p);
+    launch(xxh64_quad_kernel, (int)blocks, threads, (hipStream_t)stream, p, ev);
     return (int)hipGetLastError();
 }

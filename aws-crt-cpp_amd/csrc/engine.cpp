@@ -341,8 +341,9 @@ ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t t
 }
 
 int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
-    int e = alg == AWS_CRT_AMD_XXH64 ? amdcrc_launch_xxh64(&xp, s)
-                                     : amdcrc_launch_xxh3(alg == AWS_CRT_AMD_XXH3_64 ? 64 : 128, &xp, s);
+    int e = alg == AWS_CRT_AMD_XXH64 ? amdcrc_launch_xxh64(&xp, s, g_time_events)
+                                     : amdcrc_launch_xxh3(alg == AWS_CRT_AMD_XXH3_64 ? 64 : 128, &xp, s, g_time_events);
+    g_time_events[0] = g_time_events[1] = nullptr;
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("hash kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
 

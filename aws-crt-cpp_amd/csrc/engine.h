@@ -91,6 +91,6 @@ struct CombineParams {
 extern "C" {
 int amdcrc_launch_combine(int alg, const amdcrc::CombineParams *p, void *stream);
 int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *stream, void *const *events);
-int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream);
-int amdcrc_launch_xxh3(int bits, const amdcrc::XxhParams *p, void *stream);
+int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream, void *const *events);
+int amdcrc_launch_xxh3(int bits, const amdcrc::XxhParams *p, void *stream, void *const *events);
 }

@@ -5,6 +5,7 @@
 // class of the published algorithm is implemented; a buffer's hash is a serial chain, so the batch
 // supplies the parallelism (SURVEY.md 8(f) rank 3 -- a stripe-parallel long-input kernel is next).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "engine.h"
 
@@ -265,13 +266,22 @@ __global__ __launch_bounds__(256) void xxh3_kernel(const XxhParams p) {
 
 }  // namespace
 
-extern "C" int amdcrc_launch_xxh3(int bits, const XxhParams *p, void *stream) {
+extern "C" int amdcrc_launch_xxh3(int bits, const XxhParams *p, void *stream, void *const *ev) {
     const int threads = 256;
     const uint64_t blocks = (p->nbuf + threads - 1) / threads;
     if (blocks == 0) return 0;
-    if (bits == 64)
-        hipLaunchKernelGGL(xxh3_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, *p);
-    else
-        hipLaunchKernelGGL(xxh3_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream, *p);
+    hipStream_t s = (hipStream_t)stream;
+    const bool timed = ev && (ev[0] || ev[1]);
+    if (bits == 64) {
+        if (timed)
+            hipExtLaunchKernelGGL(xxh3_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+        else
+            hipLaunchKernelGGL(xxh3_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
+    } else {
+        if (timed)
+            hipExtLaunchKernelGGL(xxh3_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+        else
+            hipLaunchKernelGGL(xxh3_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
+    }
     return (int)hipGetLastError();
 }
