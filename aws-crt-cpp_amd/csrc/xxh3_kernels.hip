@@ -1,9 +1,10 @@
-// XXH3-64 / XXH3-128 (xxHash 0.8 algorithm) on gfx950, one lane per buffer.
+// XXH3-64 / XXH3-128 (xxHash 0.8 algorithm) on gfx950: one wavefront per buffer, stripe-parallel.
 //
 // Drop-in for aws_xxhash3_64_compute / aws_xxhash3_128_compute (reference call sites
 // source/checksum/XXHash.cpp:22,27; known answers tests/XXHashTest.cpp:44, :73-74).  Every length
-// class of the published algorithm is implemented; a buffer's hash is a serial chain, so the batch
-// supplies the parallelism (SURVEY.md 8(f) rank 3 -- a stripe-parallel long-input kernel is next).
+// class of the published algorithm is implemented.  Inputs up to 240 bytes are a short serial
+// computation (lane 0 of the buffer's wave); longer ones run the stripe-parallel wave loop below
+// (SURVEY.md 8(f) rank 3).
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
@@ -36,6 +37,7 @@ constexpr uint64_t MX1 = 0x165667919E3779F9ull, MX2 = 0x9FB21C651E98DF25ull;
 struct U128 {
     uint64_t lo, hi;
 };
+typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint64_t rd64(const uint8_t *p) {
     uint64_t v;
@@ -248,40 +250,173 @@ __device__ U128 xxh3_128(const uint8_t *p, uint64_t n, uint64_t seed) {
     return {avalanche3(rl), 0ull - avalanche3(rh)};
 }
 
+// ------------------------------------------------------------------------------------------
+// Stripe-parallel XXH3 for long inputs (> 240 bytes): one wavefront per buffer.
+//
+// The long loop's accumulators only ever add within a 1 KiB block (16 stripes of 64 bytes); the
+// nonlinear scramble runs once per block.  So a block is one coalesced wave load (lane l: 16 bytes
+// at 16 l = words 2(l&3), 2(l&3)+1 of stripe l>>2), each lane computes its two accumulator
+// contributions, the 16 lanes of each residue class mod 4 sum them (64-bit adds over lane
+// shuffles), and every lane then updates and scrambles the two accumulators of its class
+// (replicated, so the next block needs no broadcast).  The serial part per block is the reduction
+// and the scramble; the loads run several blocks ahead.
+__device__ __forceinline__ uint64_t cw(int w, uint64_t seed) {  // word w of the (seeded) secret
+    return rd64(kSecret + 8 * w) + ((w & 1) ? 0ull - seed : seed);
+}
+__device__ __forceinline__ uint64_t sec64(int off, uint64_t seed) {  // 8 secret bytes at byte offset off
+    const int w = off >> 3, b = off & 7;
+    const uint64_t lo = cw(w, seed);
+    if (!b) return lo;
+    return (lo >> (8 * b)) | (cw(w + 1, seed) << (64 - 8 * b));
+}
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t class_sum(uint64_t v) {  // sum over the 16 lanes with equal lane & 3
+    v += shfl_xor64(v, 4);
+    v += shfl_xor64(v, 8);
+    v += shfl_xor64(v, 16);
+    v += shfl_xor64(v, 32);
+    return v;
+}
+__device__ __forceinline__ uint64_t mul32x32(uint64_t k) { return (k & 0xFFFFFFFFull) * (k >> 32); }
+__device__ __forceinline__ uint64_t scramble1(uint64_t a, uint64_t s) {
+    a ^= a >> 47;
+    a ^= s;
+    return a * P32_1;
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void ld16(const uint8_t *q, uint64_t &a, uint64_t &b) {
+    if (ALIGNED) {
+        const v2u64 x = *(const __attribute__((address_space(1))) v2u64 *)q;
+        a = x.x;
+        b = x.y;
+    } else {
+        a = rd64(q);
+        b = rd64(q + 8);
+    }
+}
+
+template <int BITS, bool ALIGNED>
+__device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *ptr, uint64_t n, uint64_t seed, int lane) {
+    const int s = lane >> 2, wp = lane & 3;
+    const uint64_t ks0 = sec64(8 * s + 16 * wp, seed), ks1 = sec64(8 * s + 16 * wp + 8, seed);
+    const uint64_t st0 = sec64(128 + 16 * wp, seed), st1 = sec64(136 + 16 * wp, seed);
+    const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+    uint64_t acc0 = init[2 * wp], acc1 = init[2 * wp + 1];
+    const uint64_t nb = (n - 1) / 1024;
+    const uint8_t *q = ptr + 16 * lane;
+    constexpr int D = 4;  // blocks in flight
+    uint64_t w0[D], w1[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if ((uint64_t)d < nb) ld16<ALIGNED>(q + 1024 * d, w0[d], w1[d]);
+    uint64_t blk = 0;
+    for (; blk + D <= nb; blk += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint64_t c0 = mul32x32(w0[d] ^ ks0) + w1[d], c1 = mul32x32(w1[d] ^ ks1) + w0[d];
+            if (blk + D + d < nb) ld16<ALIGNED>(q + 1024 * (blk + D + d), w0[d], w1[d]);
+            acc0 = scramble1(acc0 + class_sum(c0), st0);
+            acc1 = scramble1(acc1 + class_sum(c1), st1);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (blk + d < nb) {
+            const uint64_t c0 = mul32x32(w0[d] ^ ks0) + w1[d], c1 = mul32x32(w1[d] ^ ks1) + w0[d];
+            acc0 = scramble1(acc0 + class_sum(c0), st0);
+            acc1 = scramble1(acc1 + class_sum(c1), st1);
+        }
+    }
+    // the partial last block (no scramble) and the last stripe, read at n - 64 (lanes 0..3)
+    const uint64_t ns = ((n - 1) - 1024 * nb) / 64;
+    uint64_t c0 = 0, c1 = 0;
+    if ((uint64_t)s < ns) {
+        uint64_t a, b;
+        ld16<ALIGNED>(q + 1024 * nb, a, b);
+        c0 = mul32x32(a ^ ks0) + b;
+        c1 = mul32x32(b ^ ks1) + a;
+    }
+    if (s == 0) {
+        uint64_t a, b;
+        ld16<false>(ptr + n - 64 + 16 * wp, a, b);
+        c0 += mul32x32(a ^ sec64(121 + 16 * wp, seed)) + b;
+        c1 += mul32x32(b ^ sec64(129 + 16 * wp, seed)) + a;
+    }
+    acc0 += class_sum(c0);
+    acc1 += class_sum(c1);
+    // lanes 0..3 hold accumulators {0,1}, {2,3}, {4,5}, {6,7}
+    uint64_t acc[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[2 * k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(acc0 >> 32), k) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)acc0, k);
+        acc[2 * k + 1] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(acc1 >> 32), k) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)acc1, k);
+    }
+    if (lane != 0) return;
+    auto mergeacc = [&](int off, uint64_t start) {
+        uint64_t r = start;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r += fold64(acc[2 * k] ^ sec64(off + 16 * k, seed), acc[2 * k + 1] ^ sec64(off + 16 * k + 8, seed));
+        return avalanche3(r);
+    };
+    if (BITS == 64) {
+        p.d_out[i] = mergeacc(11, n * P64_1);
+    } else {
+        p.d_out[2 * i] = mergeacc(117, ~(n * P64_2));  // canonical order: high half first
+        p.d_out[2 * i + 1] = mergeacc(11, n * P64_1);
+    }
+}
+
 template <int BITS>
-__global__ __launch_bounds__(256) void xxh3_kernel(const XxhParams p) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void xxh3_wave_kernel(const XxhParams p) {
+    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (i >= p.nbuf) return;
     const uint8_t *ptr = (const uint8_t *)(p.d_ptrs ? p.d_ptrs[i] : p.base + i * p.stride);
     const uint64_t n = p.d_ptrs ? p.d_lens[i] : p.len;
     const uint64_t seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
-    if (BITS == 64) {
-        p.d_out[i] = xxh3_64(ptr, n, seed);
-    } else {
-        const U128 h = xxh3_128(ptr, n, seed);
-        p.d_out[2 * i] = h.hi;  // canonical order: high half first
-        p.d_out[2 * i + 1] = h.lo;
+    if (n <= 240) {  // short inputs: the scalar published code paths, one lane
+        if (lane == 0) {
+            if (BITS == 64) {
+                p.d_out[i] = xxh3_64(ptr, n, seed);
+            } else {
+                const U128 h = xxh3_128(ptr, n, seed);
+                p.d_out[2 * i] = h.hi;
+                p.d_out[2 * i + 1] = h.lo;
+            }
+        }
+        return;
     }
+    if (((uintptr_t)ptr & 15) == 0)
+        xxh3_long_wave<BITS, true>(p, i, ptr, n, seed, lane);
+    else
+        xxh3_long_wave<BITS, false>(p, i, ptr, n, seed, lane);
 }
 
 }  // namespace
 
+// One wavefront per buffer (4 per 256-thread block): long buffers use all 64 lanes, short ones lane 0.
 extern "C" int amdcrc_launch_xxh3(int bits, const XxhParams *p, void *stream, void *const *ev) {
     const int threads = 256;
-    const uint64_t blocks = (p->nbuf + threads - 1) / threads;
+    const uint64_t blocks = (p->nbuf + 3) / 4;
     if (blocks == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     const bool timed = ev && (ev[0] || ev[1]);
     if (bits == 64) {
         if (timed)
-            hipExtLaunchKernelGGL(xxh3_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+            hipExtLaunchKernelGGL(xxh3_wave_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
         else
-            hipLaunchKernelGGL(xxh3_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
+            hipLaunchKernelGGL(xxh3_wave_kernel<64>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
     } else {
         if (timed)
-            hipExtLaunchKernelGGL(xxh3_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+            hipExtLaunchKernelGGL(xxh3_wave_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
         else
-            hipLaunchKernelGGL(xxh3_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
+            hipLaunchKernelGGL(xxh3_wave_kernel<128>, dim3((unsigned)blocks), dim3(threads), 0, s, *p);
     }
     return (int)hipGetLastError();
 }

@@ -40,7 +40,7 @@ sys.path.insert(0, os.path.join(REPO, "aws-crt-cpp_amd"))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md chip table
-ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3}
+ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
 
 
 def parse():
@@ -101,8 +101,9 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     host.copy_(dev_data[: nb * step])
     odt = torch.int64 if wide else torch.int32
     slots = [torch.empty(step, dtype=torch.uint8, device=dev_data.device) for _ in range(3)]
-    outs = [torch.empty(count, dtype=odt, device=dev_data.device) for _ in range(3)]
-    hres = torch.empty((iters, count), dtype=odt, pin_memory=True)
+    per = 2 if alg_id == 5 else 1
+    outs = [torch.empty(count * per, dtype=odt, device=dev_data.device) for _ in range(3)]
+    hres = torch.empty((iters, count * per), dtype=odt, pin_memory=True)
     cs, ks = torch.cuda.Stream(device=dev_data.device), torch.cuda.Stream(device=dev_data.device)
     copied = [torch.cuda.Event() for _ in range(3)]
     freed = [torch.cuda.Event() for _ in range(3)]
@@ -162,8 +163,9 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
-    wide = alg in ("crc64nvme", "xxh64")
-    outs = [torch.empty(count, dtype=torch.int64 if wide else torch.int32, device=dev) for _ in range(nb)]
+    wide = alg in ("crc64nvme", "xxh64", "xxh3_64", "xxh3_128")
+    per = 2 if alg == "xxh3_128" else 1  # XXH3-128: {high, low} per buffer
+    outs = [torch.empty(count * per, dtype=torch.int64 if wide else torch.int32, device=dev) for _ in range(nb)]
     streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.branches))]
 
     def launch(i, st=None):
@@ -250,7 +252,7 @@ def main():
         e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and alg in ("crc32", "crc32c", "crc64nvme", "xxh64"):
         host = data[:step_bytes].cpu().numpy()
         torch.cuda.synchronize()
         gpu0 = eng.as_unsigned(outs[0])

@@ -11,6 +11,7 @@ run c3_crc32c --buffers 16 --buffer-bytes 268435456 --batches 1 --steps 10 --war
 run c3_crc32 --alg crc32 --buffers 16 --buffer-bytes 268435456 --batches 1 --steps 10 --warmup 2 --timing-launches 4 &&
 run c4_shard --buffers 131072 --buffer-bytes 8192 --batches 1 --steps 40 --warmup 4 --timing-launches 8 &&
 run c5_crc64 --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --batches 2 --steps 20 --warmup 2 --timing-launches 4 &&
-run c5_xxh64 --alg xxh64 --buffers 8 --buffer-bytes 67108864 --batches 2 --steps 4 --warmup 1 --timing-launches 2 &&
+run c5_xxh64 --alg xxh64 --buffers 8 --buffer-bytes 67108864 --batches 2 --steps 6 --warmup 2 --timing-launches 2 --branches 2 &&
 run c2_crc64 --alg crc64nvme &&
-run c2_xxh64 --alg xxh64 --steps 20 --warmup 2 --timing-launches 4
+run c2_xxh64 --alg xxh64 --steps 40 --warmup 4 --timing-launches 8 &&
+run c2_xxh3 --alg xxh3_64 --steps 20 --warmup 4 --timing-launches 4
