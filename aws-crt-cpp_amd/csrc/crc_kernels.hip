@@ -262,10 +262,14 @@ struct BraidBasis {
 };
 
 // basis value b[k][bit] for a per-lane (runtime) table index k < 4: four compile-time candidates
+// (masks made opaque: a select chain over constants becomes a per-lane global load from a constant
+// table, which the table build would then wait for behind the payload loads already in flight)
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t basis_bit(uint32_t k, int bit) {
     constexpr BraidBasis<POLY> B{};
-    return k == 0 ? B.b[0][bit] : k == 1 ? B.b[1][bit] : k == 2 ? B.b[2][bit] : B.b[3][bit];
+    uint32_t m0 = k == 0 ? ~0u : 0u, m1 = k == 1 ? ~0u : 0u, m2 = k == 2 ? ~0u : 0u, m3 = k == 3 ? ~0u : 0u;
+    asm("" : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3));
+    return (B.b[0][bit] & m0) | (B.b[1][bit] & m1) | (B.b[2][bit] & m2) | (B.b[3][bit] & m3);
 }
 
 template <uint32_t POLY, int K>
@@ -591,7 +595,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // memory system is saturated (every CU primes at once), so priming two groups kept the first scan
     // waiting for 8 KiB per wave to be accepted.  The ring scans group 0 while group 1's loads go out
     // between its table steps.
-    BGroup r0, r1;
+    BGroup r0, r1, r2;
     braid_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
     if (any && !dyn) pf_advance();  // pool mode: after the barrier, where the pool counter is set up
     {
@@ -623,6 +627,14 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // pool mode: the prefetch cursor may reach the pool only now (the host gives every wave of a
     // pooled launch a static tile with payload, so a wave's pool tiles always follow it)
     if (dyn && any) pf_advance();
+    // Three-slot ring: the second group goes out now, so that while group g is scanned group g+1 is
+    // already in flight and group g+2 streams out between the table steps.  With two slots a wave had
+    // 4-8 KiB in flight and waited one full HBM latency per group (2048 waves x 4 KiB / ~1.7 us ~
+    // 5 TB/s on 1024 x 64 KiB); three slots keep 8-12 KiB per wave in flight.
+    if (any && !pf_done) {
+        braid_load<NT>(r1, fvb, fpad, gf, lane);
+        pf_advance();
+    }
     stamp(1);
     // Every wave publishes its 1/8 of the K image and P columns once its constants have arrived
     // (after its first group, by which time they have: loads retire in order) and counts itself in
@@ -711,13 +723,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
         // leading tiles without payload finish before the primed group is reached: publish first then
         if (dp.ngroups == 0) publish_consts();
         if (settle()) {
-            ring_step(r0, r1);
+            ring_step(r0, r2);
             publish_consts();
             for (;;) {
                 if (!settle()) break;
                 ring_step(r1, r0);
                 if (!settle()) break;
-                ring_step(r0, r1);
+                ring_step(r2, r1);
+                if (!settle()) break;
+                ring_step(r0, r2);
             }
         }
     } else {
@@ -728,6 +742,273 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     stamp(2);
     braid_publish<LIST>(p, acc, pd, eng, lane);
     braid_resolve<LIST>(p, pd, eng, lane);
+    stamp(3);
+}
+
+// ------------------------------------------------------------------------------------------
+// W = 32 streaming scan for uniform batches whose main region is a whole number of tiles (no
+// virtual front pad): 1024 x 64 KiB, 16 x 256 MiB, 131072 x 8 KiB.  The same braided rows, tables
+// and tile combine as crc32_braid_kernel, with a three-slot register ring whose vmcnt accounting is
+// explicit instead of left to the compiler:
+//
+//  * Payload rows are loaded by inline asm, so the compiler's wait-count pass never sees them.  Every
+//    scan step issues exactly 16 row loads (the group two ahead; past the wave's last group the rows
+//    of the L2-resident constant block instead), so when row r of the scanned slot is needed exactly
+//    32 loads are younger than it (the rest of its group, the next group, and the r + 1 rows issued
+//    this step): one `s_waitcnt vmcnt(32)` per row, never a drain.  Loads complete in order, so
+//    younger non-load operations (tile-finish stores) can only make such a wait longer, never short.
+//  * Two groups (8 KiB per wave) are in flight when a group's scan starts and a third streams out
+//    between its table steps.  The compiler-managed ring of the generic kernel merged its paths into
+//    a full `vmcnt(0)` drain per group, so a wave waited one whole HBM latency for every 4 KiB.
+template <int R>
+__device__ __forceinline__ uint32_t gld_row(uint32_t voff, uint64_t sbase) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, %2 offset:%3 nt" : "=v"(v) : "v"(voff), "s"(sbase), "i"(R * kBraidRow) : "memory");
+    return v;
+}
+
+template <int R, class B>
+__device__ __forceinline__ uint32_t stream_rows(uint32_t x, BGroup &cur, BGroup &nxt, uint32_t voff, uint64_t snext, const B &eng) {
+    if constexpr (R < kBraidRowsPerGroup) {
+        nxt.w[R] = gld_row<R>(voff, snext);
+        asm volatile("s_waitcnt vmcnt(32)" : "+v"(cur.w[R])::"memory");
+        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return stream_rows<R + 1>(x, cur, nxt, voff, snext, eng);
+    } else {
+        return eng.step(x);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void stream_issue(BGroup &g, uint32_t voff, uint64_t s) {
+    if constexpr (R < kBraidRowsPerGroup) {
+        g.w[R] = gld_row<R>(voff, s);
+        stream_issue<R + 1>(g, voff, s);
+    }
+}
+
+// Cross-tile combine for the streaming scan: the same group slots as braid_finish / braid_publish /
+// braid_resolve, with every global atomic in inline asm that waits for its own completion.  These
+// run once per 32-tile group at most; a compiler-visible returning atomic would instead leave its
+// destination registers "pending" across the scan loop and the compiler would guard later writes of
+// them with a full vmcnt(0) drain of the payload ring on every scan step.
+__device__ __forceinline__ unsigned long long sx_xor64_ret(unsigned long long *a, unsigned long long v) {
+    unsigned long long r;
+    asm volatile("global_atomic_xor_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=&v"(r) : "v"(a), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ unsigned long long sx_swap64_ret(unsigned long long *a, unsigned long long v) {
+    unsigned long long r;
+    asm volatile("global_atomic_swap_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=&v"(r) : "v"(a), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ unsigned int sx_add32_ret(unsigned int *a, unsigned int v) {
+    unsigned int r;
+    asm volatile("global_atomic_add %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=&v"(r) : "v"(a), "v"(v) : "memory");
+    return r;
+}
+__device__ __forceinline__ void sx_store32(unsigned int *a, unsigned int v) {  // agent-scope atomic store
+    asm volatile("global_store_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : : "v"(a), "v"(v) : "memory");
+}
+
+// publish the wave's merged tiles of one group and, if they complete it, finish the group at once
+template <class B>
+__device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g, const B &eng, int lane) {
+    if (g.slot == ~0ull) return;
+    unsigned long long old = 0;
+    if (lane == 0) old = sx_xor64_ret(&p.d_acc1[g.slot], g.val);
+    const unsigned long long now = rfl64(old) ^ g.val;
+    const uint64_t slot = g.slot;
+    g.slot = ~0ull;
+    const uint64_t n = g.T - g.g0 < 32 ? g.T - g.g0 : 32, G = (g.T + 31) / 32, shift = g.T - g.g0 - n;
+    const unsigned long long full = n >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << n) - 1) << 32);
+    if ((now & 0xFFFFFFFF00000000ull) != full) return;
+    uint32_t grp = (uint32_t)now;
+    if (G > 1 && shift) grp = mul_pcols<uint32_t, 32>(grp, p.d_pcols + shift * 32);
+    if (lane != 0) return;
+    (void)sx_swap64_ret(&p.d_acc1[slot], 0ull);
+    if (G == 1) {
+        finalize<false>(p, g.b, grp, eng);
+        return;
+    }
+    (void)sx_xor64_ret(&p.d_acc[g.b], (unsigned long long)grp);  // performed before it is counted
+    const unsigned int c = sx_add32_ret(&p.d_cnt[g.b], 1u);
+    if (c == G - 1) {
+        const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[g.b], 0ull);
+        sx_store32(&p.d_cnt[g.b], 0u);
+        finalize<false>(p, g.b, fin, eng);
+    }
+}
+
+template <class B>
+__device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc) {
+    const uint32_t r = wave_xor_s(eng.mulK(u, lane));
+    if (d.T == 1) {
+        if (lane == 0) finalize<false>(p, d.b, r, eng);
+        return;
+    }
+    const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
+    const uint32_t m = (uint32_t)(gend - 1 - d.k);
+    const uint32_t colv = lds32(eng.L, kPcolOff + 4 * (m * 32 + (lane & 31)));
+    const uint32_t sel = lane < 32 ? (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - lane, 1) : 0u;
+    const uint32_t v = wave_xor_s(colv & sel);
+    const uint64_t slot = d.tbase + g0;
+    if (slot != acc.slot) {
+        stream_publish(p, acc, eng, lane);
+        acc.slot = slot;
+        acc.val = 0;
+        acc.b = d.b;
+        acc.T = d.T;
+        acc.g0 = (uint32_t)g0;
+    }
+    acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
+}
+
+template <uint32_t POLY, bool PRIME2>
+__global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const ScanParams p) {
+    using B = Braid32<POLY, true>;
+    __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
+    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    const bool stamps = p.d_timeline != nullptr;
+    auto stamp = [&](int i) {
+        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
+    // geometry: G groups of 4 KiB per tile (power of two), T tiles per buffer, main at hoff of each
+    const uint32_t G = p.seg / kGroupBytes;
+    const uint32_t gsh = __builtin_ctz(G);
+    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
+    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
+    const uint64_t q1 = t1 << gsh;
+    const uint32_t voff = 4u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
+    // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
+    uint64_t fq = t0 << gsh, fb = t0 / T, fk = t0 - fb * T;
+    uint32_t fg = 0;
+    auto f_addr = [&]() -> uint64_t {
+        return rfl64(fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy);
+    };
+    auto f_next = [&]() {
+        ++fq;
+        if (++fg == G) {
+            fg = 0;
+            if (++fk == T) fk = 0, ++fb;
+        }
+    };
+    // K-image word and P columns of this thread (published to LDS after the first scan step), then the
+    // first group: both asm loads, complete once the first row wait of the first step has passed
+    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
+    v4u kq;
+    uint32_t pce0, pce1;
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
+    const bool work = t0 < t1;
+    BGroup ra, rb, rc;
+    if (work) {
+        stream_issue<0>(ra, voff, f_addr());
+        f_next();
+        if (PRIME2) {
+            stream_issue<0>(rb, voff, f_addr());
+            f_next();
+        }
+    }
+    {
+        const uint32_t i = threadIdx.x;
+        const uint32_t q = (i >> 1) & 3u, h = i & 1u;
+        uint32_t bq[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) bq[b] = basis_bit<POLY>(3 - q, b);
+#pragma unroll
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint32_t e = (i >> 3) + 64u * pass;
+            uint32_t te = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) te ^= ((e >> b) & 1u) ? bq[b] : 0u;
+            *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
+        }
+        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
+        if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
+    }
+    stamp(4);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    if (work && !PRIME2) {
+        stream_issue<0>(rb, voff, f_addr());
+        f_next();
+    }
+    stamp(1);
+    bool consts_ready = false, published = false;
+    auto publish_consts = [&]() {
+        if (published) return;
+        published = true;
+        *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
+        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
+        *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto await_consts = [&]() {
+        if (consts_ready) return;
+        while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+               (uint32_t)kBraidWaves)
+            __builtin_amdgcn_s_sleep(1);
+        consts_ready = true;
+    };
+    if (!work) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(kq), "+v"(pce0), "+v"(pce1)::"memory");
+        publish_consts();
+        return;
+    }
+
+    // scan cursor
+    Tile d;
+    d.T = T;
+    d.b = t0 / T;
+    d.k = t0 - d.b * T;
+    d.tbase = d.b * T;
+    d.vbase = 0;
+    d.pad = 0;
+    d.ngroups = G;
+    uint32_t g = 0;
+    uint64_t q = t0 << gsh;
+    uint32_t u = 0;
+    BGroupAcc acc{};
+    acc.slot = ~0ull;
+    auto step = [&](BGroup &cur, BGroup &nxt) {
+        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
+        const uint64_t sn = f_addr();
+        f_next();
+        u = stream_rows<0>(u, cur, nxt, voff, sn, eng);
+        if (!published) {
+            asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
+            publish_consts();
+        }
+        ++q;
+        if (++g == G) {
+            g = 0;
+            await_consts();
+            stream_finish(p, d, u, eng, lane, acc);
+            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
+        }
+    };
+    for (;;) {
+        step(ra, rc);
+        if (q >= q1) break;
+        step(rb, ra);
+        if (q >= q1) break;
+        step(rc, rb);
+        if (q >= q1) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing placeholder rows
+    stamp(2);
+    stream_publish(p, acc, eng, lane);
     stamp(3);
 }
 
@@ -1222,13 +1503,19 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     const bool list = p->list_mode != 0;
     switch (alg) {
         case ALG_CRC32:
-            if (list)
+            if (p->stream && !list)
+                launch(crc32_stream_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
+            else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
-            if (list)
+            if (p->stream && !list && (p->dbg & 8192))  // diagnostics: prime two groups before the tables
+                launch(crc32_stream_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
+            else if (p->stream && !list)
+                launch(crc32_stream_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
+            else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
             else if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
                 launch(crc32_braid_kernel<kPoly32C, false, false>, nblocks, kBraidBlock, s, p, ev);

@@ -444,7 +444,10 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     p.d_seeds = d_seeds;
     p.seed_all = seed_all;
     p.d_out = d_out;
-    if (pool) {
+    // W=32 batches whose main regions are whole tiles take the streaming scan (explicit three-slot
+    // ring, static tiles; crc_kernels.hip crc32_stream_kernel).  AMDCRC_DEBUG bit 14 disables it.
+    p.stream = width_of(alg) == 32 && ml > 0 && ml % tile == 0 && !(debug_flags() & 16384) ? 1u : 0u;
+    if (pool && !p.stream) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
         const ScanGeometry geo = scan_geometry(d, alg, p.ntiles, ml * count);
         if (p.ntiles >= 2 * geo.blocks * geo.waves_per_block) p.nstatic = geo.blocks * geo.waves_per_block;

@@ -39,7 +39,7 @@ struct ScanParams {
     uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
     uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
     uint32_t dbg;                  // diagnostics only (AMDCRC_DEBUG): bit0 skip tile finish, bit1 skip cross-tile combine
-    uint32_t pad0;
+    uint32_t stream;               // W=32 strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel)
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;

@@ -1,0 +1,139 @@
+// Streaming-read ceiling for the scan's launch shape (diagnostic, not part of the product library).
+// A kernel that only XOR-reduces its payload, with the scan kernel's geometry knobs:
+//   WGT  threads per workgroup, WPC workgroups per CU (grid = 256 * WPC)
+//   LW   dwords per lane per load (1: 256-B wave rows as in the W=32 scan, 2: 512-B rows, 4: 1 KiB)
+//   D    loads per ring slot (two slots: D..2D loads in flight per wave)
+// Per variant: mean dispatch-stamped duration of isolated launches (one stream) and the pipelined
+// rate over S streams, both over the same 64 MiB launches rotated over 8 batches (512 MiB).
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                                       \
+        }                                                                                       \
+    } while (0)
+
+template <int LW>
+struct Vec;
+template <>
+struct Vec<1> {
+    typedef unsigned T;
+};
+template <>
+struct Vec<2> {
+    typedef unsigned T __attribute__((ext_vector_type(2)));
+};
+template <>
+struct Vec<4> {
+    typedef unsigned T __attribute__((ext_vector_type(4)));
+};
+
+template <int LW>
+__device__ __forceinline__ unsigned fold(typename Vec<LW>::T v) {
+    if constexpr (LW == 1) return v;
+    else if constexpr (LW == 2) return v.x ^ v.y;
+    else return v.x ^ v.y ^ v.z ^ v.w;
+}
+
+template <int WGT, int LW, int D, bool NT>
+__global__ __launch_bounds__(WGT) void readk(const uint8_t *base, uint64_t bytes, unsigned *out) {
+    typedef typename Vec<LW>::T V;
+    typedef __attribute__((address_space(1))) const V gV;
+    constexpr int WAVES = WGT / 64;
+    constexpr uint64_t ROW = 256ull * LW;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES, gw = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+    const uint64_t rows = bytes / ROW, r0 = gw * rows / nw, r1 = (gw + 1) * rows / nw;
+    const uint64_t a0 = (uint64_t)base + r0 * ROW + (uint64_t)lane * 4 * LW;
+    const uint64_t ng = (r1 - r0) / D;  // whole slots only (the shapes used divide)
+    V s0[D], s1[D];
+    unsigned acc = 0;
+    auto ld = [&](V *s, uint64_t g) {
+        const uint64_t a = a0 + g * D * ROW;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            s[i] = NT ? __builtin_nontemporal_load((gV *)(a + i * ROW)) : *(gV *)(a + i * ROW);
+        }
+    };
+    auto use = [&](const V *s) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) acc = acc * 3u ^ fold<LW>(s[i]);
+    };
+    if (ng) ld(s0, 0);
+    uint64_t g = 0;
+    for (;;) {
+        if (g + 1 < ng) ld(s1, g + 1);
+        use(s0);
+        if (++g >= ng) break;
+        if (g + 1 < ng) ld(s0, g + 1);
+        use(s1);
+        if (++g >= ng) break;
+    }
+    if (acc == 0x12345678u) out[gw] = acc;
+}
+
+struct Variant {
+    const char *name;
+    void (*k)(const uint8_t *, uint64_t, unsigned *);
+    int wgt, wpc;
+};
+
+#define V(WGT, WPC, LW, D, NT) Variant{#WGT "t x" #WPC " LW" #LW " D" #D " NT" #NT, readk<WGT, LW, D, NT>, WGT, WPC}
+
+int main(int argc, char **argv) {
+    const uint64_t batch = (argc > 1 ? atoll(argv[1]) : 64) << 20;
+    const int nb = 8, iso = 64, pipe_n = 240, S = argc > 2 ? atoi(argv[2]) : 3;
+    uint8_t *buf;
+    unsigned *out;
+    CK(hipMalloc(&buf, batch * nb));
+    CK(hipMalloc(&out, 1 << 20));
+    CK(hipMemset(buf, 0x5a, batch * nb));
+    std::vector<Variant> vs = {
+        V(512, 1, 1, 16, true),  V(512, 1, 1, 16, false), V(512, 1, 1, 32, true), V(512, 2, 1, 16, true),
+        V(512, 1, 2, 8, true),   V(512, 1, 2, 16, true),  V(512, 2, 2, 8, true),  V(512, 1, 4, 4, true),
+        V(512, 1, 4, 8, true),   V(512, 2, 4, 4, true),   V(1024, 1, 1, 16, true), V(1024, 1, 4, 4, true),
+        V(1024, 1, 4, 8, false), V(256, 4, 4, 4, true),   V(256, 2, 4, 8, true),
+    };
+    hipStream_t st[8];
+    for (int i = 0; i < S; ++i) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    hipEvent_t e0[iso], e1[iso];
+    for (int i = 0; i < iso; ++i) {
+        CK(hipEventCreate(&e0[i]));
+        CK(hipEventCreate(&e1[i]));
+    }
+    std::printf("batch %llu MiB x %d rotating, %d streams\n", (unsigned long long)(batch >> 20), nb, S);
+    for (int rep = 0; rep < 2; ++rep)
+        for (auto &v : vs) {
+            const dim3 grid(256 * v.wpc), blk(v.wgt);
+            for (int i = 0; i < 8; ++i) hipLaunchKernelGGL(v.k, grid, blk, 0, st[0], buf + (i % nb) * batch, batch, out);
+            CK(hipStreamSynchronize(st[0]));
+            for (int i = 0; i < iso; ++i)
+                hipExtLaunchKernelGGL(v.k, grid, blk, 0, st[0], e0[i], e1[i], 0, buf + (i % nb) * batch, batch, out);
+            CK(hipStreamSynchronize(st[0]));
+            double sum = 0;
+            for (int i = 0; i < iso; ++i) {
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0[i], e1[i]));
+                sum += ms;
+            }
+            const double us = 1e3 * sum / iso;
+            CK(hipDeviceSynchronize());
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < pipe_n; ++i)
+                hipLaunchKernelGGL(v.k, grid, blk, 0, st[i % S], buf + (i % nb) * batch, batch, out);
+            CK(hipDeviceSynchronize());
+            const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            std::printf("%-28s isolated %6.2f us = %6.0f GB/s   pipelined %6.0f GiB/s = %6.0f GB/s\n", v.name, us,
+                        batch / us * 1e-3, batch * pipe_n / s / (1u << 30), batch * pipe_n / s * 1e-9);
+        }
+    return 0;
+}
