@@ -180,10 +180,12 @@ __device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typena
     const Edges e = buffer_edges<LIST>(p, b);
     if (e.end > e.tail) fin = fold_bytes(fin, e.tail, e.end, eng);
     fin = ~fin;
+    // result stores are inline asm: a compiler-visible store inside a scan loop makes the loop-header
+    // merge of the compiler's wait counts pessimistic (it then drains the payload ring early)
     if (E::W == 32)
-        ((uint32_t *)p.d_out)[b] = (uint32_t)fin;
+        asm volatile("global_store_dword %0, %1, off" : : "v"((uint32_t *)p.d_out + b), "v"((uint32_t)fin) : "memory");
     else
-        ((uint64_t *)p.d_out)[b] = (uint64_t)fin;
+        asm volatile("global_store_dwordx2 %0, %1, off" : : "v"((uint64_t *)p.d_out + b), "v"((uint64_t)fin) : "memory");
 }
 
 // r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time
@@ -241,6 +243,11 @@ constexpr uint32_t kT0Off = kPcolOff + 4096;          // plain byte table (1 KiB
 constexpr uint32_t kConstFlagOff = kT0Off + 1024;     // waves that have published their K / P words
 constexpr uint32_t kPoolOff = kConstFlagOff + 4;      // workgroup tile pool: tiles claimed so far
 constexpr uint32_t kBraidLds = kConstFlagOff + 16;
+// streaming scans: workgroup-local buffer slots (tile registers of buffers whose tiles all lie in one
+// workgroup's range are combined with LDS atomics instead of device-scope ones)
+constexpr uint32_t kLocalSlots = 128;
+constexpr uint32_t kLocalOff = kBraidLds;
+constexpr uint32_t kStreamLds = kLocalOff + 8 * kLocalSlots;
 constexpr int kBraidBlock = 512;                      // 8 waves; two workgroups per CU
 constexpr int kBraidWaves = kBraidBlock / kWave;
 
@@ -748,36 +755,51 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
 // ------------------------------------------------------------------------------------------
 // W = 32 streaming scan for uniform batches whose main region is a whole number of tiles (no
 // virtual front pad): 1024 x 64 KiB, 16 x 256 MiB, 131072 x 8 KiB.  The same braided rows, tables
-// and tile combine as crc32_braid_kernel, with a three-slot register ring whose vmcnt accounting is
-// explicit instead of left to the compiler:
+// and tile combine as crc32_braid_kernel, restructured so the compiler's wait counts stay precise:
 //
-//  * Payload rows are loaded by inline asm, so the compiler's wait-count pass never sees them.  Every
-//    scan step issues exactly 16 row loads (the group two ahead; past the wave's last group the rows
-//    of the L2-resident constant block instead), so when row r of the scanned slot is needed exactly
-//    32 loads are younger than it (the rest of its group, the next group, and the r + 1 rows issued
-//    this step): one `s_waitcnt vmcnt(32)` per row, never a drain.  Loads complete in order, so
-//    younger non-load operations (tile-finish stores) can only make such a wait longer, never short.
-//  * Two groups (8 KiB per wave) are in flight when a group's scan starts and a third streams out
-//    between its table steps.  The compiler-managed ring of the generic kernel merged its paths into
-//    a full `vmcnt(0)` drain per group, so a wave waited one whole HBM latency for every 4 KiB.
+//  * A three-slot register ring on one code path: while group g is scanned, group g+1 is in flight
+//    and group g+2 streams out between the table steps (8-12 KiB per wave in flight).  Past a wave's
+//    last group the placeholder rows read the L2-resident constant block, so every step issues the
+//    same 16 loads.  The generic kernel's merged paths left the compiler a full vmcnt(0) drain per
+//    group, so a wave waited one whole HBM latency for every 4 KiB.
+//  * Nothing else in the loop is a compiler-visible vector-memory operation: the combine atomics and
+//    result stores are inline asm (rare, self-waiting) and the tables' basis constants immediates.
+//    A returning atomic left pending across the loop made the compiler's loop-header merge drain
+//    the ring.
+//  * The row loads themselves stay compiler-visible.  Inline-asm loads with hand-counted waits were
+//    tried: the compiler may move or reuse the destination register of an in-flight asm load, and
+//    the returning data then overwrote live values (device faults).
 template <int R>
 __device__ __forceinline__ uint32_t gld_row(uint32_t voff, uint64_t sbase) {
-    uint32_t v;
-    asm volatile("global_load_dword %0, %1, %2 offset:%3 nt" : "=v"(v) : "v"(voff), "s"(sbase), "i"(R * kBraidRow) : "memory");
-    return v;
+    return __builtin_nontemporal_load((gu32 *)(sbase + voff + R * kBraidRow));
 }
 
-template <int R, class B>
+template <int R, class B, bool NOLOOK = false>
 __device__ __forceinline__ uint32_t stream_rows(uint32_t x, BGroup &cur, BGroup &nxt, uint32_t voff, uint64_t snext, const B &eng) {
     if constexpr (R < kBraidRowsPerGroup) {
         nxt.w[R] = gld_row<R>(voff, snext);
-        asm volatile("s_waitcnt vmcnt(32)" : "+v"(cur.w[R])::"memory");
-        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        if (NOLOOK)
+            x = (x * 3u) ^ cur.w[R];
+        else
+            x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
         __builtin_amdgcn_sched_barrier(0);
-        return stream_rows<R + 1>(x, cur, nxt, voff, snext, eng);
+        return stream_rows<R + 1, B, NOLOOK>(x, cur, nxt, voff, snext, eng);
     } else {
-        return eng.step(x);
+        return NOLOOK ? x : eng.step(x);
     }
+}
+
+// Keep a ring slot's registers live up to this point.  A row load whose value is never read (the
+// placeholder rows past a wave's last group) would otherwise leave its destination registers "free"
+// to the compiler while the load is still in flight, and the returning data would overwrite whatever
+// the compiler placed there (tile-finish temporaries, addresses).  Used after the final vmcnt(0).
+#define AMDCRC_R16(g) "+v"(g.w[0]), "+v"(g.w[1]), "+v"(g.w[2]), "+v"(g.w[3]), "+v"(g.w[4]), "+v"(g.w[5]), "+v"(g.w[6]), \
+    "+v"(g.w[7]), "+v"(g.w[8]), "+v"(g.w[9]), "+v"(g.w[10]), "+v"(g.w[11]), "+v"(g.w[12]), "+v"(g.w[13]),          \
+    "+v"(g.w[14]), "+v"(g.w[15])
+__device__ __forceinline__ void ring_drain(BGroup &a, BGroup &b, BGroup &c) {
+    asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R16(a)::"memory");
+    asm volatile("" : AMDCRC_R16(b));
+    asm volatile("" : AMDCRC_R16(c));
 }
 
 template <int R>
@@ -787,6 +809,22 @@ __device__ __forceinline__ void stream_issue(BGroup &g, uint32_t voff, uint64_t 
         stream_issue<R + 1>(g, voff, s);
     }
 }
+
+#ifdef AMDCRC_GUARD
+// Debug builds only (-DAMDCRC_GUARD): every global address the streaming scan forms is range-checked;
+// a bad one is recorded here and replaced, so a cursor bug reports instead of faulting the device.
+__device__ unsigned long long g_amdcrc_guard[4];
+__device__ __forceinline__ bool guard_ok(bool ok, int what, unsigned long long v) {
+    if (!ok) {
+        __hip_atomic_fetch_or(&g_amdcrc_guard[0], 1ull << what, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g_amdcrc_guard[1 + (what & 1)] = v;
+    }
+    return ok;
+}
+#define AMDCRC_GUARD_OK(c, w, v) guard_ok((c), (w), (unsigned long long)(v))
+#else
+#define AMDCRC_GUARD_OK(c, w, v) true
+#endif
 
 // Cross-tile combine for the streaming scan: the same group slots as braid_finish / braid_publish /
 // braid_resolve, with every global atomic in inline asm that waits for its own completion.  These
@@ -816,6 +854,7 @@ __device__ __forceinline__ void sx_store32(unsigned int *a, unsigned int v) {  /
 template <class B>
 __device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g, const B &eng, int lane) {
     if (g.slot == ~0ull) return;
+    if (!AMDCRC_GUARD_OK(g.slot < p.ntiles && g.b < p.nbuf, 4, g.slot)) return;
     unsigned long long old = 0;
     if (lane == 0) old = sx_xor64_ret(&p.d_acc1[g.slot], g.val);
     const unsigned long long now = rfl64(old) ^ g.val;
@@ -841,9 +880,16 @@ __device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g
     }
 }
 
+// Buffers [b0, b1) lie wholly inside this workgroup's tiles (T <= 32): combined in LDS slots
+struct LocalBufs {
+    uint64_t b0, b1;
+};
+
 template <class B>
-__device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc) {
+__device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc,
+                                              const LocalBufs &lb) {
     const uint32_t r = wave_xor_s(eng.mulK(u, lane));
+    if (!AMDCRC_GUARD_OK(d.b < p.nbuf && d.k < d.T, 2, d.b)) return;
     if (d.T == 1) {
         if (lane == 0) finalize<false>(p, d.b, r, eng);
         return;
@@ -853,6 +899,17 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
     const uint32_t colv = lds32(eng.L, kPcolOff + 4 * (m * 32 + (lane & 31)));
     const uint32_t sel = lane < 32 ? (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - lane, 1) : 0u;
     const uint32_t v = wave_xor_s(colv & sel);
+    if (d.b >= lb.b0 && d.b < lb.b1) {  // T <= 32 here: the group end is the buffer end
+        if (lane == 0) {
+            const unsigned long long add = (unsigned long long)v | (1ull << (32 + d.k));
+            unsigned long long *slot = (unsigned long long *)(eng.L + kLocalOff) + (d.b - lb.b0);
+            const unsigned long long now =
+                __hip_atomic_fetch_xor(slot, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ^ add;
+            const unsigned long long full = d.T >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << d.T) - 1) << 32);
+            if ((now & 0xFFFFFFFF00000000ull) == full) finalize<false>(p, d.b, (uint32_t)now, eng);
+        }
+        return;
+    }
     const uint64_t slot = d.tbase + g0;
     if (slot != acc.slot) {
         stream_publish(p, acc, eng, lane);
@@ -865,33 +922,46 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY, bool PRIME2>
+// Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
+//
+// DIAG (diagnostics only, wrong results): bit 0 skips the table build, bit 1 the tile finishes,
+// bit 2 replaces the table steps by a plain XOR (the ring and waits unchanged)
+template <uint32_t POLY, int DIAG = 0>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const ScanParams p) {
     using B = Braid32<POLY, true>;
-    __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
+    __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
 
     const int lane = threadIdx.x & 63;
+    const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
+    const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
+    const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
     const bool stamps = p.d_timeline != nullptr;
     auto stamp = [&](int i) {
         if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
     };
     stamp(0);
-    // geometry: G groups of 4 KiB per tile (power of two), T tiles per buffer, main at hoff of each
+    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
     const uint32_t G = p.seg / kGroupBytes;
-    const uint32_t gsh = __builtin_ctz(G);
     const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint64_t q1 = t1 << gsh;
     const uint32_t voff = 4u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
+    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    const uint32_t gsh = __builtin_ctz(G);
+    const uint64_t q1 = t1 << gsh;
+    const bool work = t0 < t1;
     // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
     uint64_t fq = t0 << gsh, fb = t0 / T, fk = t0 - fb * T;
     uint32_t fg = 0;
     auto f_addr = [&]() -> uint64_t {
-        return rfl64(fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy);
+        uint64_t a = fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
+        if (!AMDCRC_GUARD_OK(fq >= q1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
+                                                                 p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
+                             1, a))
+            a = dummy;
+        return rfl64(a);
     };
     auto f_next = [&]() {
         ++fq;
@@ -908,17 +978,18 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
     asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
     asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
-    const bool work = t0 < t1;
+    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
+    LocalBufs lb{0, 0};
+    if (T > 1 && T <= 32) {
+        const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
+        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
+    }
     BGroup ra, rb, rc;
     if (work) {
         stream_issue<0>(ra, voff, f_addr());
         f_next();
-        if (PRIME2) {
-            stream_issue<0>(rb, voff, f_addr());
-            f_next();
-        }
     }
-    {
+    if (!(DIAG & 1)) {
         const uint32_t i = threadIdx.x;
         const uint32_t q = (i >> 1) & 3u, h = i & 1u;
         uint32_t bq[8];
@@ -933,13 +1004,14 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
             *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
         }
         if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
-        if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
     }
+    if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
+    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(lds + kLocalOff))[threadIdx.x] = 0ull;
     stamp(4);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
-    if (work && !PRIME2) {
+    if (work) {
         stream_issue<0>(rb, voff, f_addr());
         f_next();
     }
@@ -967,7 +1039,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         return;
     }
 
-    // scan cursor
+    // scan cursor: tile d (buffer, index in buffer), group g, global group q
     Tile d;
     d.T = T;
     d.b = t0 / T;
@@ -976,16 +1048,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     d.vbase = 0;
     d.pad = 0;
     d.ngroups = G;
-    uint32_t g = 0;
+    uint32_t g = 0, u = 0;
     uint64_t q = t0 << gsh;
-    uint32_t u = 0;
     BGroupAcc acc{};
     acc.slot = ~0ull;
     auto step = [&](BGroup &cur, BGroup &nxt) {
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
         const uint64_t sn = f_addr();
         f_next();
-        u = stream_rows<0>(u, cur, nxt, voff, sn, eng);
+        u = stream_rows<0, B, (DIAG & 4) != 0>(u, cur, nxt, voff, sn, eng);
         if (!published) {
             asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
             publish_consts();
@@ -994,7 +1065,11 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         if (++g == G) {
             g = 0;
             await_consts();
-            stream_finish(p, d, u, eng, lane, acc);
+            if (DIAG & 2) {
+                if (u == 0x9e3779b9u) p.d_timeline[lane] = u;  // keep the scan live
+            } else {
+                stream_finish(p, d, u, eng, lane, acc, lb);
+            }
             if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
         }
     };
@@ -1006,7 +1081,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         step(rc, rb);
         if (q >= q1) break;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing placeholder rows
+    ring_drain(ra, rb, rc);  // the trailing placeholder rows
     stamp(2);
     stream_publish(p, acc, eng, lane);
     stamp(3);
@@ -1476,6 +1551,18 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineParams p) {
 
 }  // namespace
 
+// Debug builds (-DAMDCRC_GUARD): read and clear the streaming scan's guard record
+extern "C" __attribute__((visibility("default"))) int amdcrc_debug_guard(unsigned long long *out4) {
+#ifdef AMDCRC_GUARD
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_amdcrc_guard), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+    unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_amdcrc_guard), z, sizeof(z)) == hipSuccess ? 1 : -1;
+#else
+    (void)out4;
+    return 0;
+#endif
+}
+
 extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stream) {
     const unsigned blocks = (unsigned)((p->n + 255) / 256);
     hipStream_t s = (hipStream_t)stream;
@@ -1504,17 +1591,22 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     switch (alg) {
         case ALG_CRC32:
             if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
+                launch(crc32_stream_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
-            if (p->stream && !list && (p->dbg & 8192))  // diagnostics: prime two groups before the tables
-                launch(crc32_stream_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
+            if (p->stream && !list) {  // DIAG bits (diagnostics): AMDCRC_DEBUG bits 16-18
+                switch ((p->dbg >> 16) & 7) {
+                    case 1: launch(crc32_stream_kernel<kPoly32C, 1>, nblocks, kBraidBlock, s, p, ev); break;
+                    case 2: launch(crc32_stream_kernel<kPoly32C, 2>, nblocks, kBraidBlock, s, p, ev); break;
+                    case 4: launch(crc32_stream_kernel<kPoly32C, 4>, nblocks, kBraidBlock, s, p, ev); break;
+                    case 7: launch(crc32_stream_kernel<kPoly32C, 7>, nblocks, kBraidBlock, s, p, ev); break;
+                    default: launch(crc32_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev); break;
+                }
+            }
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
             else if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3

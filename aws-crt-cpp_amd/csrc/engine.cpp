@@ -329,7 +329,12 @@ struct ScanGeometry {
 };
 ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main) {
     const uint64_t wpb = width_of(alg) == 32 ? 8 : (uint64_t)kWavesPerBlock;
-    const uint64_t per_cu = width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
+    static const int wpc = [] {  // diagnostics: AMDCRC_WG_PER_CU forces the W=32 workgroups per CU
+        const char *e = std::getenv("AMDCRC_WG_PER_CU");
+        return e ? std::atoi(e) : 0;
+    }();
+    const uint64_t per_cu = width_of(alg) == 32 && wpc > 0 ? (uint64_t)wpc
+                            : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
     uint64_t cap = (uint64_t)d->cus * per_cu;
     static const double frac = [] {  // diagnostics: AMDCRC_GRID_FRAC caps the grid at a share of the slots
         const char *e = std::getenv("AMDCRC_GRID_FRAC");
@@ -432,6 +437,11 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     // measured slower on 1024 x 64 KiB (3704 vs 4380 GiB/s), while on 16 x 256 MiB and 131072 x 8 KiB
     // the pool gains 3-4 % at equal tiles.
     p.seg = choose_seg(d, ml * count, ml, 1);
+    static const uint32_t seg_env = [] {  // diagnostics: AMDCRC_SEG forces bytes per lane per tile
+        const char *e = std::getenv("AMDCRC_SEG");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    if (seg_env >= (uint32_t)kGroupBytes && (seg_env & (seg_env - 1)) == 0) p.seg = seg_env;
     const bool pool = width_of(alg) == 32 && ml > 0 && !(debug_flags() & 4096) && choose_seg(d, ml * count, ml, 2) == p.seg;
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const uint64_t T = ml ? (ml + tile - 1) / tile : 1;

@@ -44,8 +44,10 @@ __device__ __forceinline__ unsigned fold(typename Vec<LW>::T v) {
     else return v.x ^ v.y ^ v.z ^ v.w;
 }
 
-template <int WGT, int LW, int D, bool NT>
+template <int WGT, int LW, int D, bool NT, int LDSB = 0>
 __global__ __launch_bounds__(WGT) void readk(const uint8_t *base, uint64_t bytes, unsigned *out) {
+    __shared__ unsigned lds_pad[LDSB / 4 + 1];  // LDSB: the scan kernel's LDS footprint (occupancy)
+    if (LDSB && bytes == 1) lds_pad[threadIdx.x] = 1u, out[0] = lds_pad[threadIdx.x ^ 1];
     typedef typename Vec<LW>::T V;
     typedef __attribute__((address_space(1))) const V gV;
     constexpr int WAVES = WGT / 64;
@@ -88,6 +90,7 @@ struct Variant {
 };
 
 #define V(WGT, WPC, LW, D, NT) Variant{#WGT "t x" #WPC " LW" #LW " D" #D " NT" #NT, readk<WGT, LW, D, NT>, WGT, WPC}
+#define VL(WGT, WPC, LW, D, NT, L) Variant{#WGT "t x" #WPC " LW" #LW " D" #D " lds" #L, readk<WGT, LW, D, NT, L>, WGT, WPC}
 
 int main(int argc, char **argv) {
     const uint64_t batch = (argc > 1 ? atoll(argv[1]) : 64) << 20;
@@ -98,6 +101,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&out, 1 << 20));
     CK(hipMemset(buf, 0x5a, batch * nb));
     std::vector<Variant> vs = {
+        VL(512, 1, 1, 16, true, 78864), VL(512, 1, 1, 32, true, 78864), VL(512, 1, 1, 16, true, 40000),
         V(512, 1, 1, 16, true),  V(512, 1, 1, 16, false), V(512, 1, 1, 32, true), V(512, 2, 1, 16, true),
         V(512, 1, 2, 8, true),   V(512, 1, 2, 16, true),  V(512, 2, 2, 8, true),  V(512, 1, 4, 4, true),
         V(512, 1, 4, 8, true),   V(512, 2, 4, 4, true),   V(1024, 1, 1, 16, true), V(1024, 1, 4, 4, true),

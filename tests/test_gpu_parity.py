@@ -111,7 +111,11 @@ def test_config2_full_size(engine, alg):
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
 @pytest.mark.parametrize("L,off,count", [(8192, 0, 4096), (8192 + 16, 0, 300), (65536 + 48, 0, 200),
                                          (1000, 0, 257), (4096, 3, 1), (100, 0, 999), (1 << 20, 0, 16),
-                                         ((1 << 20) + 5, 7, 1), (0, 0, 5), (1, 0, 33), (17, 0, 64)])
+                                         ((1 << 20) + 5, 7, 1), (0, 0, 5), (1, 0, 33), (17, 0, 64),
+                                         # streaming scan (main region a whole number of tiles): fewer
+                                         # tiles than waves, head + tail bytes around whole tiles, and
+                                         # buffers of many 32-tile groups
+                                         (4096, 0, 5), (65554, 5, 300), (1 << 26, 0, 2)])
 def test_strided_shapes_with_seeds(engine, alg, L, off, count):
     import torch
 
