@@ -1300,6 +1300,24 @@ __device__ __forceinline__ void b64_finish(const ScanParams &p, const Tile &d, u
     }
 }
 
+// T'_t: two waves per table (t wave-uniform), each thread two entries x 8 copies; T0 (1024 threads)
+template <uint64_t POLY>
+__device__ __forceinline__ void b64_build_tables(char *lds) {
+    const uint32_t i = threadIdx.x, wv = i >> 6;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(wv >> 1);
+    const uint32_t reg = t >= 4 ? 0u : 1u, q = t >= 4 ? 7u - t : 3u - t;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const uint32_t e = ((wv & 1u) << 7) | ((uint32_t)n << 6) | (i & 63u);
+        const uint64_t v = basis64_rt<POLY>(t, e);
+        const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
+        char *row = lds + (reg << 16) + (e << 8) + (q << 6);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) *(v4u *)(row + (((h + i) & 3u) << 4)) = vv;  // rotated: spread banks
+    }
+    if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
+}
+
 template <uint64_t POLY, bool LIST, bool NT = true>
 __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams p) {
     using B = Braid64<POLY>;
@@ -1356,22 +1374,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     B64Group r0, r1;
     b64_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
     if (any) pf_advance();
-    {
-        // T'_t: two waves per table (t wave-uniform), each thread two entries x 8 copies; T0
-        const uint32_t i = threadIdx.x, wv = i >> 6;
-        const uint32_t t = __builtin_amdgcn_readfirstlane(wv >> 1);
-        const uint32_t reg = t >= 4 ? 0u : 1u, q = t >= 4 ? 7u - t : 3u - t;
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            const uint32_t e = ((wv & 1u) << 7) | ((uint32_t)n << 6) | (i & 63u);
-            const uint64_t v = basis64_rt<POLY>(t, e);
-            const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
-            char *row = lds + (reg << 16) + (e << 8) + (q << 6);
-#pragma unroll
-            for (int h = 0; h < 4; ++h) *(v4u *)(row + (((h + i) & 3u) << 4)) = vv;  // rotated: spread banks
-        }
-        if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
-    }
+    b64_build_tables<POLY>(lds);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
@@ -1418,6 +1421,159 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
         }
     } else {
         settle();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// W = 64 streaming scan (CRC64NVME) for uniform batches whose main region is a whole number of
+// tiles: crc32_stream_kernel's structure on crc64_braid_kernel's 512-byte rows.  A three-slot ring
+// of 8-row groups (4 KiB per wave per slot, 48 VGPRs) on one code path, placeholder rows past the
+// wave's last group, one static tile per wave slot, and the tile combine with self-waiting asm
+// atomics, so the compiler's wait counts for the row loads stay exact.
+template <int R>
+__device__ __forceinline__ uint64_t gld_row64(uint32_t voff, uint64_t sbase) {
+    return __builtin_nontemporal_load((gu64 *)(sbase + voff + R * kB64Row));
+}
+
+template <int R, class B>
+__device__ __forceinline__ uint64_t stream64_rows(uint64_t x, B64Group &cur, B64Group &nxt, uint32_t voff, uint64_t snext,
+                                                  const B &eng) {
+    if constexpr (R < kB64RowsPerGroup) {
+        nxt.w[R] = gld_row64<R>(voff, snext);
+        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return stream64_rows<R + 1>(x, cur, nxt, voff, snext, eng);
+    } else {
+        return eng.step(x);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void stream64_issue(B64Group &g, uint32_t voff, uint64_t s) {
+    if constexpr (R < kB64RowsPerGroup) {
+        g.w[R] = gld_row64<R>(voff, s);
+        stream64_issue<R + 1>(g, voff, s);
+    }
+}
+
+// b64_finish with self-waiting asm atomics: the tile register into its 32-tile group slot (value,
+// then arrival count); the group's last arrival moves the group to the buffer end and counts groups
+// per buffer; the buffer's last group finalises.
+template <class B>
+__device__ __forceinline__ void stream64_finish(const ScanParams &p, const Tile &d, uint64_t u, const B &eng, int lane) {
+    const uint64_t r = wave_xor64_s(eng.mulK(u));
+    if (d.T == 1) {
+        if (lane == 0) finalize<false>(p, d.b, r, eng);
+        return;
+    }
+    const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
+    const uint64_t v = mul_pcols<uint64_t, 64>(r, p.d_pcols + (gend - 1 - d.k) * 64);
+    const uint64_t slot = d.tbase + g0;
+    unsigned int c = 0;
+    if (lane == 0) {
+        (void)sx_xor64_ret(&p.d_acc1[slot], (unsigned long long)v);  // performed before it is counted
+        c = sx_add32_ret(&p.d_cnt1[slot], 1u);
+    }
+    c = __builtin_amdgcn_readfirstlane(c);
+    if (c != (unsigned int)(gend - g0 - 1)) return;
+    unsigned long long gv = 0;
+    if (lane == 0) {
+        gv = sx_swap64_ret(&p.d_acc1[slot], 0ull);
+        sx_store32(&p.d_cnt1[slot], 0u);
+    }
+    gv = rfl64(gv);
+    const uint64_t G = (d.T + 31) / 32;
+    if (G == 1) {
+        if (lane == 0) finalize<false>(p, d.b, (uint64_t)gv, eng);
+        return;
+    }
+    const uint64_t gs = d.T > gend ? mul_pcols<uint64_t, 64>((uint64_t)gv, p.d_pcols + (d.T - gend) * 64) : (uint64_t)gv;
+    if (lane == 0) {
+        (void)sx_xor64_ret(&p.d_acc[d.b], (unsigned long long)gs);
+        const unsigned int c2 = sx_add32_ret(&p.d_cnt[d.b], 1u);
+        if (c2 == (unsigned int)(G - 1)) {
+            const uint64_t fin = sx_swap64_ret(&p.d_acc[d.b], 0ull);
+            sx_store32(&p.d_cnt[d.b], 0u);
+            finalize<false>(p, d.b, fin, eng);
+        }
+    }
+}
+
+template <uint64_t POLY>
+__global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParams p) {
+    using B = Braid64<POLY>;
+    __shared__ __attribute__((aligned(16))) char lds[kB64Lds];
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
+    const uint32_t G = p.seg / kGroupBytes;
+    const uint32_t gsh = __builtin_ctz(G);
+    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
+    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
+    const uint32_t voff = 8u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
+    const uint64_t q1 = t1 << gsh;
+    const bool work = t0 < t1;
+    uint64_t fq = t0 << gsh, fb = t0 / T, fk = t0 - fb * T;
+    uint32_t fg = 0;
+    auto f_addr = [&]() -> uint64_t {
+        return rfl64(fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
+                             : dummy);
+    };
+    auto f_next = [&]() {
+        ++fq;
+        if (++fg == G) {
+            fg = 0;
+            if (++fk == T) fk = 0, ++fb;
+        }
+    };
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
+    B64Group ra, rb, rc;
+    if (work) {
+        stream64_issue<0>(ra, voff, f_addr());
+        f_next();
+    }
+    b64_build_tables<POLY>(lds);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    if (!work) return;
+    stream64_issue<0>(rb, voff, f_addr());
+    f_next();
+
+    Tile d;
+    d.T = T;
+    d.b = t0 / T;
+    d.k = t0 - d.b * T;
+    d.tbase = d.b * T;
+    d.vbase = 0;
+    d.pad = 0;
+    d.ngroups = G;
+    uint32_t g = 0;
+    uint64_t u = 0, q = t0 << gsh;
+    auto step = [&](B64Group &cur, B64Group &nxt) {
+        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0ull;
+        const uint64_t sn = f_addr();
+        f_next();
+        u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
+        ++q;
+        if (++g == G) {
+            g = 0;
+            stream64_finish(p, d, u, eng, lane);
+            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
+        }
+    };
+    for (;;) {
+        step(ra, rc);
+        if (q >= q1) break;
+        step(rb, ra);
+        if (q >= q1) break;
+        step(rc, rb);
+        if (q >= q1) break;
     }
 }
 
@@ -1617,7 +1773,9 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (list)
+            if (p->stream && !list)
+                launch(crc64_stream_kernel<kPoly64Nvme>, nblocks, kBlock, s, p, ev);
+            else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);
             else
                 launch(crc64_braid_kernel<kPoly64Nvme, false>, nblocks, kBlock, s, p, ev);

@@ -304,10 +304,11 @@ inline uint64_t main_len(uint64_t ptr, uint64_t n) {
 
 // Bytes per lane per tile.  A tile is 64*seg bytes; pick the largest seg (fewest partials to
 // combine) that still gives every wavefront slot on the chip a tile and does not exceed the
-// typical buffer.
-// typical buffer.  per_slot: tiles wanted per wave slot (2 when a dynamic pool balances the waves).
-uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main, uint64_t per_slot = 1) {
-    const uint64_t slots = (uint64_t)d->cus * kWavesPerBlock * per_slot;
+// typical buffer.  per_slot: tiles wanted per wave slot (2 when a dynamic pool balances the waves);
+// waves_per_cu: the launch's wave slots per CU.
+uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main, uint64_t per_slot = 1,
+                    uint64_t waves_per_cu = kWavesPerBlock) {
+    const uint64_t slots = (uint64_t)d->cus * waves_per_cu * per_slot;
     uint64_t seg = 4096;
     while (seg > kGroupBytes && (total_main / (seg * kWave) < slots || seg * kWave > std::max<uint64_t>(typical_main, 1)))
         seg >>= 1;
@@ -437,12 +438,21 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     // measured slower on 1024 x 64 KiB (3704 vs 4380 GiB/s), while on 16 x 256 MiB and 131072 x 8 KiB
     // the pool gains 3-4 % at equal tiles.
     p.seg = choose_seg(d, ml * count, ml, 1);
+    // Batches whose main regions are whole tiles take the streaming scans (crc_kernels.hip
+    // crc32_stream_kernel / crc64_stream_kernel; AMDCRC_DEBUG bit 14 disables them).  Their tiles are
+    // sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C measured 5250-5315 GiB/s with
+    // one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
+    const bool w32 = width_of(alg) == 32;
+    const uint64_t wpc = w32 ? 8 * (ml * count >= kSmallBatchBytes ? 2 : 1) : (uint64_t)kWavesPerBlock;
+    const uint32_t seg_stream = choose_seg(d, ml * count, ml, 1, wpc);
+    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0 && !(debug_flags() & 16384);
+    if (stream) p.seg = seg_stream;
     static const uint32_t seg_env = [] {  // diagnostics: AMDCRC_SEG forces bytes per lane per tile
         const char *e = std::getenv("AMDCRC_SEG");
         return e ? (uint32_t)std::atoi(e) : 0u;
     }();
     if (seg_env >= (uint32_t)kGroupBytes && (seg_env & (seg_env - 1)) == 0) p.seg = seg_env;
-    const bool pool = width_of(alg) == 32 && ml > 0 && !(debug_flags() & 4096) && choose_seg(d, ml * count, ml, 2) == p.seg;
+    const bool pool = w32 && ml > 0 && !(debug_flags() & 4096) && choose_seg(d, ml * count, ml, 2) == p.seg;
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const uint64_t T = ml ? (ml + tile - 1) / tile : 1;
     p.base = base;
@@ -454,9 +464,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     p.d_seeds = d_seeds;
     p.seed_all = seed_all;
     p.d_out = d_out;
-    // W=32 batches whose main regions are whole tiles take the streaming scan (explicit three-slot
-    // ring, static tiles; crc_kernels.hip crc32_stream_kernel).  AMDCRC_DEBUG bit 14 disables it.
-    p.stream = width_of(alg) == 32 && ml > 0 && ml % tile == 0 && !(debug_flags() & 16384) ? 1u : 0u;
+    p.stream = stream && ml % tile == 0 ? 1u : 0u;
     if (pool && !p.stream) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
         const ScanGeometry geo = scan_geometry(d, alg, p.ntiles, ml * count);
