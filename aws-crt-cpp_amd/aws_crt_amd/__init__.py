@@ -94,6 +94,15 @@ def time_next_launch(start_event, stop_event) -> None:
     L.aws_crt_amd_debug_time_next_launch(start_event.cuda_event, stop_event.cuda_event)
 
 
+def read_ceiling(base, nbytes: int, stream=None, base_offset: int = 0) -> None:
+    """Diagnostics: one launch of the streaming-read ceiling kernel (the W=32 streaming scan's launch
+    shape, CRC removed) over nbytes of device memory; honours time_next_launch."""
+    L = lib()
+    L.aws_crt_amd_debug_read_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    addr = (base.data_ptr() if hasattr(base, "data_ptr") else int(base)) + base_offset
+    _check(L.aws_crt_amd_debug_read_ceiling(addr, nbytes, _stream_handle(stream)))
+
+
 def event_ms(start_event, stop_event) -> float:
     """Milliseconds between two events stamped by time_next_launch."""
     L = lib()

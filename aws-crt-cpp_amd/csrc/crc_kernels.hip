@@ -1707,6 +1707,55 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineParams p) {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------
+// Streaming-read ceiling (diagnostics; SURVEY.md §8(d) "secondary denominator"): the W=32 streaming
+// scan's launch shape with the CRC removed -- 512-thread workgroups, one per CU, each wave a
+// contiguous slab read as 256-byte non-temporal rows, two 16-row groups in flight, XOR-reduced.
+// What an HBM-bound kernel of this shape can reach for the same bytes per launch.
+__global__ __launch_bounds__(kBraidBlock) void read_ceiling_kernel(const uint8_t *base, uint64_t bytes, uint32_t *sink) {
+    constexpr int D = kBraidRowsPerGroup;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves, gw = (uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6);
+    const uint64_t rows = bytes / kBraidRow, r0 = gw * rows / nw, r1 = (gw + 1) * rows / nw;
+    const uint64_t a0 = (uint64_t)base + r0 * kBraidRow + 4u * lane;
+    const uint64_t ng = (r1 - r0) / D;
+    uint32_t s0[D], s1[D], acc = 0;
+    auto ld = [&](uint32_t *s, uint64_t g) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) s[i] = __builtin_nontemporal_load((gu32 *)(a0 + (g * D + i) * kBraidRow));
+    };
+    auto use = [&](const uint32_t *s) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) acc = acc * 3u ^ s[i];
+    };
+    if (ng) ld(s0, 0);
+    for (uint64_t g = 0; g < ng;) {
+        if (g + 1 < ng) ld(s1, g + 1);
+        use(s0);
+        if (++g >= ng) break;
+        if (g + 1 < ng) ld(s0, g + 1);
+        use(s1);
+        ++g;
+    }
+    if (acc == 0x9E3779B9u) sink[gw] = acc;  // keeps the loads live; practically never stored
+}
+
+extern "C" int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint32_t *sink, int nblocks, void *stream,
+                                          void *const *ev) {
+    struct Args {
+        const uint8_t *b;
+        uint64_t n;
+        uint32_t *s;
+    } a{(const uint8_t *)base, bytes, sink};
+    hipStream_t s = (hipStream_t)stream;
+    if (ev && (ev[0] || ev[1]))
+        hipExtLaunchKernelGGL(read_ceiling_kernel, dim3(nblocks), dim3(kBraidBlock), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0,
+                              a.b, a.n, a.s);
+    else
+        hipLaunchKernelGGL(read_ceiling_kernel, dim3(nblocks), dim3(kBraidBlock), 0, s, a.b, a.n, a.s);
+    return (int)hipGetLastError();
+}
+
 // Debug builds (-DAMDCRC_GUARD): read and clear the streaming scan's guard record
 extern "C" __attribute__((visibility("default"))) int amdcrc_debug_guard(unsigned long long *out4) {
 #ifdef AMDCRC_GUARD

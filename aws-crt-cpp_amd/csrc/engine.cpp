@@ -735,6 +735,23 @@ AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_e
     return ms;
 }
 
+// Diagnostics: one launch of the streaming-read ceiling kernel (crc_kernels.hip read_ceiling_kernel)
+// over [d_base, d_base + bytes), in the W=32 streaming scan's small-batch shape (one 512-thread
+// workgroup per CU).  Honours aws_crt_amd_debug_time_next_launch.
+AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t bytes, void *hip_stream) {
+    Device *d;
+    int rc = get_device(&d);
+    if (rc) return rc;
+    static DevBuf sink;  // one word per wave (practically never written)
+    {
+        std::lock_guard<std::mutex> g(d->mu);
+        if (!sink.p) HIP_TRY(hipMalloc(&sink.p, (size_t)d->cus * 8 * sizeof(uint32_t)));
+    }
+    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)sink.p, d->cus, hip_stream, g_time_events);
+    g_time_events[0] = g_time_events[1] = nullptr;
+    return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+}
+
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,
                                                  const void *d_seeds, void *d_out, void *hip_stream) {
     if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");

@@ -93,4 +93,5 @@ int amdcrc_launch_combine(int alg, const amdcrc::CombineParams *p, void *stream)
 int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *stream, void *const *events);
 int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream, void *const *events);
 int amdcrc_launch_xxh3(int bits, const amdcrc::XxhParams *p, void *stream, void *const *events);
+int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint32_t *sink, int nblocks, void *stream, void *const *events);
 }

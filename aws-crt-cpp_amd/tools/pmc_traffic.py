@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--rdreq")
-    ap.add_argument("--kernel", default="crc32_braid_kernel")
+    ap.add_argument("--kernel", default="crc32_stream_kernel")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--bytes-per-launch", type=int, required=True)
     a = ap.parse_args()

@@ -25,6 +25,8 @@ back D2H.  Reported as `e2e_pinned` next to `value`, never as `value`.
 
 Prints one JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per launch (1 byte read per
 payload byte) / mean kernel duration from HIP events recorded on the launch stream.
+`roofline.read_ceiling` = the same two measurements for a read-only XOR-reduce kernel of the same
+launch shape over the same batches (the achievable streaming read for this bytes-per-launch).
 `cpu_baseline` = the oracle's SSE4.2 crc32q 3-way path (the technique class of aws-checksums)
 timed on this host over a bounded sample, rank 0 at N=1 only.
 """
@@ -58,6 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-read-ceiling", action="store_true", help="skip the streaming-read ceiling kernel")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
     return ap.parse_args()
 
@@ -237,6 +240,33 @@ def main():
     kernel_ms = sum(durs) / nt
     achieved_gbs = step_bytes / (kernel_ms * 1e-3) / 1e9
 
+    # secondary denominator: the streaming-read ceiling of this launch shape -- the
+    # same batches read by an XOR-reduce kernel with the W=32 scan's geometry, timed the same two ways
+    ceiling = None
+    if not args.no_read_ceiling:
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(40e6))
+        for i in range(nt):
+            starts[i].record(st)
+            ends[i].record(st)
+            eng.time_next_launch(starts[i], ends[i])
+            eng.read_ceiling(data, step_bytes, stream=st, base_offset=(i % nb) * step_bytes)
+        torch.cuda.synchronize()
+        rc_ms = sum(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends)) / nt
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            eng.read_ceiling(data, step_bytes, stream=streams[i % len(streams)], base_offset=(i % nb) * step_bytes)
+        torch.cuda.synchronize()
+        rc_el = time.perf_counter() - t1
+        rc_gbs = step_bytes / (rc_ms * 1e-3) / 1e9
+        ceiling = {"kernel_ms": round(rc_ms, 5), "achieved": round(rc_gbs, 1), "unit": "GB/s",
+                   "pipelined_gibs": round(args.steps * step_bytes / max(rc_el, 1e-9) / 2**30, 2),
+                   "scan_frac_of_ceiling": round(achieved_gbs / rc_gbs, 4),
+                   "kernel": "read_ceiling_kernel: same launch shape, 256-B non-temporal rows XOR-reduced"}
+
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -284,7 +314,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel_ms": round(kernel_ms, 5), "kernel_ms_median": round(durs[nt // 2], 5),
-                         "bytes_per_launch": step_bytes, "timing_launches": nt},
+                         "bytes_per_launch": step_bytes, "timing_launches": nt, "read_ceiling": ceiling},
             "cpu_baseline": cpu,
             "e2e_pinned": e2e,
         }
