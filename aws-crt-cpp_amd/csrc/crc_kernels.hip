@@ -602,7 +602,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // memory system is saturated (every CU primes at once), so priming two groups kept the first scan
     // waiting for 8 KiB per wave to be accepted.  The ring scans group 0 while group 1's loads go out
     // between its table steps.
-    BGroup r0, r1, r2;
+    BGroup r0, r1;
     braid_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
     if (any && !dyn) pf_advance();  // pool mode: after the barrier, where the pool counter is set up
     {
@@ -634,14 +634,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // pool mode: the prefetch cursor may reach the pool only now (the host gives every wave of a
     // pooled launch a static tile with payload, so a wave's pool tiles always follow it)
     if (dyn && any) pf_advance();
-    // Three-slot ring: the second group goes out now, so that while group g is scanned group g+1 is
-    // already in flight and group g+2 streams out between the table steps.  With two slots a wave had
-    // 4-8 KiB in flight and waited one full HBM latency per group (2048 waves x 4 KiB / ~1.7 us ~
-    // 5 TB/s on 1024 x 64 KiB); three slots keep 8-12 KiB per wave in flight.
-    if (any && !pf_done) {
-        braid_load<NT>(r1, fvb, fpad, gf, lane);
-        pf_advance();
-    }
     stamp(1);
     // Every wave publishes its 1/8 of the K image and P columns once its constants have arrived
     // (after its first group, by which time they have: loads retire in order) and counts itself in
@@ -730,15 +722,13 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
         // leading tiles without payload finish before the primed group is reached: publish first then
         if (dp.ngroups == 0) publish_consts();
         if (settle()) {
-            ring_step(r0, r2);
+            ring_step(r0, r1);
             publish_consts();
             for (;;) {
                 if (!settle()) break;
                 ring_step(r1, r0);
                 if (!settle()) break;
-                ring_step(r2, r1);
-                if (!settle()) break;
-                ring_step(r0, r2);
+                ring_step(r0, r1);
             }
         }
     } else {
@@ -950,14 +940,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
     const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
     const uint32_t gsh = __builtin_ctz(G);
-    const uint64_t q1 = t1 << gsh;
+    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
     const bool work = t0 < t1;
     // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
-    uint64_t fq = t0 << gsh, fb = t0 / T, fk = t0 - fb * T;
+    uint32_t fq = 0;  // groups issued
+    uint64_t fb = t0 / T, fk = t0 - fb * T;
     uint32_t fg = 0;
     auto f_addr = [&]() -> uint64_t {
-        uint64_t a = fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
-        if (!AMDCRC_GUARD_OK(fq >= q1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
+        uint64_t a = fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
+        if (!AMDCRC_GUARD_OK(fq >= nq || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
                                                                  p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
                              1, a))
             a = dummy;
@@ -1049,7 +1040,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     d.pad = 0;
     d.ngroups = G;
     uint32_t g = 0, u = 0;
-    uint64_t q = t0 << gsh;
+    uint32_t q = 0;  // groups scanned
     BGroupAcc acc{};
     acc.slot = ~0ull;
     auto step = [&](BGroup &cur, BGroup &nxt) {
@@ -1075,11 +1066,11 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     };
     for (;;) {
         step(ra, rc);
-        if (q >= q1) break;
+        if (q >= nq) break;
         step(rb, ra);
-        if (q >= q1) break;
+        if (q >= nq) break;
         step(rc, rb);
-        if (q >= q1) break;
+        if (q >= nq) break;
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
     stamp(2);
@@ -1515,12 +1506,13 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParam
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
     const uint32_t voff = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
-    const uint64_t q1 = t1 << gsh;
+    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
     const bool work = t0 < t1;
-    uint64_t fq = t0 << gsh, fb = t0 / T, fk = t0 - fb * T;
+    uint32_t fq = 0;  // groups issued
+    uint64_t fb = t0 / T, fk = t0 - fb * T;
     uint32_t fg = 0;
     auto f_addr = [&]() -> uint64_t {
-        return rfl64(fq < q1 ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
+        return rfl64(fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
                              : dummy);
     };
     auto f_next = [&]() {
@@ -1554,7 +1546,8 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParam
     d.pad = 0;
     d.ngroups = G;
     uint32_t g = 0;
-    uint64_t u = 0, q = t0 << gsh;
+    uint64_t u = 0;
+    uint32_t q = 0;  // groups scanned
     auto step = [&](B64Group &cur, B64Group &nxt) {
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0ull;
         const uint64_t sn = f_addr();
@@ -1569,11 +1562,11 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParam
     };
     for (;;) {
         step(ra, rc);
-        if (q >= q1) break;
+        if (q >= nq) break;
         step(rb, ra);
-        if (q >= q1) break;
+        if (q >= nq) break;
         step(rc, rb);
-        if (q >= q1) break;
+        if (q >= nq) break;
     }
 }
 

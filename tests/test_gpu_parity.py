@@ -151,6 +151,49 @@ def test_ragged_list_random(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
+def test_fuzz_lengths_alignments_seeds(engine, alg):
+    """GPU-vs-oracle differential fuzzing: 2000 buffers of uniformly random length
+    0..4200, every start alignment mod 16, random seeds, one ragged batch (fixed RNG seed)."""
+    import torch
+
+    rng = random.Random(0xF022 + ALG[alg])
+    lens = [rng.randrange(0, 4201) for _ in range(2000)]
+    offs, pos = [], 0
+    for ln in lens:
+        pos = (pos + 15) // 16 * 16 + rng.randrange(16)
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 11 + ALG[alg])
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.checksum(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+def test_fuzz_strided_shapes(engine, alg):
+    """Random uniform batches (count, length, base alignment, stride slack), half of them whole-tile
+    shapes that take the streaming scans, with random seeds (fixed RNG seed)."""
+    import torch
+
+    rng = random.Random(0x5712 + ALG[alg])
+    for _ in range(12):
+        L = 4096 * rng.choice([1, 2, 3, 8, 16, 24]) if rng.random() < 0.5 else rng.randrange(1, 70000)
+        count = rng.randrange(1, 1500)
+        off = rng.choice([0, 0, rng.randrange(16)])
+        stride = (L + 15) // 16 * 16 + 16 * rng.randrange(3) if count > 1 else L
+        d = dev_random(stride * count + off + 16, rng.randrange(1 << 30))
+        seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in range(count)]
+        out = engine.checksum_strided(ALG[alg], d, stride, L, count, seeds=seeds_tensor(alg, seeds), base_offset=off)
+        torch.cuda.synchronize()
+        h = host_bytes(d)
+        want = [oracle.crc(alg, h[off + i * stride: off + i * stride + L], seeds[i]) for i in range(count)]
+        assert engine.as_unsigned(out) == want, (L, count, off, stride)
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c"])
 def test_config3_chunked_running_crc(engine, alg):
     """BASELINE config 3 shape (256 MiB buffers, 8 MiB chunks): one-shot == chained == combine."""
