@@ -164,20 +164,22 @@ int get_kvals(Device *d, int alg, uint32_t seg, const uint64_t **out) {
 // x^-1 * t : inverse of gf2_mulx (the reflected polynomial's top bit is the x^0 coefficient, 1)
 inline uint32_t inv_mulx32(uint32_t t, uint32_t poly) { return (t & 0x80000000u) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 
-// W=32 braided-scan constants (layout: engine.h kBraidConstWords)
-int get_braid_consts(Device *d, int alg, const uint64_t **out) {
-    auto it = d->braid.find(alg);
+// W=32 braided-scan constants (layout: engine.h kBraidConstWords).  word_bytes: bytes per lane per
+// row (4: 256-byte rows, K_l = x^(-32 l); 8: the 512-byte-row streaming scan, K_l = x^(-64 l))
+int get_braid_consts(Device *d, int alg, const uint64_t **out, int word_bytes = 4) {
+    const int key = alg + (word_bytes == 8 ? 16 : 0);
+    auto it = d->braid.find(key);
     if (it == d->braid.end()) {
         const uint32_t poly = (uint32_t)alg_poly(alg);
         std::vector<uint32_t> c(kBraidConstWords, 0);
-        uint32_t kl = 0x80000000u;  // x^0, then x^(-32 l)
+        uint32_t kl = 0x80000000u;  // x^0, then x^(-8 word_bytes l)
         for (int l = 0; l < 64; ++l) {
             uint32_t col = kl;
             for (int j = 0; j < 32; ++j) {
                 c[((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
                 col = (uint32_t)gf2_mulx(col, poly);
             }
-            for (int i = 0; i < 32; ++i) kl = inv_mulx32(kl, poly);
+            for (int i = 0; i < 8 * word_bytes; ++i) kl = inv_mulx32(kl, poly);
         }
         const uint64_t skip = gf2_xpow8n(kBraidRow - 4, poly, 32);
         for (int i = 0; i < 1024; ++i)
@@ -186,7 +188,7 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
         DevBuf b;
         int rc = upload(b, c.data(), c.size() * 4);
         if (rc) return rc;
-        it = d->braid.emplace(alg, b).first;
+        it = d->braid.emplace(key, b).first;
     }
     *out = (const uint64_t *)it->second.p;
     return 0;
@@ -382,7 +384,8 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     }
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const bool braided = width_of(alg) == 32 || !(p.dbg & 2048);  // dbg 2048: first-generation W=64 scan
-    int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals)
+    const int word_bytes = p.stream && alg == ALG_CRC32C && (p.dbg & 32768) ? 8 : 4;  // crc32_stream8_kernel
+    int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals, word_bytes)
              : braided           ? get_braid64_consts(d, alg, &p.d_kvals)
                                  : get_kvals(d, alg, p.seg, &p.d_kvals);
     if (rc) return rc;
