@@ -36,6 +36,46 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def test_slice_bounds_partition_is_exact():
+    for total in (0, 1, 4095, 4096, 4097, 10 ** 6, 1 << 30):
+        for world in (1, 2, 3, 8):
+            sl = [sharding.slice_bounds(total, r, world) for r in range(world)]
+            assert sl[0].start == 0 and sl[-1].stop == total
+            assert all(a.stop == b.start for a, b in zip(sl, sl[1:]))
+            assert all(s.start % 4096 == 0 for s in sl if len(s))
+
+
+def _split_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = random.Random(99).randbytes(3 * 1000 * 1000 + 17)  # same buffer on every rank
+    ok = []
+    for alg in ("crc32", "crc32c", "crc64nvme"):
+        got = sharding.split_buffer_crc(alg, len(data), lambda sl: oracle.crc(alg, data[sl.start:sl.stop]))
+        ok.append(got == oracle.crc(alg, data))
+    q.put((rank, all(ok)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_split_buffer_combine():
+    """One huge buffer split into contiguous per-rank slices, slice CRCs folded with the engine's
+    host-side Combine; the oracle stands in for each rank's GPU."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30600 + random.Random().randrange(1000)
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok in res), res
+
+
 @pytest.mark.parametrize("world", [2])
 def test_gloo_world2_gather_matches_single_rank(world):
     ctx = mp.get_context("spawn")
