@@ -1136,7 +1136,14 @@ __device__ __forceinline__ uint64_t basis64_rt(uint32_t t, uint32_t e) {  // t w
     }
 }
 
-template <uint64_t POLY>
+// COPIES = 8: the layout above (two 64 KiB regions).  COPIES = 4 (crc64_stream4_kernel): one
+// 64 KiB region, row e = the low dword's four tables in bytes [0, 128) and the high dword's in
+// [128, 256), quarter q = 4 copies x 8 bytes; a ds_read_b64 half-wave then meets 16 slots (2-way
+// bank conflicts) but two workgroups share a CU.
+constexpr uint32_t kB64x4T0Off = 65536;
+constexpr uint32_t kB64x4Lds = kB64x4T0Off + 2048;
+
+template <uint64_t POLY, int COPIES = 8>
 struct Braid64 {
     using T = uint64_t;
     static constexpr int W = 64;
@@ -1146,13 +1153,19 @@ struct Braid64 {
 
     __device__ void init(const char *lds, int lane) {
         L = lds;
-        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
+        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & (COPIES - 1u);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t q = (k + j) & 3u;
-            cst[k] = (q << 6) | (cp << 3);
-            csth[k] = cst[k] | 0x10000u;
-            sel[k] = 0x0c060004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a, byte2 <- region
+            if (COPIES == 8) {
+                cst[k] = (q << 6) | (cp << 3);
+                csth[k] = cst[k] | 0x10000u;
+                sel[k] = 0x0c060004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a, byte2 <- region
+            } else {
+                cst[k] = (q << 5) | (cp << 3);
+                csth[k] = cst[k] | 0x80u;         // high dword's tables: second half of the row
+                sel[k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a
+            }
         }
     }
     // a * x^(8*512) ^ wn
@@ -1174,7 +1187,7 @@ struct Braid64 {
     __device__ __forceinline__ uint64_t step(uint64_t a) const { return step_x(a, 0); }
     // plain byte step for head / tail bytes (s wave-uniform: broadcast reads)
     __device__ __forceinline__ uint64_t byte(uint64_t s, uint32_t b) const {
-        return (s >> 8) ^ lds64(L, kB64T0Off + 8 * (((uint32_t)s ^ b) & 0xffu));
+        return (s >> 8) ^ lds64(L, (COPIES == 8 ? kB64T0Off : kB64x4T0Off) + 8 * (((uint32_t)s ^ b) & 0xffu));
     }
     // r * K_l, bit-serial (once per tile)
     __device__ __forceinline__ uint64_t mulK(uint64_t r) const {
@@ -1307,6 +1320,25 @@ __device__ __forceinline__ void b64_build_tables(char *lds) {
         for (int h = 0; h < 4; ++h) *(v4u *)(row + (((h + i) & 3u) << 4)) = vv;  // rotated: spread banks
     }
     if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
+}
+
+// the 4-copy layout (Braid64<POLY, 4>) from 512 threads: thread i fills table t = i >> 6 (wave-
+// uniform) for entries (i & 63) + 64 n, n < 4, two 16-byte stores (4 copies) each; then T0
+template <uint64_t POLY>
+__device__ __forceinline__ void b64x4_build_tables(char *lds) {
+    const uint32_t i = threadIdx.x;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(i >> 6);
+    const uint32_t reg = t >= 4 ? 0u : 1u, q = t >= 4 ? 7u - t : 3u - t;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const uint32_t e = (i & 63u) + 64u * n;
+        const uint64_t v = basis64_rt<POLY>(t, e);
+        const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
+        char *row = lds + (e << 8) + (reg << 7) + (q << 5);
+        *(v4u *)(row + (((i >> 2) & 1u) << 4)) = vv;
+        *(v4u *)(row + ((((i >> 2) & 1u) ^ 1u) << 4)) = vv;
+    }
+    if (i < 256) *(uint64_t *)(lds + kB64x4T0Off + 8 * i) = basis64<POLY, 8>(i);
 }
 
 template <uint64_t POLY, bool LIST, bool NT = true>
@@ -2042,6 +2074,91 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParam
     }
 }
 
+// The same scan on the 4-copy table layout (66 KiB of LDS) in 512-thread workgroups, two per CU, so
+// a launch queued on another stream co-resides with the running one.  The default W=64 streaming
+// scan: C5 pipelined 5500-5558 vs 5138-5143 GiB/s for the 8-copy kernel (AMDCRC_DEBUG bit 20), at a
+// 4 % slower isolated launch (2-way bank conflicts on the lookups).
+template <uint64_t POLY>
+__global__ __launch_bounds__(kBraidBlock, 4) void crc64_stream4_kernel(const ScanParams p) {
+    using B = Braid64<POLY, 4>;
+    __shared__ __attribute__((aligned(16))) char lds[kB64x4Lds];
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
+    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
+    const uint32_t G = p.seg / kGroupBytes;
+    const uint32_t gsh = __builtin_ctz(G);
+    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
+    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
+    const uint32_t voff = 8u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
+    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
+    const bool work = t0 < t1;
+    uint32_t fq = 0;  // groups issued
+    uint64_t fb = t0 / T, fk = t0 - fb * T;
+    uint32_t fg = 0;
+    auto f_addr = [&]() -> uint64_t {
+        return rfl64(fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
+                             : dummy);
+    };
+    auto f_next = [&]() {
+        ++fq;
+        if (++fg == G) {
+            fg = 0;
+            if (++fk == T) fk = 0, ++fb;
+        }
+    };
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
+    B64Group ra, rb, rc;
+    if (work) {
+        stream64_issue<0>(ra, voff, f_addr());
+        f_next();
+    }
+    b64x4_build_tables<POLY>(lds);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    if (!work) return;
+    stream64_issue<0>(rb, voff, f_addr());
+    f_next();
+
+    Tile d;
+    d.T = T;
+    d.b = t0 / T;
+    d.k = t0 - d.b * T;
+    d.tbase = d.b * T;
+    d.vbase = 0;
+    d.pad = 0;
+    d.ngroups = G;
+    uint32_t g = 0;
+    uint64_t u = 0;
+    uint32_t q = 0;  // groups scanned
+    auto step = [&](B64Group &cur, B64Group &nxt) {
+        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0ull;
+        const uint64_t sn = f_addr();
+        f_next();
+        u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
+        ++q;
+        if (++g == G) {
+            g = 0;
+            stream64_finish(p, d, u, eng, lane);
+            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
+        }
+    };
+    for (;;) {
+        step(ra, rc);
+        if (q >= nq) break;
+        step(rb, ra);
+        if (q >= nq) break;
+        step(rc, rb);
+        if (q >= nq) break;
+    }
+}
+
+
 // ------------------------------------------------------------------------------------------
 // xxHash64 (aws_xxhash64_compute, XXHash.cpp:17).  The published algorithm is four serial chains
 // per buffer (nonlinear: add, rotate, multiply mod 2^64), so a buffer has at most four lanes of
@@ -2291,8 +2408,10 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (p->stream && !list)
+            if (p->stream && !list && (p->dbg & 1048576))  // diagnostics: 8-copy tables, one workgroup per CU
                 launch(crc64_stream_kernel<kPoly64Nvme>, nblocks, kBlock, s, p, ev);
+            else if (p->stream && !list)  // 4-copy tables, two workgroups per CU
+                launch(crc64_stream4_kernel<kPoly64Nvme>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);
             else

@@ -330,13 +330,15 @@ constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
-ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main) {
-    const uint64_t wpb = width_of(alg) == 32 ? 8 : (uint64_t)kWavesPerBlock;
+ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main, bool w64_half_blocks = false) {
+    // w64_half_blocks: crc64_stream4_kernel, 512-thread workgroups two per CU (66 KiB of LDS)
+    const uint64_t wpb = width_of(alg) == 32 || w64_half_blocks ? 8 : (uint64_t)kWavesPerBlock;
     static const int wpc = [] {  // diagnostics: AMDCRC_WG_PER_CU forces the W=32 workgroups per CU
         const char *e = std::getenv("AMDCRC_WG_PER_CU");
         return e ? std::atoi(e) : 0;
     }();
-    const uint64_t per_cu = width_of(alg) == 32 && wpc > 0 ? (uint64_t)wpc
+    const uint64_t per_cu = w64_half_blocks                       ? 2
+                            : width_of(alg) == 32 && wpc > 0         ? (uint64_t)wpc
                             : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
     uint64_t cap = (uint64_t)d->cus * per_cu;
     static const double frac = [] {  // diagnostics: AMDCRC_GRID_FRAC caps the grid at a share of the slots
@@ -407,7 +409,8 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_cnt1 = w->cnt1;
         p.d_claim = w->claim;
     }
-    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main).blocks;
+    const bool w64_half = width_of(alg) == 64 && p.stream && !(p.dbg & 1048576);  // crc64_stream4_kernel
+    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half).blocks;
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;

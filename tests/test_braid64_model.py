@@ -179,6 +179,48 @@ def test_lds_schedule_is_conflict_free_and_complete(br):
         assert br.step_lds(a, rnd.randrange(64)) == br.step(a)
 
 
+def test_four_copy_layout(br):
+    """crc64_stream4_kernel's 64 KiB layout (Braid64<POLY, 4>, b64x4_build_tables): row e = the low
+    dword's tables in bytes [0, 128), the high dword's in [128, 256), quarter q = 4 copies x 8 B.
+    The table build (thread i: table t = i >> 6, entries (i & 63) + 64 n, both 16-byte halves)
+    fills every address the lookups form with the right entry, the lookups reproduce the slice-by-8
+    step, and a ds_read_b64 half-wave meets each bank pair at most twice (2-way conflicts)."""
+    lds = {}
+    for i in range(512):
+        t = i >> 6
+        reg, q = (0, 7 - t) if t >= 4 else (1, 3 - t)
+        for n in range(4):
+            e = (i & 63) + 64 * n
+            row = (e << 8) + (reg << 7) + (q << 5)
+            for half in range(2):
+                for c in range(2):
+                    lds[row + (half << 4) + 8 * c] = br.Tp[t][e]
+    assert len(lds) == 256 * 2 * 4 * 4  # 64 KiB of 8-byte entries, all distinct addresses
+
+    def step_lds4(a, lane):
+        j, cp = (lane >> 3) & 3, lane & 3
+        v = 0
+        for k in range(4):
+            q = (k + j) & 3
+            cst = (q << 5) | (cp << 3)
+            v ^= lds[cst | (((a >> (8 * q)) & 255) << 8)]               # low dword: region 0
+            v ^= lds[(cst | 0x80) | (((a >> (32 + 8 * q)) & 255) << 8)]  # high dword: +128
+        return v
+
+    rnd = random.Random(5)
+    for _ in range(200):
+        a = rnd.getrandbits(64)
+        assert step_lds4(a, rnd.randrange(64)) == br.step(a)
+    for k in range(4):
+        for hi in (0, 1):
+            use = {}
+            for lane in range(32):
+                j, cp = (lane >> 3) & 3, lane & 3
+                addr = ((((k + j) & 3) << 5) | (cp << 3) | (hi << 7)) + (rnd.randrange(256) << 8)
+                use[(addr >> 3) & 31] = use.get((addr >> 3) & 31, 0) + 1
+            assert max(use.values()) <= 2
+
+
 def test_step_is_multiply_by_x4096(br):
     rnd = random.Random(4)
     for _ in range(20):
