@@ -1450,414 +1450,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
 }
 
 // ------------------------------------------------------------------------------------------
-// Compact-table variant of crc32_stream_kernel (AMDCRC_DEBUG bit 21).  The same four T' tables in 8
-// quarter-rotated copies, but each entry's row is 128 bytes instead of 256: the v_perm address
-// (entry byte at bit 8, quarter and copy in the low byte, pre-scaled by 2) is shifted right once per
-// lookup.  Banks stay those of Braid32 (the entry's low bit only adds 32 to every lane's bank), so
-// the lookups remain conflict-free; the tables take 32 KiB, the workgroup 46 KiB, and three
-// workgroups -- three queued launches -- fit a CU when the kernel stays within 80 VGPRs.
-constexpr uint32_t kTabC = 32768;
-constexpr uint32_t kStreamLdsC = kTabC + (kStreamLds - kBKOff);
-
-template <uint32_t POLY>
-struct Braid32c {
-    using T = uint32_t;
-    static constexpr int W = 32;
-    const char *L;  // tables
-    const char *C;  // constants region: K image, P columns, byte table, flags, local slots
-    uint32_t cst[4], sel[4];
-
-    __device__ void init(const char *lds, int lane) {
-        L = lds;
-        C = lds + kTabC;
-        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t q = (k + j) & 3u;
-            cst[k] = (q << 6) | (cp << 3);
-            sel[k] = 0x0c0c0004u | (q << 8);
-        }
-    }
-    __device__ __forceinline__ uint32_t look(uint32_t a, int k) const {
-        return lds32(L, __builtin_amdgcn_perm(cst[k], a, sel[k]) >> 1);
-    }
-    __device__ __forceinline__ uint32_t step(uint32_t a) const { return look(a, 0) ^ look(a, 1) ^ look(a, 2) ^ look(a, 3); }
-    __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
-        const uint32_t l0 = look(a, 0), l1 = look(a, 1), l2 = look(a, 2), l3 = look(a, 3);
-        return xor3(xor3(l0, l1, wn), l2, l3);
-    }
-    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-        return (s >> 8) ^ lds32(C, (kT0Off - kBKOff) + 4 * ((s ^ b) & 0xffu));
-    }
-    __device__ __forceinline__ const char *cbase() const { return C; }
-    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint4 c = *(const uint4 *)(C + (g * 64 + lane) * 16);
-            acc = xor_and(acc, c.x, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 0), 1));
-            acc = xor_and(acc, c.y, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 1), 1));
-            acc = xor_and(acc, c.z, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 2), 1));
-            acc = xor_and(acc, c.w, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 3), 1));
-        }
-        return acc;
-    }
-};
-
-template <uint32_t POLY>
-__global__ __launch_bounds__(kBraidBlock) __attribute__((amdgpu_waves_per_eu(6))) void crc32_streamc_kernel(const ScanParams p) {
-    using B = Braid32c<POLY>;
-    constexpr int DIAG = 0;
-    __shared__ __attribute__((aligned(16))) char lds[kStreamLdsC];
-    char *const cb = lds + kTabC;  // constants region
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
-    const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
-    const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
-    const bool stamps = p.d_timeline != nullptr;
-    auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
-    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
-    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = 4u * (uint32_t)lane;
-    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
-    const uint32_t gsh = __builtin_ctz(G);
-    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
-    const bool work = t0 < t1;
-    // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
-    uint32_t fq = 0;  // groups issued
-    uint64_t fb = t0 / T, fk = t0 - fb * T;
-    uint32_t fg = 0;
-    auto f_addr = [&]() -> uint64_t {
-        uint64_t a = fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
-        if (!AMDCRC_GUARD_OK(fq >= nq || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
-                                                                 p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
-                             1, a))
-            a = dummy;
-        return rfl64(a);
-    };
-    auto f_next = [&]() {
-        ++fq;
-        if (++fg == G) {
-            fg = 0;
-            if (++fk == T) fk = 0, ++fb;
-        }
-    };
-    // K-image word and P columns of this thread (published to LDS after the first scan step), then the
-    // first group: both asm loads, complete once the first row wait of the first step has passed
-    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    v4u kq;
-    uint32_t pce0, pce1;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
-    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
-    LocalBufs lb{0, 0};
-    if (T > 1 && T <= 32) {
-        const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
-        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
-    }
-    BGroup ra, rb, rc;
-    if (work) {
-        stream_issue<0>(ra, voff, f_addr());
-        f_next();
-    }
-    if (!(DIAG & 1)) {
-        const uint32_t i = threadIdx.x;
-        const uint32_t q = (i >> 1) & 3u, h = i & 1u;
-        uint32_t bq[8];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) bq[b] = basis_bit<POLY>(3 - q, b);
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint32_t e = (i >> 3) + 64u * pass;
-            uint32_t te = 0;
-#pragma unroll
-            for (int b = 0; b < 8; ++b) te ^= ((e >> b) & 1u) ? bq[b] : 0u;
-            *(uint4 *)(lds + (e << 7) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
-        }
-        if (i < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * i) = basis_entry<POLY, 4>(i);
-    }
-    if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
-    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(cb + (kLocalOff - kBKOff)))[threadIdx.x] = 0ull;
-    stamp(4);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    B eng;
-    eng.init(lds, lane);
-    if (work) {
-        stream_issue<0>(rb, voff, f_addr());
-        f_next();
-    }
-    stamp(1);
-    bool consts_ready = false, published = false;
-    auto publish_consts = [&]() {
-        if (published) return;
-        published = true;
-        *(v4u *)(cb + 16 * threadIdx.x) = kq;
-        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * threadIdx.x) = pce0;
-        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * (threadIdx.x + kBraidBlock)) = pce1;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(cb + (kConstFlagOff - kBKOff)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto await_consts = [&]() {
-        if (consts_ready) return;
-        while (__hip_atomic_load((uint32_t *)(cb + (kConstFlagOff - kBKOff)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)kBraidWaves)
-            __builtin_amdgcn_s_sleep(1);
-        consts_ready = true;
-    };
-    if (!work) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(kq), "+v"(pce0), "+v"(pce1)::"memory");
-        publish_consts();
-        return;
-    }
-
-    // scan cursor: tile d (buffer, index in buffer), group g, global group q
-    Tile d;
-    d.T = T;
-    d.b = t0 / T;
-    d.k = t0 - d.b * T;
-    d.tbase = d.b * T;
-    d.vbase = 0;
-    d.pad = 0;
-    d.ngroups = G;
-    uint32_t g = 0, u = 0;
-    uint32_t q = 0;  // groups scanned
-    BGroupAcc acc{};
-    acc.slot = ~0ull;
-    auto step = [&](BGroup &cur, BGroup &nxt) {
-        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
-        const uint64_t sn = f_addr();
-        f_next();
-        u = stream_rows<0, B, (DIAG & 4) != 0>(u, cur, nxt, voff, sn, eng);
-        if (!published) {
-            asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
-            publish_consts();
-        }
-        ++q;
-        if (++g == G) {
-            g = 0;
-            await_consts();
-            if (DIAG & 2) {
-                if (u == 0x9e3779b9u) p.d_timeline[lane] = u;  // keep the scan live
-            } else {
-                stream_finish(p, d, u, eng, lane, acc, lb);
-            }
-            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
-        }
-    };
-    for (;;) {
-        step(ra, rc);
-        if (q >= nq) break;
-        step(rb, ra);
-        if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
-    }
-    ring_drain(ra, rb, rc);  // the trailing placeholder rows
-    stamp(2);
-    stream_publish(p, acc, eng, lane);
-    stamp(3);
-}
-
-
-// Workgroup-pool variant of crc32_stream_kernel (AMDCRC_DEBUG bit 19): one static tile per wave,
-// the rest of the workgroup's share claimed as waves run dry, so a wave the memory system serves
-// late scans less (diagnostics: measured against the static split).
-template <uint32_t POLY>
-__global__ __launch_bounds__(kBraidBlock, 4) void crc32_pool_kernel(const ScanParams p) {
-    using B = Braid32<POLY, true>;
-    constexpr int DIAG = 0;
-    __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
-    const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
-    const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
-    const bool stamps = p.d_timeline != nullptr;
-    auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
-    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
-    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = 4u * (uint32_t)lane;
-    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    // tile source: one static tile per wave (wt0 + wave), then claims from the workgroup's pool
-    // [wt0 + waves, wt1) through an LDS counter (lgkmcnt: never in the payload's vmcnt stream)
-    uint64_t s0 = rfl64(wt0 + wv), s1 = s0 < wt1 ? s0 + 1 : s0;  // (a workgroup with < 8 tiles: no pool)
-    const uint64_t pbase = wt0 + kBraidWaves, psize = wt1 > pbase ? wt1 - pbase : 0;
-    auto next_tile = [&](uint64_t &t) -> bool {
-        if (s0 < s1) {
-            t = s0++;
-            return true;
-        }
-        uint32_t v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add((uint32_t *)(lds + kPoolOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        v = __builtin_amdgcn_readfirstlane(v);
-        if (v < psize) {
-            t = pbase + v;
-            return true;
-        }
-        return false;
-    };
-    auto tile_addr = [&](uint64_t t) -> uint64_t {
-        const uint64_t bb = t / T;
-        return p.base + bb * p.stride + hoff + (t - bb * T) * tile_bytes;
-    };
-    // prefetch cursor: tile ftile, group fg (fg == G: enter the next tile at the next issue).  The scan
-    // cursor is exactly two issues behind: it reads its (tile, group) from a two-deep issue record
-    constexpr uint64_t kNone = ~0ull;
-    uint64_t ftile = 0, fbase = dummy, h0t = kNone, h1t = kNone;
-    uint32_t fg = 0, h0g = 0, h1g = 0;
-    bool fvalid = next_tile(ftile);
-    if (fvalid) fbase = tile_addr(ftile);
-    const bool work = fvalid;
-    auto f_addr = [&]() -> uint64_t {
-        if (fvalid && fg == G) {
-            fg = 0;
-            fvalid = next_tile(ftile);
-            if (fvalid) fbase = tile_addr(ftile);
-        }
-        h1t = h0t, h1g = h0g;
-        h0t = fvalid ? ftile : kNone, h0g = fg;
-        return rfl64(fvalid ? fbase + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy);
-    };
-    auto f_next = [&]() { ++fg; };
-    // K-image word and P columns of this thread (published to LDS after the first scan step), then the
-    // first group: both asm loads, complete once the first row wait of the first step has passed
-    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    v4u kq;
-    uint32_t pce0, pce1;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
-    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
-    LocalBufs lb{0, 0};
-    if (T > 1 && T <= 32) {
-        const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
-        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
-    }
-    BGroup ra, rb, rc;
-    if (work) {
-        stream_issue<0>(ra, voff, f_addr());
-        f_next();
-    }
-    if (!(DIAG & 1)) {
-        const uint32_t i = threadIdx.x;
-        const uint32_t q = (i >> 1) & 3u, h = i & 1u;
-        uint32_t bq[8];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) bq[b] = basis_bit<POLY>(3 - q, b);
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint32_t e = (i >> 3) + 64u * pass;
-            uint32_t te = 0;
-#pragma unroll
-            for (int b = 0; b < 8; ++b) te ^= ((e >> b) & 1u) ? bq[b] : 0u;
-            *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
-        }
-        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
-    }
-    if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
-    if (threadIdx.x == 0) *(uint32_t *)(lds + kPoolOff) = 0u;
-    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(lds + kLocalOff))[threadIdx.x] = 0ull;
-    stamp(4);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    B eng;
-    eng.init(lds, lane);
-    if (work) {
-        stream_issue<0>(rb, voff, f_addr());
-        f_next();
-    }
-    stamp(1);
-    bool consts_ready = false, published = false;
-    auto publish_consts = [&]() {
-        if (published) return;
-        published = true;
-        *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
-        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
-        *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto await_consts = [&]() {
-        if (consts_ready) return;
-        while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)kBraidWaves)
-            __builtin_amdgcn_s_sleep(1);
-        consts_ready = true;
-    };
-    if (!work) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(kq), "+v"(pce0), "+v"(pce1)::"memory");
-        publish_consts();
-        return;
-    }
-
-    // scan cursor: the (tile, group) issued two issues earlier
-    auto make = [&](uint64_t t) {
-        Tile dd;
-        dd.T = T;
-        dd.b = t / T;
-        dd.k = t - dd.b * T;
-        dd.tbase = dd.b * T;
-        dd.vbase = 0;
-        dd.pad = 0;
-        dd.ngroups = G;
-        return dd;
-    };
-    Tile d = make(0);
-    uint32_t u = 0;
-    bool done = false;
-    BGroupAcc acc{};
-    acc.slot = ~0ull;
-    auto step = [&](BGroup &cur, BGroup &nxt) {
-        const uint64_t ct = h1t;
-        const uint32_t cg = h1g;
-        if (cg == 0) {
-            d = make(ct);
-            u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
-        }
-        const uint64_t sn = f_addr();
-        f_next();
-        u = stream_rows<0, B, false>(u, cur, nxt, voff, sn, eng);
-        if (!published) {
-            asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
-            publish_consts();
-        }
-        if (cg + 1 == G) {
-            await_consts();
-            stream_finish(p, d, u, eng, lane, acc, lb);
-        }
-        done = h1t == kNone;
-    };
-    for (;;) {
-        step(ra, rc);
-        if (done) break;
-        step(rb, ra);
-        if (done) break;
-        step(rc, rb);
-        if (done) break;
-    }
-    ring_drain(ra, rb, rc);  // the trailing placeholder rows
-    stamp(2);
-    stream_publish(p, acc, eng, lane);
-    stamp(3);
-}
-
-
-// ------------------------------------------------------------------------------------------
 // W = 32 streaming scan on 512-byte rows (AMDCRC_DEBUG bit 15 selects it over the 256-byte rows).
 // Lane l owns the 8-byte word at 8l of every row (one global_load_dwordx2 per row: 512 contiguous
 // bytes per wave instruction), and one row step is a slice-by-8 step whose tables fold in the skip
@@ -2608,11 +2200,7 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
-            if (p->stream && !list && (p->dbg & 2097152))  // diagnostics: compact tables, 3 workgroups per CU
-                launch(crc32_streamc_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->stream && !list && (p->dbg & 524288))  // diagnostics: workgroup tile pool
-                launch(crc32_pool_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->stream && !list && (p->dbg & 32768))  // diagnostics: 512-byte rows
+            if (p->stream && !list && (p->dbg & 32768))  // diagnostics: 512-byte rows
                 launch(crc32_stream8_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             else if (p->stream && !list) {  // DIAG bits (diagnostics): AMDCRC_DEBUG bits 16-18
                 switch ((p->dbg >> 16) & 7) {
