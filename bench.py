@@ -23,6 +23,10 @@ End-to-end (PCIe-inclusive): the same batches start in pinned hos
 on a copy stream overlap the scans on a compute stream through a 3-slot device ring, results come
 back D2H.  Reported as `e2e_pinned` next to `value`, never as `value`.
 
+North-star shape (`target_shape`, rank 0 at N=1): BASELINE.json's target, CRC32C over batches of
+16 x 64 MiB device-resident buffers (>= 80 % of HBM peak), measured the same two ways; reported
+beside `value`, never as `value`.  The profiling passes run with --target-buffers 0.
+
 Prints one JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per launch (1 byte read per
 payload byte) / mean kernel duration from HIP events recorded on the launch stream.
 `roofline.read_ceiling` = the same two measurements for a read-only XOR-reduce kernel of the same
@@ -62,6 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-read-ceiling", action="store_true", help="skip the streaming-read ceiling kernel")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
+    ap.add_argument("--target-buffers", type=int, default=16,
+                    help="north-star shape leg: batches of this many 64 MiB buffers (0: skip)")
     return ap.parse_args()
 
 
@@ -141,6 +147,51 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     return {"value": round(iters * step / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(iters * step / el_h2d / 2**30, 2),
             "sample": f"{iters} batches of {count} x {L // 1024} KiB from {nb * step >> 20} MiB pinned host memory, "
                       f"H2D on a copy stream overlapped with the scans, results D2H"}
+
+
+def target_shape(eng, alg_id, dev, streams, nbuf, steps=20, nb=2, timing=6):
+    """BASELINE.json north_star target shape, reported beside `value` (never as `value`): CRC32C over
+    batches of `nbuf` device-resident 64 MiB buffers, pipelined over the same streams as the headline
+    leg, plus the dispatch-stamped duration of `timing` serialized launches."""
+    import torch
+
+    L = 64 << 20
+    step_bytes = nbuf * L
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x7A26)
+    data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
+    outs = [torch.empty(nbuf, dtype=torch.int32, device=dev) for _ in range(nb)]
+
+    def launch(i, st):
+        eng.checksum_strided(alg_id, data, L, L, nbuf, out=outs[i % nb], stream=st, base_offset=(i % nb) * step_bytes)
+
+    for i in range(max(nb * len(streams), 3)):
+        launch(i, streams[i % len(streams)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        launch(i, streams[i % len(streams)])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = streams[0]
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(timing)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(timing)]
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(int(40e6))
+    for i in range(timing):
+        starts[i].record(st)
+        ends[i].record(st)
+        eng.time_next_launch(starts[i], ends[i])
+        launch(i, st)
+    torch.cuda.synchronize()
+    kms = sum(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends)) / timing
+    gibs = steps * step_bytes / el / 2**30
+    del data
+    return {"workload": f"{nbuf} x 64 MiB buffers per step, CRC32C, device-resident, {nb} rotating batches",
+            "value": round(gibs, 2), "unit": "GiB/s", "steps": steps,
+            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
+            "kernel_ms": round(kms, 4), "roofline_frac": round(step_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "target_pct": 80.0}
 
 
 def main():
@@ -281,6 +332,10 @@ def main():
     if rank == 0 and world == 1 and args.e2e_batches > 0:
         e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
 
+    target = None
+    if rank == 0 and world == 1 and alg == "crc32c" and args.target_buffers > 0:
+        target = target_shape(eng, ALG[alg], dev, streams, args.target_buffers)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and alg in ("crc32", "crc32c", "crc64nvme", "xxh64"):
         host = data[:step_bytes].cpu().numpy()
@@ -317,6 +372,7 @@ def main():
                          "bytes_per_launch": step_bytes, "timing_launches": nt, "read_ceiling": ceiling},
             "cpu_baseline": cpu,
             "e2e_pinned": e2e,
+            "target_shape": target,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
