@@ -327,6 +327,7 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 // are long enough to amortise their own ramp and use both slots.  The W=64 scan runs one
 // 1024-thread workgroup per CU (130 KiB LDS).
 constexpr uint64_t kSmallBatchBytes = 256ull << 20;
+uint32_t debug_flags();
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
@@ -346,7 +347,10 @@ ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t t
         return e ? std::atof(e) : 1.0;
     }();
     if (frac > 0 && frac < 1) cap = std::max<uint64_t>(1, (uint64_t)(cap * frac));
-    const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, cap);
+    // diagnostics: AMDCRC_DEBUG bit 22 spreads a W=64 small batch's tiles over twice the workgroups
+    // (every other wave idle), so every CU holds tiles instead of half of them
+    const uint64_t tpb = w64_half_blocks && total_main < kSmallBatchBytes && (debug_flags() & 4194304) ? wpb / 2 : wpb;
+    const uint64_t blocks = std::min<uint64_t>((ntiles + tpb - 1) / tpb, cap);
     return {blocks, wpb};
 }
 
@@ -448,8 +452,13 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     // crc32_stream_kernel / crc64_stream_kernel; AMDCRC_DEBUG bit 14 disables them).  Their tiles are
     // sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C measured 5250-5315 GiB/s with
     // one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
+    // W=64 small batches: tiles for 4 waves per CU.  A tile that spans a whole buffer finishes without
+    // the cross-tile combine (global atomics with return, pcol loads), which costs a W=64 wave more
+    // than the idle slots do once other streams' launches fill them: 1024 x 64 KiB CRC64NVME measured
+    // 2774 GiB/s with 16 KiB tiles (4 per buffer), 3930 with 32 KiB, 4010 with 64 KiB.
     const bool w32 = width_of(alg) == 32;
-    const uint64_t wpc = w32 ? 8 * (ml * count >= kSmallBatchBytes ? 2 : 1) : (uint64_t)kWavesPerBlock;
+    const bool small = ml * count < kSmallBatchBytes;
+    const uint64_t wpc = w32 ? 8 * (small ? 1 : 2) : small ? 4 : (uint64_t)kWavesPerBlock;
     const uint32_t seg_stream = choose_seg(d, ml * count, ml, 1, wpc);
     const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0 && !(debug_flags() & 16384);
     if (stream) p.seg = seg_stream;
