@@ -2102,6 +2102,99 @@ __global__ __launch_bounds__(256) void combine_kernel(const CombineParams p) {
     ((T *)p.d_out)[i] = (T)(gf2_mulmod(a, m, POLY, W) ^ b);
 }
 
+// ------------------------------------------------------------------------------------------
+// Lane-per-buffer scan for lists of short buffers (event-stream framing CRCs: an 8-byte prelude and
+// a message body per message).  The wave-per-tile scans fold a short
+// buffer's unaligned head and tail with serial scalar loads and spend a tile pass on a few hundred
+// bytes; here each lane owns one buffer: bytes up to 8-byte alignment, then slice-by-8 steps
+// (eight independent table lookups per aligned 8-byte word, one dependent XOR chain per word),
+// then the tail bytes.  Tables: eight 256-entry tables in LDS (8 KiB for W=32, 16 KiB for W=64),
+// T_0 = the bytewise table, T_k[e] = T_(k-1)[e] advanced over one zero byte.  Lanes of a wave read
+// neighbouring buffers, so packed messages share cache lines across lanes.
+template <class T, T POLY>
+__device__ __forceinline__ void lane_tables(T (*tab)[256]) {
+    const uint32_t i = threadIdx.x;
+    T c = (T)i;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? POLY : (T)0);
+    tab[0][i] = c;
+    __syncthreads();
+#pragma unroll
+    for (int t = 1; t < 8; ++t) {
+        c = (c >> 8) ^ tab[0][c & 0xff];
+        tab[t][i] = c;
+    }
+    __syncthreads();
+}
+
+// register s advanced over [ptr, ptr + n): bytes to 8-byte alignment, slice-by-8 words, tail bytes
+template <class T>
+__device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, const T (*tab)[256]) {
+    while (n && ((uintptr_t)ptr & 7)) {
+        s = (s >> 8) ^ tab[0][(s ^ *ptr++) & 0xff];
+        --n;
+    }
+    const uint64_t *w = (const uint64_t *)ptr;
+    for (uint64_t k = n >> 3; k; --k) {
+        const uint64_t v = *w++;
+        if (sizeof(T) == 4) {
+            const uint32_t lo = (uint32_t)v ^ (uint32_t)s, hi = (uint32_t)(v >> 32);
+            s = tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
+                tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
+        } else {
+            const uint64_t x = v ^ (uint64_t)s;
+            s = tab[7][x & 0xff] ^ tab[6][(x >> 8) & 0xff] ^ tab[5][(x >> 16) & 0xff] ^ tab[4][(x >> 24) & 0xff] ^
+                tab[3][(x >> 32) & 0xff] ^ tab[2][(x >> 40) & 0xff] ^ tab[1][(x >> 48) & 0xff] ^ tab[0][x >> 56];
+        }
+    }
+    ptr = (const uint8_t *)w;
+    for (n &= 7; n; --n) s = (s >> 8) ^ tab[0][(s ^ *ptr++) & 0xff];
+    return s;
+}
+
+template <class T, T POLY>
+__global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
+    __shared__ T tab[8][256];
+    lane_tables<T, POLY>(tab);
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= p.nbuf) return;
+    uint64_t seed = p.seed_all;
+    if (p.d_seeds) seed = sizeof(T) == 4 ? (uint64_t)((const uint32_t *)p.d_seeds)[b] : ((const uint64_t *)p.d_seeds)[b];
+    const T s = lane_scan<T>((T)~seed, (const uint8_t *)p.d_ptrs[b], p.d_lens[b], tab);
+    ((T *)p.d_out)[b] = (T)~s;
+}
+
+// Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads
+// total_length from the message's prelude (big-endian), refuses lengths outside [16, limit - offset]
+// before touching the body, then folds the prelude (-> prelude CRC) and continues over the headers
+// and payload (-> message CRC, the running form of CRC32 over [0, total - 4)), and compares both
+// with the big-endian values stored at offset 8 and total - 4.
+__device__ __forceinline__ uint32_t be32(const uint8_t *q) {
+    return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+}
+__global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
+    __shared__ uint32_t tab[8][256];
+    lane_tables<uint32_t, kPoly32>(tab);
+    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= p.count) return;
+    const uint64_t off = p.d_offsets[m];
+    uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
+    if (off <= p.limit && p.limit - off >= 16) {
+        const uint8_t *q = p.base + off;
+        const uint64_t total = be32(q);
+        if (total >= 16 && total <= p.limit - off) {
+            uint32_t s = lane_scan<uint32_t>(~0u, q, 8, tab);
+            pre = ~s;
+            s = lane_scan<uint32_t>(s, q + 8, total - 12, tab);
+            msg = ~s;
+            st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
+        }
+    }
+    p.d_prelude_crc[m] = pre;
+    p.d_message_crc[m] = msg;
+    p.d_status[m] = st;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -2232,6 +2325,26 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             break;
         default: return -1;
     }
+    return (int)hipGetLastError();
+}
+
+extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, void *const *ev) {
+    const uint64_t blocks = (p->nbuf + 255) / 256;
+    if (blocks == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    switch (alg) {
+        case ALG_CRC32: launch(crc_lanes_kernel<uint32_t, kPoly32>, (int)blocks, 256, s, p, ev); break;
+        case ALG_CRC32C: launch(crc_lanes_kernel<uint32_t, kPoly32C>, (int)blocks, 256, s, p, ev); break;
+        case ALG_CRC64NVME: launch(crc_lanes_kernel<uint64_t, kPoly64Nvme>, (int)blocks, 256, s, p, ev); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
+extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
+    const uint64_t blocks = (p->count + 255) / 256;
+    if (blocks == 0) return 0;
+    launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
     return (int)hipGetLastError();
 }
 

@@ -327,6 +327,8 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 // are long enough to amortise their own ramp and use both slots.  The W=64 scan runs one
 // 1024-thread workgroup per CU (130 KiB LDS).
 constexpr uint64_t kSmallBatchBytes = 256ull << 20;
+// Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
+constexpr uint64_t kLaneMaxBytes = 4096;
 uint32_t debug_flags();
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
@@ -529,13 +531,31 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     std::lock_guard<std::mutex> g(d->mu);
     // plan: seg from the median main length, tiles per buffer, per-wave starting buffer
     std::vector<uint64_t> mains(count);
-    uint64_t total = 0;
+    uint64_t total = 0, maxlen = 0;
     for (size_t i = 0; i < count; ++i) {
         if (lens[i] && !ptrs[i]) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer with nonzero length");
         mains[i] = main_len((uint64_t)(uintptr_t)ptrs[i], lens[i]);
         total += mains[i];
+        maxlen = std::max<uint64_t>(maxlen, lens[i]);
     }
     const bool xxh = is_hash(alg);
+    // lists of short buffers only (event-stream framing): one lane per buffer (crc_lanes_kernel);
+    // AMDCRC_DEBUG bit 23 keeps them on the wave-per-tile scan
+    if (!xxh && maxlen <= kLaneMaxBytes && !(debug_flags() & 8388608)) {
+        uint64_t *h;
+        int rc1 = stage_begin(d, s, count * 16, (void **)&h);
+        if (rc1) return rc1;
+        for (size_t i = 0; i < count; ++i) {
+            h[i] = (uint64_t)(uintptr_t)ptrs[i];
+            h[count + i] = lens[i];
+        }
+        const uint64_t *dl;
+        if ((rc1 = stage_end(d, s, count * 16, (const void **)&dl))) return rc1;
+        LaneParams lp{dl, dl + count, count, d_seeds, 0, d_out};
+        int e = amdcrc_launch_lanes(alg, &lp, s, g_time_events);
+        g_time_events[0] = g_time_events[1] = nullptr;
+        return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+    }
     uint32_t seg = kGroupBytes;
     uint64_t tile = 0;
     if (!xxh) {
@@ -784,6 +804,21 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs
     int rc = get_device(&d);
     if (rc) return rc;
     return list_impl(d, alg, d_ptrs, lens, count, d_seeds, d_out, (hipStream_t)hip_stream);
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(const void *base, uint64_t limit, const uint64_t *d_offsets, size_t count,
+                                                 uint32_t *d_prelude_crc, uint32_t *d_message_crc, uint32_t *d_status,
+                                                 void *hip_stream) {
+    if (count == 0) return 0;
+    if (!base || !d_offsets || !d_prelude_crc || !d_message_crc || !d_status)
+        return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
+    Device *d;
+    int rc = get_device(&d);
+    if (rc) return rc;
+    EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status};
+    int e = amdcrc_launch_eventstream(&ep, hip_stream, g_time_events);
+    g_time_events[0] = g_time_events[1] = nullptr;
+    return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("event-stream kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_host(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,

@@ -86,9 +86,29 @@ struct CombineParams {
     const uint64_t *d_xpow2;  // x^(8 * 2^i) mod P, i < 64
 };
 
+// Lane-per-buffer scan of a ragged list of short buffers (crc_lanes_kernel)
+struct LaneParams {
+    const uint64_t *d_ptrs;  // device addresses
+    const uint64_t *d_lens;
+    uint64_t nbuf;
+    const void *d_seeds;  // u32/u64 per buffer, or null -> seed_all
+    uint64_t seed_all;
+    void *d_out;  // u32/u64 per buffer
+};
+
+// Event-stream framing check (eventstream_kernel)
+struct EventStreamParams {
+    const uint8_t *base;
+    const uint64_t *d_offsets;  // message starts, bytes from base
+    uint64_t count, limit;      // limit: bytes readable from base
+    uint32_t *d_prelude_crc, *d_message_crc, *d_status;
+};
+
 }  // namespace amdcrc
 
 extern "C" {
+int amdcrc_launch_eventstream(const amdcrc::EventStreamParams *p, void *stream, void *const *events);
+int amdcrc_launch_lanes(int alg, const amdcrc::LaneParams *p, void *stream, void *const *events);
 int amdcrc_launch_combine(int alg, const amdcrc::CombineParams *p, void *stream);
 int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *stream, void *const *events);
 int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream, void *const *events);

@@ -91,6 +91,27 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list(
     void *hip_stream);
 
 /*
+ * Event-stream framing check (aws-c-event-stream wire format; SURVEY.md 8(f) rank 4, initialised by
+ * the reference at source/Api.cpp:51).  Message i starts at base + d_offsets[i] (d_offsets, and the
+ * three outputs, are DEVICE arrays of count entries; base is device memory with `limit` readable
+ * bytes).  Its prelude is total_length (u32 BE) | headers_length (u32 BE) | prelude_crc (u32 BE), its
+ * last 4 bytes the message CRC (u32 BE) over bytes [0, total_length - 4).  Writes the computed
+ * prelude and message CRC32s and d_status[i]: bit 0 = stored prelude CRC matches, bit 1 = stored
+ * message CRC matches, bit 2 = malformed (total_length < 16 or past `limit`; nothing beyond the
+ * first 16 bytes is read then, and both CRCs are 0).  One lane per message: for many short
+ * messages; a message of megabytes is better checked with aws_crt_amd_checksum_strided.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(
+    const void *base,
+    uint64_t limit,
+    const uint64_t *d_offsets,
+    size_t count,
+    uint32_t *d_prelude_crc,
+    uint32_t *d_message_crc,
+    uint32_t *d_status,
+    void *hip_stream);
+
+/*
  * Device-side combine of running CRCs (CombineCRC32/32C/64NVME, CRC.h:41-51, over a batch):
  * d_out[i] = d_crc1[i] * x^(8*len2[i]) ^ d_crc2[i].  len2 is a HOST array.  For S3 multipart
  * composition of part CRCs into an object CRC.

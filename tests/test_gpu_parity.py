@@ -174,6 +174,32 @@ def test_fuzz_lengths_alignments_seeds(engine, alg):
 
 
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+def test_fuzz_short_lists_lane_path(engine, alg):
+    """Lists whose buffers are all <= 4096 bytes take the lane-per-buffer scan (crc_lanes_kernel):
+    3000 buffers of random length 0..4096 (plus 0..8 and exactly 4096) at every alignment mod 16,
+    with random seeds and with no seeds (seed 0)."""
+    import torch
+
+    rng = random.Random(0x1A4E + ALG[alg])
+    lens = [rng.randrange(0, 4097) for _ in range(2990)] + list(range(9)) + [4096]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for ln in lens:
+        pos = (pos + 15) // 16 * 16 + rng.randrange(16)
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 23 + ALG[alg])
+    ptrs = [d.data_ptr() + o for o in offs]
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], ptrs, lens, seeds=seeds_tensor(alg, seeds))
+    out0 = engine.checksum_list(ALG[alg], ptrs, lens)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    assert results(engine, alg, out) == [oracle.checksum(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out0) == [oracle.checksum(alg, h[o: o + ln]) for o, ln in zip(offs, lens)]
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
 def test_fuzz_strided_shapes(engine, alg):
     """Random uniform batches (count, length, base alignment, stride slack), half of them whole-tile
     shapes that take the streaming scans, with random seeds (fixed RNG seed)."""
