@@ -2127,28 +2127,48 @@ __device__ __forceinline__ void lane_tables(T (*tab)[256]) {
     __syncthreads();
 }
 
-// register s advanced over [ptr, ptr + n): bytes to 8-byte alignment, slice-by-8 words, tail bytes
+// register s advanced over [ptr, ptr + n).  All loads are aligned 8-byte words: the unaligned head
+// and the tail come from the aligned words that contain them (never past their page), so a short
+// buffer costs a few independent loads, not a serial chain of byte loads; whole words go four loads
+// at a time before their slice-by-8 steps.
+template <class T>
+__device__ __forceinline__ T lane_word(T s, uint64_t v, const T (*tab)[256]) {
+    if (sizeof(T) == 4) {
+        const uint32_t lo = (uint32_t)v ^ (uint32_t)s, hi = (uint32_t)(v >> 32);
+        return tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
+               tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
+    } else {
+        const uint64_t x = v ^ (uint64_t)s;
+        return tab[7][x & 0xff] ^ tab[6][(x >> 8) & 0xff] ^ tab[5][(x >> 16) & 0xff] ^ tab[4][(x >> 24) & 0xff] ^
+               tab[3][(x >> 32) & 0xff] ^ tab[2][(x >> 40) & 0xff] ^ tab[1][(x >> 48) & 0xff] ^ tab[0][x >> 56];
+    }
+}
+template <class T>
+__device__ __forceinline__ T lane_bytes(T s, uint64_t v, uint32_t nb, const T (*tab)[256]) {
+    for (uint32_t j = 0; j < nb; ++j, v >>= 8) s = (s >> 8) ^ tab[0][(s ^ (T)v) & 0xff];
+    return s;
+}
 template <class T>
 __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, const T (*tab)[256]) {
-    while (n && ((uintptr_t)ptr & 7)) {
-        s = (s >> 8) ^ tab[0][(s ^ *ptr++) & 0xff];
-        --n;
+    if (n == 0) return s;
+    const uintptr_t a = (uintptr_t)ptr;
+    const uint64_t *w = (const uint64_t *)(a & ~(uintptr_t)7);
+    const uint32_t o = (uint32_t)(a & 7);
+    if (o) {
+        const uint32_t hb = n < 8 - o ? (uint32_t)n : 8 - o;
+        s = lane_bytes<T>(s, *w++ >> (8 * o), hb, tab);
+        n -= hb;
     }
-    const uint64_t *w = (const uint64_t *)ptr;
-    for (uint64_t k = n >> 3; k; --k) {
-        const uint64_t v = *w++;
-        if (sizeof(T) == 4) {
-            const uint32_t lo = (uint32_t)v ^ (uint32_t)s, hi = (uint32_t)(v >> 32);
-            s = tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
-                tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
-        } else {
-            const uint64_t x = v ^ (uint64_t)s;
-            s = tab[7][x & 0xff] ^ tab[6][(x >> 8) & 0xff] ^ tab[5][(x >> 16) & 0xff] ^ tab[4][(x >> 24) & 0xff] ^
-                tab[3][(x >> 32) & 0xff] ^ tab[2][(x >> 40) & 0xff] ^ tab[1][(x >> 48) & 0xff] ^ tab[0][x >> 56];
-        }
+    uint64_t k = n >> 3;
+    for (; k >= 4; k -= 4, w += 4) {
+        const uint64_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
+        s = lane_word<T>(s, v0, tab);
+        s = lane_word<T>(s, v1, tab);
+        s = lane_word<T>(s, v2, tab);
+        s = lane_word<T>(s, v3, tab);
     }
-    ptr = (const uint8_t *)w;
-    for (n &= 7; n; --n) s = (s >> 8) ^ tab[0][(s ^ *ptr++) & 0xff];
+    for (; k; --k) s = lane_word<T>(s, *w++, tab);
+    if (n & 7) s = lane_bytes<T>(s, *w, (uint32_t)(n & 7), tab);
     return s;
 }
 
