@@ -308,19 +308,31 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     uint64_t acc0 = init[2 * wp], acc1 = init[2 * wp + 1];
     const uint64_t nb = (n - 1) / 1024;
     const uint8_t *q = ptr + 16 * lane;
-    constexpr int D = 4;  // blocks in flight
+    // D blocks per round: their lane contributions and class sums are independent of the
+    // accumulators, so all D reductions issue together and only the scrambles stay serial
+    constexpr int D = 8;  // blocks in flight
     uint64_t w0[D], w1[D];
 #pragma unroll
     for (int d = 0; d < D; ++d)
         if ((uint64_t)d < nb) ld16<ALIGNED>(q + 1024 * d, w0[d], w1[d]);
     uint64_t blk = 0;
     for (; blk + D <= nb; blk += D) {
+        uint64_t c0[D], c1[D];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const uint64_t c0 = mul32x32(w0[d] ^ ks0) + w1[d], c1 = mul32x32(w1[d] ^ ks1) + w0[d];
+            c0[d] = mul32x32(w0[d] ^ ks0) + w1[d];
+            c1[d] = mul32x32(w1[d] ^ ks1) + w0[d];
             if (blk + D + d < nb) ld16<ALIGNED>(q + 1024 * (blk + D + d), w0[d], w1[d]);
-            acc0 = scramble1(acc0 + class_sum(c0), st0);
-            acc1 = scramble1(acc1 + class_sum(c1), st1);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            c0[d] = class_sum(c0[d]);
+            c1[d] = class_sum(c1[d]);
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            acc0 = scramble1(acc0 + c0[d], st0);
+            acc1 = scramble1(acc1 + c1[d], st1);
         }
     }
 #pragma unroll
