@@ -2129,7 +2129,7 @@ __device__ __forceinline__ void lane_tables(T (*tab)[256]) {
 
 // register s advanced over [ptr, ptr + n).  All loads are aligned 8-byte words: the unaligned head
 // and the tail come from the aligned words that contain them (never past their page), so a short
-// buffer costs a few independent loads, not a serial chain of byte loads; whole words go four loads
+// buffer costs a few independent loads, not a serial chain of byte loads; whole words go eight loads
 // at a time before their slice-by-8 steps.
 template <class T>
 __device__ __forceinline__ T lane_word(T s, uint64_t v, const T (*tab)[256]) {
@@ -2160,12 +2160,21 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
         n -= hb;
     }
     uint64_t k = n >> 3;
-    for (; k >= 4; k -= 4, w += 4) {
+    for (; k >= 8; k -= 8, w += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = w[j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
+    }
+    if (k >= 4) {
         const uint64_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
         s = lane_word<T>(s, v0, tab);
         s = lane_word<T>(s, v1, tab);
         s = lane_word<T>(s, v2, tab);
         s = lane_word<T>(s, v3, tab);
+        k -= 4;
+        w += 4;
     }
     for (; k; --k) s = lane_word<T>(s, *w++, tab);
     if (n & 7) s = lane_bytes<T>(s, *w, (uint32_t)(n & 7), tab);
