@@ -84,3 +84,19 @@ def test_no_device_fails_loudly():
     rc = L.aws_crt_amd_checksum_strided(1, ctypes.c_void_p(0x1000), 16, 16, 1, None, ctypes.c_void_p(0x2000), None)
     assert rc == -1
     assert b"no HIP device" in L.aws_crt_amd_last_error()
+
+
+def test_eventstream_abi_argument_checks():
+    """aws_crt_amd_eventstream_crcs: count 0 is a no-op, null arrays are refused before any device
+    work, and without a device a real call fails loudly."""
+    L = ctypes.CDLL(LIB)
+    vp = ctypes.c_void_p
+    f = L.aws_crt_amd_eventstream_crcs
+    f.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_size_t, vp, vp, vp, vp]
+    L.aws_crt_amd_last_error.restype = ctypes.c_char_p
+    assert f(None, 0, None, 0, None, None, None, None) == 0
+    rc = f(vp(0x1000), 64, None, 4, vp(0x2000), vp(0x3000), vp(0x4000), None)
+    assert rc != 0 and b"null argument" in L.aws_crt_amd_last_error()
+    if L.aws_crt_amd_device_count() == 0:
+        rc = f(vp(0x1000), 64, vp(0x1800), 4, vp(0x2000), vp(0x3000), vp(0x4000), None)
+        assert rc == -1 and b"no HIP device" in L.aws_crt_amd_last_error()
