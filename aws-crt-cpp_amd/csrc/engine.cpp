@@ -71,6 +71,7 @@ struct Device {
     std::map<std::pair<int, uint64_t>, DevBuf> pcols;           // (alg, tile) -> tmax x W x u64
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
     std::map<hipStream_t, Workspace> ws;
+    std::map<hipStream_t, DevBuf> xsums;  // split XXH3 long path: per-block accumulator sums
     DevBuf xpow2;                                               // per alg: 64 x x^(8*2^i)
     // list-mode descriptor staging
     std::map<hipStream_t, std::pair<DevBuf, DevBuf>> desc;      // (device, pinned host)
@@ -329,6 +330,8 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 constexpr uint64_t kLaneMaxBytes = 4096;
+// Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
+constexpr uint64_t kXxh3SplitBlocks = 4096;
 uint32_t debug_flags();
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
@@ -437,6 +440,28 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         xp.d_seeds = (const uint64_t *)d_seeds;
         xp.seed_all = seed_all;
         xp.d_out = (uint64_t *)d_out;
+        // XXH3 over long uniform buffers: a block-sum pass over all CUs, then one wave per buffer
+        // scrambles the 64-byte sums (xxh3_kernels.hip; AMDCRC_DEBUG bit 24 keeps one pass)
+        const uint64_t nb = len > 240 ? (len - 1) / 1024 : 0;
+        if (alg != AWS_CRT_AMD_XXH64 && nb >= kXxh3SplitBlocks && !(debug_flags() & 16777216)) {
+            std::lock_guard<std::mutex> g(d->mu);
+            DevBuf &xs = d->xsums[s];
+            const size_t need = count * nb * 64;
+            if (xs.bytes < need) {
+                if (xs.p) {
+                    HIP_TRY(hipStreamSynchronize(s));  // queued launches may still read the old sums
+                    (void)hipFree(xs.p);
+                    xs.p = nullptr;
+                    xs.bytes = 0;
+                }
+                HIP_TRY(hipMalloc(&xs.p, need));
+                xs.bytes = need;
+            }
+            xp.d_sums = (uint64_t *)xs.p;
+            int e = amdcrc_launch_xxh3_blocksum(&xp, s, g_time_events[0]);
+            g_time_events[0] = nullptr;
+            if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh3 block-sum launch: ") + hipGetErrorString((hipError_t)e));
+        }
         return launch_hash(alg, xp, s);
     }
     if (count > 1 && (stride % 16) != 0)

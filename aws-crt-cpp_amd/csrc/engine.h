@@ -75,6 +75,7 @@ struct XxhParams {
     const uint64_t *d_seeds;
     uint64_t seed_all;
     uint64_t *d_out;
+    uint64_t *d_sums;  // split XXH3 long path: 8 accumulator sums per full 1 KiB block, or null
 };
 
 struct CombineParams {
@@ -112,6 +113,7 @@ int amdcrc_launch_lanes(int alg, const amdcrc::LaneParams *p, void *stream, void
 int amdcrc_launch_combine(int alg, const amdcrc::CombineParams *p, void *stream);
 int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *stream, void *const *events);
 int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream, void *const *events);
+int amdcrc_launch_xxh3_blocksum(const amdcrc::XxhParams *p, void *stream, void *start_event);
 int amdcrc_launch_xxh3(int bits, const amdcrc::XxhParams *p, void *stream, void *const *events);
 int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint32_t *sink, int nblocks, void *stream, void *const *events);
 }

@@ -299,7 +299,16 @@ __device__ __forceinline__ void ld16(const uint8_t *q, uint64_t &a, uint64_t &b)
     }
 }
 
-template <int BITS, bool ALIGNED>
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// SPLIT: the full blocks' class sums were written by xxh3_blocksum_kernel (64 B per block at
+// p.d_sums + 8 (i nb + blk)); this wave only scrambles.  Lane l loads the two sums of class l & 3
+// for block g + (l >> 2): one coalesced 1 KiB load per 16 blocks, four loads in flight, and the
+// per-block values reach their class lanes by shuffles that do not depend on the accumulators.
+template <int BITS, bool ALIGNED, bool SPLIT = false>
 __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *ptr, uint64_t n, uint64_t seed, int lane) {
     const int s = lane >> 2, wp = lane & 3;
     const uint64_t ks0 = sec64(8 * s + 16 * wp, seed), ks1 = sec64(8 * s + 16 * wp + 8, seed);
@@ -308,39 +317,81 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     uint64_t acc0 = init[2 * wp], acc1 = init[2 * wp + 1];
     const uint64_t nb = (n - 1) / 1024;
     const uint8_t *q = ptr + 16 * lane;
-    // D blocks per round: their lane contributions and class sums are independent of the
-    // accumulators, so all D reductions issue together and only the scrambles stay serial
-    constexpr int D = 8;  // blocks in flight
-    uint64_t w0[D], w1[D];
+    if (SPLIT) {
+        const uint64_t *S = p.d_sums + i * nb * 8;
+        constexpr int G = 16, DS = 4;
+        const uint64_t ng = (nb + G - 1) / G;
+        uint64_t x0[DS], x1[DS];
+        auto ldg = [&](uint64_t g, uint64_t &a, uint64_t &b) {
+            const uint64_t blk = g * G + (uint64_t)s;
+            if (blk < nb) {
+                const v2u64 v = *(const __attribute__((address_space(1))) v2u64 *)(S + blk * 8 + 2 * wp);
+                a = v.x;
+                b = v.y;
+            } else {
+                a = b = 0;
+            }
+        };
 #pragma unroll
-    for (int d = 0; d < D; ++d)
-        if ((uint64_t)d < nb) ld16<ALIGNED>(q + 1024 * d, w0[d], w1[d]);
-    uint64_t blk = 0;
-    for (; blk + D <= nb; blk += D) {
-        uint64_t c0[D], c1[D];
+        for (int d = 0; d < DS; ++d) ldg(d, x0[d], x1[d]);
+        for (uint64_t g = 0; g < ng; g += DS) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            c0[d] = mul32x32(w0[d] ^ ks0) + w1[d];
-            c1[d] = mul32x32(w1[d] ^ ks1) + w0[d];
-            if (blk + D + d < nb) ld16<ALIGNED>(q + 1024 * (blk + D + d), w0[d], w1[d]);
+            for (int d = 0; d < DS; ++d) {
+                if (g + d < ng) {
+                    const uint64_t base = (g + d) * G;
+                    const uint64_t cnt = nb - base < (uint64_t)G ? nb - base : (uint64_t)G;
+                    uint64_t v0[G], v1[G];
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        v0[j] = shfl64(x0[d], 4 * j + wp);
+                        v1[j] = shfl64(x1[d], 4 * j + wp);
+                    }
+                    ldg(g + d + DS, x0[d], x1[d]);
+#pragma unroll
+                    for (int j = 0; j < G; ++j) {
+                        if ((uint64_t)j < cnt) {
+                            acc0 = scramble1(acc0 + v0[j], st0);
+                            acc1 = scramble1(acc1 + v1[j], st1);
+                        }
+                    }
+                }
+            }
         }
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            c0[d] = class_sum(c0[d]);
-            c1[d] = class_sum(c1[d]);
+    } else {
+        // D blocks per round: their lane contributions and class sums are independent of the
+        // accumulators, so all D reductions issue together and only the scrambles stay serial
+        constexpr int D = 8;  // blocks in flight
+        uint64_t w0[D], w1[D];
+    #pragma unroll
+        for (int d = 0; d < D; ++d)
+            if ((uint64_t)d < nb) ld16<ALIGNED>(q + 1024 * d, w0[d], w1[d]);
+        uint64_t blk = 0;
+        for (; blk + D <= nb; blk += D) {
+            uint64_t c0[D], c1[D];
+    #pragma unroll
+            for (int d = 0; d < D; ++d) {
+                c0[d] = mul32x32(w0[d] ^ ks0) + w1[d];
+                c1[d] = mul32x32(w1[d] ^ ks1) + w0[d];
+                if (blk + D + d < nb) ld16<ALIGNED>(q + 1024 * (blk + D + d), w0[d], w1[d]);
+            }
+    #pragma unroll
+            for (int d = 0; d < D; ++d) {
+                c0[d] = class_sum(c0[d]);
+                c1[d] = class_sum(c1[d]);
+            }
+    #pragma unroll
+            for (int d = 0; d < D; ++d) {
+                acc0 = scramble1(acc0 + c0[d], st0);
+                acc1 = scramble1(acc1 + c1[d], st1);
+            }
         }
-#pragma unroll
+    #pragma unroll
         for (int d = 0; d < D; ++d) {
-            acc0 = scramble1(acc0 + c0[d], st0);
-            acc1 = scramble1(acc1 + c1[d], st1);
-        }
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (blk + d < nb) {
-            const uint64_t c0 = mul32x32(w0[d] ^ ks0) + w1[d], c1 = mul32x32(w1[d] ^ ks1) + w0[d];
-            acc0 = scramble1(acc0 + class_sum(c0), st0);
-            acc1 = scramble1(acc1 + class_sum(c1), st1);
+            if (blk + d < nb) {
+                const uint64_t c0 = mul32x32(w0[d] ^ ks0) + w1[d], c1 = mul32x32(w1[d] ^ ks1) + w0[d];
+                acc0 = scramble1(acc0 + class_sum(c0), st0);
+                acc1 = scramble1(acc1 + class_sum(c1), st1);
+            }
         }
     }
     // the partial last block (no scramble) and the last stripe, read at n - 64 (lanes 0..3)
@@ -384,6 +435,52 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     }
 }
 
+// Phase 1 of the split long path (strided batches of long buffers): wave w sums the lane
+// contributions of kSumBlocks consecutive full blocks of one buffer (the accumulate step is a pure
+// addition within a block) and writes each block's eight accumulator sums (64 B) for the scramble
+// pass; all CUs stream the payload instead of one wave per buffer.
+constexpr uint64_t kSumBlocks = 64;
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const XxhParams p) {
+    const uint64_t nb = (p.len - 1) / 1024;
+    const uint64_t wpb = (nb + kSumBlocks - 1) / kSumBlocks;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= p.nbuf * wpb) return;
+    const uint64_t i = w / wpb, b0 = (w - i * wpb) * kSumBlocks;
+    const uint64_t b1 = b0 + kSumBlocks < nb ? b0 + kSumBlocks : nb;
+    const int lane = threadIdx.x & 63, s = lane >> 2, wp = lane & 3;
+    const uint64_t seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
+    const uint64_t ks0 = sec64(8 * s + 16 * wp, seed), ks1 = sec64(8 * s + 16 * wp + 8, seed);
+    const uint8_t *q = (const uint8_t *)(p.base + i * p.stride) + 16 * lane;
+    uint64_t *S = p.d_sums + i * nb * 8 + 2 * wp;
+    constexpr int D = 8;
+    for (uint64_t blk = b0; blk < b1; blk += D) {
+        uint64_t c0[D], c1[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            uint64_t a = 0, b = 0;
+            if (blk + d < b1) ld16<ALIGNED>(q + 1024 * (blk + d), a, b);
+            c0[d] = mul32x32(a ^ ks0) + b;
+            c1[d] = mul32x32(b ^ ks1) + a;
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            c0[d] = class_sum(c0[d]);
+            c1[d] = class_sum(c1[d]);
+        }
+        if (s == 0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                if (blk + d < b1) {
+                    v2u64 v;
+                    v.x = c0[d];
+                    v.y = c1[d];
+                    *(__attribute__((address_space(1))) v2u64 *)(S + (blk + d) * 8) = v;
+                }
+        }
+    }
+}
+
 template <int BITS>
 __global__ __launch_bounds__(256) void xxh3_wave_kernel(const XxhParams p) {
     const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -404,13 +501,30 @@ __global__ __launch_bounds__(256) void xxh3_wave_kernel(const XxhParams p) {
         }
         return;
     }
-    if (((uintptr_t)ptr & 15) == 0)
+    if (p.d_sums)  // phase 2 of the split long path (strided batches only)
+        xxh3_long_wave<BITS, false, true>(p, i, ptr, n, seed, lane);
+    else if (((uintptr_t)ptr & 15) == 0)
         xxh3_long_wave<BITS, true>(p, i, ptr, n, seed, lane);
     else
         xxh3_long_wave<BITS, false>(p, i, ptr, n, seed, lane);
 }
 
 }  // namespace
+
+// Phase 1 of the split path: one wave per kSumBlocks blocks of every buffer (p->d_sums set, p->len > 240)
+extern "C" int amdcrc_launch_xxh3_blocksum(const XxhParams *p, void *stream, void *start_event) {
+    const uint64_t nb = (p->len - 1) / 1024;
+    const uint64_t waves = p->nbuf * ((nb + kSumBlocks - 1) / kSumBlocks);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const bool aligned = ((p->base | p->stride) & 15) == 0;
+    if (aligned)
+        hipExtLaunchKernelGGL(xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, (hipEvent_t)start_event, nullptr, 0, *p);
+    else
+        hipExtLaunchKernelGGL(xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, (hipEvent_t)start_event, nullptr, 0, *p);
+    return (int)hipGetLastError();
+}
 
 // One wavefront per buffer (4 per 256-thread block): long buffers use all 64 lanes, short ones lane 0.
 extern "C" int amdcrc_launch_xxh3(int bits, const XxhParams *p, void *stream, void *const *ev) {

@@ -173,6 +173,28 @@ def test_fuzz_lengths_alignments_seeds(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("alg", ["xxh3_64", "xxh3_128"])
+def test_xxh3_split_long_strided(engine, alg):
+    """Strided XXH3 over buffers of >= 4096 full blocks takes the split path (block-sum pass, then
+    the scramble pass over the sums): lengths at, around and past the threshold and not a multiple
+    of the block, aligned and unaligned bases, per-buffer seeds and seed 0."""
+    import torch
+
+    rng = random.Random(0x5A1 + ALG[alg])
+    for L, count, off in [(4096 * 1024 + 1, 3, 0), (4097 * 1024 + 777, 2, 5), (8 << 20, 2, 16),
+                          (3 * (1 << 20) + 100, 2, 3), (9 * (1 << 20) + 63, 1, 1)]:
+        stride = L + 16
+        d = dev_random(off + stride * count + 64, 31 + L % 97)
+        seeds = [rng.getrandbits(64) for _ in range(count)]
+        out = engine.checksum_strided(ALG[alg], d, stride, L, count, seeds=seeds_tensor(alg, seeds), base_offset=off)
+        out0 = engine.checksum_strided(ALG[alg], d, stride, L, count, base_offset=off)
+        torch.cuda.synchronize()
+        h = host_bytes(d)
+        bufs = [h[off + k * stride: off + k * stride + L] for k in range(count)]
+        assert results(engine, alg, out) == [oracle.checksum(alg, b, sd) for b, sd in zip(bufs, seeds)], (L, off)
+        assert results(engine, alg, out0) == [oracle.checksum(alg, b) for b in bufs], (L, off)
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
 def test_fuzz_short_lists_lane_path(engine, alg):
     """Lists whose buffers are all <= 4096 bytes take the lane-per-buffer scan (crc_lanes_kernel):
