@@ -1,7 +1,8 @@
 """ctypes binding of the MI355X checksum engine's C ABI (include/aws_crt_amd/checksums_batch.h,
 include/aws/checksums/crc.h).  Used by tests/ and bench.py; torch supplies device memory and
 streams only.  Every compute call goes through lib/libaws-crt-cpp-amd.so -- there is no Python
-or CPU fallback: if the library or a gfx950 device is missing, calls raise.
+checksum code: if the library is missing, calls raise; device-batch calls raise without a gfx950
+device.  The library's own host path (csrc/cpu/) serves host memory per its dispatch mode.
 
 Reference API being mirrored: Aws::Crt::Checksum (include/aws/crt/checksum/CRC.h:20-51,
 XXHash.h:21-37) -> aws-checksums (source/checksum/CRC.cpp:17-42, XXHash.cpp:17-65).
@@ -16,6 +17,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-crt-cpp-amd.so")
 
 CRC32, CRC32C, CRC64NVME, XXH64, XXH3_64, XXH3_128 = 0, 1, 2, 3, 4, 5
+DISPATCH_AUTO, DISPATCH_CPU, DISPATCH_GPU = 0, 1, 2
 ALGORITHMS = {"crc32": CRC32, "crc32c": CRC32C, "crc64nvme": CRC64NVME, "xxh64": XXH64, "xxh3_64": XXH3_64,
               "xxh3_128": XXH3_128}
 WIDE = {CRC64NVME, XXH64, XXH3_64, XXH3_128}  # 64-bit result words (XXH3_128: two per buffer)
@@ -42,6 +44,10 @@ def lib() -> ctypes.CDLL:
         L.aws_crt_amd_init.restype = ctypes.c_int
         L.aws_crt_amd_device_count.restype = ctypes.c_int
         L.aws_crt_amd_last_error.restype = ctypes.c_char_p
+        L.aws_crt_amd_fallback_count.restype = ctypes.c_ulonglong
+        L.aws_crt_amd_cpu_tier.restype = ctypes.c_char_p
+        L.aws_crt_amd_cpu_batch.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz,
+                                            ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.c_int]
         L.aws_crt_amd_checksum_strided.argtypes = [ctypes.c_int, vp, sz, sz, sz, vp, vp, vp]
         L.aws_crt_amd_checksum_list.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp, vp]
         L.aws_crt_amd_checksum_host.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp]
@@ -60,6 +66,35 @@ def lib() -> ctypes.CDLL:
 def _check(rc: int) -> None:
     if rc != 0:
         raise EngineError(f"aws_crt_amd error {rc}: {lib().aws_crt_amd_last_error().decode()}")
+
+
+def set_dispatch(mode: int) -> None:
+    """Where the single-buffer ABI runs host-memory input (DISPATCH_AUTO / _CPU / _GPU)."""
+    _check(lib().aws_crt_amd_set_dispatch(mode))
+
+
+def fallback_count() -> int:
+    """GPU calls that failed and were served by the host path instead (process-wide)."""
+    return int(lib().aws_crt_amd_fallback_count())
+
+
+def cpu_tier() -> str:
+    return lib().aws_crt_amd_cpu_tier().decode()
+
+
+def cpu_batch(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, threads: int = 1) -> list:
+    """The library's host path over host buffers (raw addresses), `threads` std::threads; one value
+    per buffer (XXH3_128: 128-bit ints)."""
+    n = len(ptrs)
+    P = (ctypes.c_void_p * max(n, 1))(*ptrs)
+    S = (ctypes.c_size_t * max(n, 1))(*lens)
+    sd = (ctypes.c_uint64 * max(n, 1))(*seeds) if seeds is not None else None
+    per = 2 if alg == XXH3_128 else 1
+    out = (ctypes.c_uint64 * max(n * per, 1))()
+    _check(lib().aws_crt_amd_cpu_batch(alg, P, S, n, sd, out, threads))
+    if per == 2:
+        return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
+    return [int(out[i]) for i in range(n)]
 
 
 def device_count() -> int:
@@ -181,7 +216,8 @@ def multipart_crc(alg: int, parts, stream=None):
 
 
 def checksum_host(alg: int, buffers: Sequence[bytes], seeds: Optional[Sequence[int]] = None):
-    """Host buffers -> host results, through pinned staging and the GPU (synchronous)."""
+    """Host buffers -> host results (synchronous): the host path, or pinned staging and the GPU when
+    the dispatch mode is DISPATCH_GPU."""
     n = len(buffers)
     keep = [ctypes.create_string_buffer(bytes(b), len(b)) for b in buffers]
     P = (ctypes.c_void_p * n)(*[ctypes.addressof(k) for k in keep])

@@ -1,0 +1,75 @@
+// Host (x86-64) checksum path of the engine: the part of aws-checksums' job that stays on the CPU.
+//
+// The reference computes every checksum on the calling thread with a CPU implementation chosen
+// by hardware capability at aws_checksums_library_init (include/aws/crt/checksum/CRC.h:17-19,
+// source/Api.cpp:53).  This engine keeps the same contract: small host buffers, few-buffer xxHash
+// and every call on a machine without a usable gfx950 device run here; device-resident data and
+// large batches go to the GPU (engine.cpp dispatch).  Product code: nothing here comes from or
+// links oracle/ (the test-only restatement).
+//
+// Tiers, picked once from CPUID:
+//   CRC32 / CRC32C / CRC64NVME   AVX-512 VPCLMULQDQ folding (4 x 512-bit accumulators, 256 B per
+//                                iteration) > PCLMULQDQ folding (4 x 128-bit) > slice-by-8 tables;
+//                                CRC32C short inputs use the SSE4.2 crc32 instruction.
+//   XXH64                        scalar (four serial chains: nothing to vectorise)
+//   XXH3-64 / XXH3-128           AVX-512 > AVX2 > scalar stripe accumulation
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace amdcrc {
+namespace cpu {
+
+struct Features {
+    bool sse42, pclmul, avx2, avx512, vpclmul;
+};
+const Features &features();
+
+enum Tier { TIER_TABLE = 0, TIER_PCLMUL = 1, TIER_VPCLMUL = 2 };
+// Highest CRC tier this host supports (the one the API uses), and a way to force a lower one
+// (tests and the CPU baseline compare tiers; the arithmetic is identical).
+Tier best_tier();
+
+// CRC_ex semantics (CRC.h:20-36): previous = finalised CRC of the preceding bytes.
+uint32_t crc32(const uint8_t *p, size_t n, uint32_t previous);
+uint32_t crc32c(const uint8_t *p, size_t n, uint32_t previous);
+uint64_t crc64nvme(const uint8_t *p, size_t n, uint64_t previous);
+// alg 0/1/2 as engine.h; tier <= best_tier()
+uint64_t crc_tier(int alg, const uint8_t *p, size_t n, uint64_t previous, Tier tier);
+
+// xxHash (published algorithms; XXHash.h:21-37)
+uint64_t xxh64(const uint8_t *p, size_t n, uint64_t seed);
+uint64_t xxh3_64(const uint8_t *p, size_t n, uint64_t seed);
+void xxh3_128(const uint8_t *p, size_t n, uint64_t seed, uint64_t out_hi_lo[2]);
+
+// Streaming states: O(1) memory whatever the stream length (XXHash.h:40-91).
+struct Xxh64State {
+    uint64_t v[4];
+    uint64_t seed, total;
+    uint8_t mem[32];
+    uint32_t memn;
+};
+void xxh64_reset(Xxh64State *s, uint64_t seed);
+void xxh64_update(Xxh64State *s, const uint8_t *p, size_t n);
+uint64_t xxh64_digest(const Xxh64State *s);
+
+struct Xxh3State {
+    uint64_t acc[8];
+    uint64_t seed, total;
+    uint8_t secret[192];  // kSecret, or the seed-derived secret
+    uint8_t buf[256];     // unconsumed input (all of it while total <= 240)
+    uint8_t last[64];     // the 64 bytes consumed just before buf (for the final overlapping stripe)
+    uint32_t bufn, stripes;  // bytes in buf; stripes consumed in the current 1 KiB block
+};
+void xxh3_reset(Xxh3State *s, uint64_t seed);
+void xxh3_update(Xxh3State *s, const uint8_t *p, size_t n);
+uint64_t xxh3_64_digest(const Xxh3State *s);
+void xxh3_128_digest(const Xxh3State *s, uint64_t out_hi_lo[2]);
+
+// Batch of host buffers over `threads` std::threads (buffers round-robin), results as uint64_t per
+// buffer (XXH3-128: two words, high then low).  alg as aws_crt_amd_algorithm.  seeds may be null.
+void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64_t *seeds, uint64_t *out, size_t count,
+           int threads);
+
+}  // namespace cpu
+}  // namespace amdcrc

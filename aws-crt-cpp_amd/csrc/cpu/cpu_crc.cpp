@@ -1,0 +1,280 @@
+// Host CRC32 / CRC32C / CRC64NVME (see cpu_checksums.h for where this sits in the engine).
+//
+// Folding (PCLMULQDQ / VPCLMULQDQ), the technique aws-checksums dispatches to on x86-64
+// ("Where time goes today"), derived here for any reflected CRC of width 32 or 64:
+//
+//   A 16-byte block loaded little-endian into a 128-bit X holds the message polynomial relative to
+//   the block's end with bit p <-> x^(127-p).  Its low qword H and high qword L are 64-bit reflected
+//   values (bit b <-> x^(63-b)) with X = H x^64 + L.  Moving X forward by D bytes,
+//       X x^(8D) = H x^(64+8D) + L x^(8D)   (mod P),
+//   is two carry-less products.  clmul of two 64-bit reflected values yields bit k <-> x^(126-k), one
+//   short of the 128-bit convention, so the constants carry one power of x less:
+//       K_D = { x^(64+8D-1) mod P , x^(8D-1) mod P }  (64-bit reflected; W=32 values shifted up 32).
+//   Products stay below degree 128, so the folded X is congruent (mod P) to everything it absorbed.
+//   The register is XORed into the first W bits of the first block (a reflected CRC's register lines
+//   up with the next bytes), and at the end the register equals the CRC register of X's 16 bytes
+//   taken from state 0 -- a table (or crc32 instruction) pass over 16 bytes.
+//
+// Accumulators: AVX-512 four zmm (256 B per iteration, D = 256), reduced with D = 192/128/64 and the
+// four 128-bit lanes with D = 48/32/16; SSE four xmm (64 B per iteration).  Tails and short inputs:
+// slice-by-8 tables, or the SSE4.2 crc32 instruction for CRC32C.
+#include <immintrin.h>
+#include <cpuid.h>
+#include <string.h>
+
+#include <thread>
+#include <vector>
+
+#include "../gf2.h"
+#include "cpu_checksums.h"
+
+namespace amdcrc {
+namespace cpu {
+
+namespace {
+
+uint64_t xgetbv0() {
+    uint32_t lo, hi;
+    __asm__ volatile("xgetbv" : "=a"(lo), "=d"(hi) : "c"(0));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+Features detect() {
+    Features f{};
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return f;
+    f.sse42 = (c & bit_SSE4_2) != 0;
+    f.pclmul = (c & bit_PCLMUL) != 0 && f.sse42;
+    const bool osxsave = (c & bit_OSXSAVE) != 0;
+    const uint64_t xcr0 = osxsave ? xgetbv0() : 0;
+    const bool ymm_os = (xcr0 & 0x6) == 0x6, zmm_os = (xcr0 & 0xE6) == 0xE6;
+    if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) {
+        f.avx2 = ymm_os && (b & bit_AVX2) != 0;
+        f.avx512 = zmm_os && (b & bit_AVX512F) != 0 && (b & bit_AVX512BW) != 0 && (b & bit_AVX512VL) != 0;
+        f.vpclmul = f.avx512 && f.pclmul && (c & bit_VPCLMULQDQ) != 0;
+    }
+    return f;
+}
+
+// x^n mod P for any bit exponent n, W-bit reflected register form
+uint64_t xpow_bits(uint64_t n, uint64_t poly, int w) {
+    uint64_t result = 1ull << (w - 1), base = result >> 1;  // x^0, x^1
+    while (n) {
+        if (n & 1) result = gf2_mulmod(result, base, poly, w);
+        base = gf2_mulmod(base, base, poly, w);
+        n >>= 1;
+    }
+    return result;
+}
+
+struct PolyTables {
+    int alg, w;
+    uint64_t poly;
+    uint64_t t[8][256];  // t[k][e] = e * x^(8(k+1)): byte e followed by k zero bytes
+    // fold constants {high-qword multiplier, low-qword multiplier} for D bytes
+    alignas(16) uint64_t k16[2], k32[2], k48[2], k64[2], k128[2], k192[2], k256[2];
+
+    explicit PolyTables(int a) : alg(a), w(alg_width(a)), poly(alg_poly(a)) {
+        for (int e = 0; e < 256; ++e) {
+            uint64_t c = (uint64_t)e;
+            for (int k = 0; k < 8; ++k) {
+                for (int i = 0; i < 8; ++i) c = gf2_mulx(c, poly);
+                t[k][e] = c;
+            }
+        }
+        set(k16, 16), set(k32, 32), set(k48, 48), set(k64, 64), set(k128, 128), set(k192, 192), set(k256, 256);
+    }
+    void set(uint64_t *k, uint64_t d) {
+        const int sh = 64 - w;
+        k[0] = xpow_bits(64 + 8 * d - 1, poly, w) << sh;
+        k[1] = xpow_bits(8 * d - 1, poly, w) << sh;
+    }
+};
+
+const PolyTables &tables(int alg) {
+    static const PolyTables t32(ALG_CRC32), t32c(ALG_CRC32C), t64(ALG_CRC64NVME);
+    return alg == ALG_CRC32 ? t32 : alg == ALG_CRC32C ? t32c : t64;
+}
+
+inline uint64_t rd64(const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+
+// register r advanced over n bytes with the slice-by-8 tables
+uint64_t tab_update(const PolyTables &T, uint64_t r, const uint8_t *p, size_t n) {
+    for (; n >= 8; n -= 8, p += 8) {
+        const uint64_t x = rd64(p) ^ r;
+        r = T.t[7][x & 0xff] ^ T.t[6][(x >> 8) & 0xff] ^ T.t[5][(x >> 16) & 0xff] ^ T.t[4][(x >> 24) & 0xff] ^
+            T.t[3][(x >> 32) & 0xff] ^ T.t[2][(x >> 40) & 0xff] ^ T.t[1][(x >> 48) & 0xff] ^ T.t[0][x >> 56];
+    }
+    for (; n; --n, ++p) r = (r >> 8) ^ T.t[0][(r ^ *p) & 0xff];
+    return r;
+}
+
+// CRC32C register over n bytes with the SSE4.2 crc32 instruction
+__attribute__((target("sse4.2"))) uint64_t crc32c_hw(uint64_t r, const uint8_t *p, size_t n) {
+    uint64_t c = (uint32_t)r;
+    for (; n >= 8; n -= 8, p += 8) c = _mm_crc32_u64(c, rd64(p));
+    uint32_t c32 = (uint32_t)c;
+    for (; n; --n, ++p) c32 = _mm_crc32_u8(c32, *p);
+    return c32;
+}
+
+// register of X's 16 bytes from state 0
+uint64_t finish16(const PolyTables &T, const uint8_t *x16) {
+    if (T.alg == ALG_CRC32C && features().sse42) return crc32c_hw(0, x16, 16);
+    return tab_update(T, 0, x16, 16);
+}
+
+__attribute__((target("sse4.2,pclmul"))) inline __m128i fold128(__m128i x, __m128i k) {
+    return _mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11));
+}
+
+// register after the first (n & ~15) bytes; n >= 32
+__attribute__((target("sse4.2,pclmul"))) uint64_t fold_sse(const PolyTables &T, uint64_t r, const uint8_t *p, size_t n) {
+    const __m128i rv = _mm_set_epi64x(0, (long long)r);
+    const __m128i K16 = _mm_load_si128((const __m128i *)T.k16);
+    __m128i x;
+    if (n >= 128) {
+        const __m128i K64 = _mm_load_si128((const __m128i *)T.k64);
+        __m128i a0 = _mm_xor_si128(_mm_loadu_si128((const __m128i *)p), rv);
+        __m128i a1 = _mm_loadu_si128((const __m128i *)(p + 16));
+        __m128i a2 = _mm_loadu_si128((const __m128i *)(p + 32));
+        __m128i a3 = _mm_loadu_si128((const __m128i *)(p + 48));
+        p += 64, n -= 64;
+        for (; n >= 64; n -= 64, p += 64) {
+            a0 = _mm_xor_si128(fold128(a0, K64), _mm_loadu_si128((const __m128i *)p));
+            a1 = _mm_xor_si128(fold128(a1, K64), _mm_loadu_si128((const __m128i *)(p + 16)));
+            a2 = _mm_xor_si128(fold128(a2, K64), _mm_loadu_si128((const __m128i *)(p + 32)));
+            a3 = _mm_xor_si128(fold128(a3, K64), _mm_loadu_si128((const __m128i *)(p + 48)));
+        }
+        x = _mm_xor_si128(_mm_xor_si128(fold128(a0, _mm_load_si128((const __m128i *)T.k48)),
+                                        fold128(a1, _mm_load_si128((const __m128i *)T.k32))),
+                          _mm_xor_si128(fold128(a2, K16), a3));
+    } else {
+        x = _mm_xor_si128(_mm_loadu_si128((const __m128i *)p), rv);
+        p += 16, n -= 16;
+    }
+    for (; n >= 16; n -= 16, p += 16) x = _mm_xor_si128(fold128(x, K16), _mm_loadu_si128((const __m128i *)p));
+    alignas(16) uint8_t b[16];
+    _mm_store_si128((__m128i *)b, x);
+    return finish16(T, b);
+}
+
+#define CPU_AVX512_TARGET "avx512f,avx512bw,avx512vl,vpclmulqdq,pclmul,sse4.2"
+
+__attribute__((target(CPU_AVX512_TARGET))) inline __m512i fold512(__m512i x, __m512i k) {
+    return _mm512_xor_si512(_mm512_clmulepi64_epi128(x, k, 0x00), _mm512_clmulepi64_epi128(x, k, 0x11));
+}
+__attribute__((target(CPU_AVX512_TARGET))) inline __m512i bcast(const uint64_t *k) {
+    return _mm512_broadcast_i32x4(_mm_load_si128((const __m128i *)k));
+}
+// a ^ fold(x, k): one ternary-logic XOR of the two products and a
+__attribute__((target(CPU_AVX512_TARGET))) inline __m512i fold512_x(__m512i x, __m512i k, __m512i a) {
+    return _mm512_ternarylogic_epi64(_mm512_clmulepi64_epi128(x, k, 0x00), _mm512_clmulepi64_epi128(x, k, 0x11), a, 0x96);
+}
+
+// register after the first (n & ~15) bytes; n >= 256
+__attribute__((target(CPU_AVX512_TARGET))) uint64_t fold_avx512(const PolyTables &T, uint64_t r, const uint8_t *p, size_t n) {
+    const __m512i K256 = bcast(T.k256), K64 = bcast(T.k64);
+    __m512i z0 = _mm512_xor_si512(_mm512_loadu_si512(p), _mm512_set_epi64(0, 0, 0, 0, 0, 0, 0, (long long)r));
+    __m512i z1 = _mm512_loadu_si512(p + 64), z2 = _mm512_loadu_si512(p + 128), z3 = _mm512_loadu_si512(p + 192);
+    p += 256, n -= 256;
+    for (; n >= 256; n -= 256, p += 256) {
+        z0 = fold512_x(z0, K256, _mm512_loadu_si512(p));
+        z1 = fold512_x(z1, K256, _mm512_loadu_si512(p + 64));
+        z2 = fold512_x(z2, K256, _mm512_loadu_si512(p + 128));
+        z3 = fold512_x(z3, K256, _mm512_loadu_si512(p + 192));
+    }
+    __m512i z = _mm512_ternarylogic_epi64(fold512(z0, bcast(T.k192)), fold512(z1, bcast(T.k128)), fold512_x(z2, K64, z3), 0x96);
+    for (; n >= 64; n -= 64, p += 64) z = fold512_x(z, K64, _mm512_loadu_si512(p));
+    // lanes l0 (oldest) .. l3: l0 x^(8*48) + l1 x^(8*32) + l2 x^(8*16) + l3
+    const __m128i l0 = _mm512_extracti32x4_epi32(z, 0), l1 = _mm512_extracti32x4_epi32(z, 1);
+    const __m128i l2 = _mm512_extracti32x4_epi32(z, 2), l3 = _mm512_extracti32x4_epi32(z, 3);
+    const __m128i K16 = _mm_load_si128((const __m128i *)T.k16);
+    __m128i x = _mm_xor_si128(_mm_xor_si128(fold128(l0, _mm_load_si128((const __m128i *)T.k48)),
+                                            fold128(l1, _mm_load_si128((const __m128i *)T.k32))),
+                              _mm_xor_si128(fold128(l2, K16), l3));
+    for (; n >= 16; n -= 16, p += 16) x = _mm_xor_si128(fold128(x, K16), _mm_loadu_si128((const __m128i *)p));
+    alignas(16) uint8_t b[16];
+    _mm_store_si128((__m128i *)b, x);
+    return finish16(T, b);
+}
+
+uint64_t update(int alg, uint64_t r, const uint8_t *p, size_t n, Tier tier) {
+    const PolyTables &T = tables(alg);
+    if (tier == TIER_VPCLMUL && n >= 256) {
+        const size_t m = n & ~(size_t)15;
+        r = fold_avx512(T, r, p, m);
+        p += m, n -= m;
+    } else if (tier >= TIER_PCLMUL && n >= (alg == ALG_CRC32C ? 256 : 32)) {
+        const size_t m = n & ~(size_t)15;
+        r = fold_sse(T, r, p, m);
+        p += m, n -= m;
+    }
+    if (!n) return r;
+    if (alg == ALG_CRC32C && tier != TIER_TABLE && features().sse42) return crc32c_hw(r, p, n);
+    return tab_update(T, r, p, n);
+}
+
+}  // namespace
+
+const Features &features() {
+    static const Features f = detect();
+    return f;
+}
+
+Tier best_tier() {
+    static const Tier t = [] {
+        const Features &f = features();
+        return f.vpclmul ? TIER_VPCLMUL : f.pclmul ? TIER_PCLMUL : TIER_TABLE;
+    }();
+    return t;
+}
+
+uint64_t crc_tier(int alg, const uint8_t *p, size_t n, uint64_t previous, Tier tier) {
+    if (tier > best_tier()) tier = best_tier();
+    const uint64_t mask = alg_mask(alg);
+    if (!n) return previous & mask;
+    return ~update(alg, ~previous & mask, p, n, tier) & mask;
+}
+
+uint32_t crc32(const uint8_t *p, size_t n, uint32_t previous) { return (uint32_t)crc_tier(ALG_CRC32, p, n, previous, best_tier()); }
+uint32_t crc32c(const uint8_t *p, size_t n, uint32_t previous) {
+    return (uint32_t)crc_tier(ALG_CRC32C, p, n, previous, best_tier());
+}
+uint64_t crc64nvme(const uint8_t *p, size_t n, uint64_t previous) {
+    return crc_tier(ALG_CRC64NVME, p, n, previous, best_tier());
+}
+
+void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64_t *seeds, uint64_t *out, size_t count,
+           int threads) {
+    auto one = [&](size_t i) {
+        const uint64_t s = seeds ? seeds[i] : 0;
+        switch (alg) {
+            case 0: out[i] = crc32(ptrs[i], lens[i], (uint32_t)s); break;
+            case 1: out[i] = crc32c(ptrs[i], lens[i], (uint32_t)s); break;
+            case 2: out[i] = crc64nvme(ptrs[i], lens[i], s); break;
+            case 3: out[i] = xxh64(ptrs[i], lens[i], s); break;
+            case 4: out[i] = xxh3_64(ptrs[i], lens[i], s); break;
+            default: xxh3_128(ptrs[i], lens[i], s, out + 2 * i); break;
+        }
+    };
+    if (threads <= 1 || count <= 1) {
+        for (size_t i = 0; i < count; ++i) one(i);
+        return;
+    }
+    const size_t nt = std::min<size_t>((size_t)threads, count);
+    std::vector<std::thread> pool;
+    pool.reserve(nt);
+    for (size_t t = 0; t < nt; ++t)
+        pool.emplace_back([&, t] {
+            for (size_t i = t; i < count; i += nt) one(i);
+        });
+    for (auto &th : pool) th.join();
+}
+
+}  // namespace cpu
+}  // namespace amdcrc

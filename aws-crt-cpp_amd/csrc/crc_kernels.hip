@@ -288,7 +288,7 @@ __device__ __forceinline__ uint32_t basis_entry(uint32_t e) {
     return v;
 }
 
-template <uint32_t POLY, bool BITOP3 = true>
+template <uint32_t POLY>
 struct Braid32 {
     using T = uint32_t;
     static constexpr int W = 32;
@@ -322,7 +322,6 @@ struct Braid32 {
     __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
         uint32_t l3, l2, l1, l0;
         look(a, l3, l2, l1, l0);
-        if (!BITOP3) return l3 ^ l2 ^ l1 ^ l0 ^ wn;
         return xor3(xor3(l3, l2, wn), l1, l0);
     }
     // plain byte step for head / tail bytes (s is wave-uniform: broadcast reads)
@@ -502,9 +501,9 @@ __device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d,
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY, bool LIST, bool BITOP3 = true, bool NT = true>
+template <uint32_t POLY, bool LIST, bool NT = true>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanParams p) {
-    using B = Braid32<POLY, BITOP3>;
+    using B = Braid32<POLY>;
     __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
 
     const int lane = threadIdx.x & 63;
@@ -531,12 +530,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // tiles entered by the prefetch cursor from the pool, in order, for the scan cursor
     uint64_t fifo0 = 0, fifo1 = 0;
     uint32_t fifo_n = 0;
-    // diagnostics: per-wave timeline (start, tables built, scan done, exit) on the 100 MHz clock
-    const bool stamps = p.d_timeline != nullptr;
-    auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
 
     Walker w0{0, 0, 0};
     if (LIST && t0 < t1) {
@@ -628,7 +621,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
         if (i == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
         if (i == 0) *(uint32_t *)(lds + kPoolOff) = 0u;
     }
-    stamp(4);  // LDS stores issued
     // LDS-only barrier: __syncthreads()'s fence would also wait vmcnt(0) for the prefetched group
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
@@ -636,7 +628,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // pool mode: the prefetch cursor may reach the pool only now (the host gives every wave of a
     // pooled launch a static tile with payload, so a wave's pool tiles always follow it)
     if (dyn && any) pf_advance();
-    stamp(1);
     // Every wave publishes its 1/8 of the K image and P columns once its constants have arrived
     // (after its first group, by which time they have: loads retire in order) and counts itself in
     // LDS; a wave spins on the count only before its first tile finish.  A wave without work
@@ -738,10 +729,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
         settle();
     }
     publish_consts();
-    stamp(2);
     braid_publish<LIST>(p, acc, pd, eng, lane);
     braid_resolve<LIST>(p, pd, eng, lane);
-    stamp(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -766,18 +755,15 @@ __device__ __forceinline__ uint32_t gld_row(uint32_t voff, uint64_t sbase) {
     return __builtin_nontemporal_load((gu32 *)(sbase + voff + R * kBraidRow));
 }
 
-template <int R, class B, bool NOLOOK = false>
+template <int R, class B>
 __device__ __forceinline__ uint32_t stream_rows(uint32_t x, BGroup &cur, BGroup &nxt, uint32_t voff, uint64_t snext, const B &eng) {
     if constexpr (R < kBraidRowsPerGroup) {
         nxt.w[R] = gld_row<R>(voff, snext);
-        if (NOLOOK)
-            x = (x * 3u) ^ cur.w[R];
-        else
-            x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
         __builtin_amdgcn_sched_barrier(0);
-        return stream_rows<R + 1, B, NOLOOK>(x, cur, nxt, voff, snext, eng);
+        return stream_rows<R + 1, B>(x, cur, nxt, voff, snext, eng);
     } else {
-        return NOLOOK ? x : eng.step(x);
+        return eng.step(x);
     }
 }
 
@@ -915,12 +901,9 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
 }
 
 // Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
-//
-// DIAG (diagnostics only, wrong results): bit 0 skips the table build, bit 1 the tile finishes,
-// bit 2 replaces the table steps by a plain XOR (the ring and waits unchanged)
-template <uint32_t POLY, int DIAG = 0>
+template <uint32_t POLY>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const ScanParams p) {
-    using B = Braid32<POLY, true>;
+    using B = Braid32<POLY>;
     __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
 
     const int lane = threadIdx.x & 63;
@@ -929,11 +912,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
     const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
     const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
-    const bool stamps = p.d_timeline != nullptr;
-    auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
     // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
     const uint32_t G = p.seg / kGroupBytes;
     const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
@@ -963,14 +941,12 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
             if (++fk == T) fk = 0, ++fb;
         }
     };
-    // K-image word and P columns of this thread (published to LDS after the first scan step), then the
-    // first group: both asm loads, complete once the first row wait of the first step has passed
+    // K-image word and P columns of this thread, published to LDS after the first scan step (ordinary
+    // loads: issued before the first group, so the compiler's wait for them in the peeled first step
+    // is the exact count of the row loads issued after them)
     const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    v4u kq;
-    uint32_t pce0, pce1;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + 4 * threadIdx.x);
+    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
     // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
     LocalBufs lb{0, 0};
     if (T > 1 && T <= 32) {
@@ -982,7 +958,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         stream_issue<0>(ra, voff, f_addr());
         f_next();
     }
-    if (!(DIAG & 1)) {
+    {
         const uint32_t i = threadIdx.x;
         const uint32_t q = (i >> 1) & 3u, h = i & 1u;
         uint32_t bq[8];
@@ -1000,7 +976,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     }
     if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
     if (threadIdx.x < kLocalSlots) ((unsigned long long *)(lds + kLocalOff))[threadIdx.x] = 0ull;
-    stamp(4);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
@@ -1008,11 +983,10 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         stream_issue<0>(rb, voff, f_addr());
         f_next();
     }
-    stamp(1);
-    bool consts_ready = false, published = false;
+    bool consts_ready = false;
+    // every wave publishes its share of the K image and P columns once and counts itself in LDS; a
+    // wave spins on the count only before its first tile finish
     auto publish_consts = [&]() {
-        if (published) return;
-        published = true;
         *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
         *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
         *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
@@ -1027,7 +1001,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         consts_ready = true;
     };
     if (!work) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(kq), "+v"(pce0), "+v"(pce1)::"memory");
         publish_consts();
         return;
     }
@@ -1045,39 +1018,32 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     uint32_t q = 0;  // groups scanned
     BGroupAcc acc{};
     acc.slot = ~0ull;
-    auto step = [&](BGroup &cur, BGroup &nxt) {
+    auto step = [&](BGroup &cur, BGroup &nxt, bool first) {
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
         const uint64_t sn = f_addr();
         f_next();
-        u = stream_rows<0, B, (DIAG & 4) != 0>(u, cur, nxt, voff, sn, eng);
-        if (!published) {
-            asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
-            publish_consts();
-        }
+        u = stream_rows<0, B>(u, cur, nxt, voff, sn, eng);
+        if (first) publish_consts();
         ++q;
         if (++g == G) {
             g = 0;
             await_consts();
-            if (DIAG & 2) {
-                if (u == 0x9e3779b9u) p.d_timeline[lane] = u;  // keep the scan live
-            } else {
-                stream_finish(p, d, u, eng, lane, acc, lb);
-            }
+            stream_finish(p, d, u, eng, lane, acc, lb);
             if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
         }
     };
-    for (;;) {
-        step(ra, rc);
+    // the first step is peeled (it publishes the constants, whose loads are then out of the loop),
+    // so the loop header sees the same two ring slots in flight from the prologue and the back edge
+    step(ra, rc, true);
+    while (q < nq) {
+        step(rb, ra, false);
         if (q >= nq) break;
-        step(rb, ra);
+        step(rc, rb, false);
         if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
+        step(ra, rc, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
-    stamp(2);
     stream_publish(p, acc, eng, lane);
-    stamp(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1450,291 +1416,6 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
 }
 
 // ------------------------------------------------------------------------------------------
-// W = 32 streaming scan on 512-byte rows (AMDCRC_DEBUG bit 15 selects it over the 256-byte rows).
-// Lane l owns the 8-byte word at 8l of every row (one global_load_dwordx2 per row: 512 contiguous
-// bytes per wave instruction), and one row step is a slice-by-8 step whose tables fold in the skip
-// over the other 63 words:  u <- (u ^ w) * x^(8*512), with w = (lo, hi):
-//     u' = sum_q T''_(7-q)[byte q of (u ^ lo)]  ^  sum_q T''_(3-q)[byte q of hi],
-//     T''_k[e] = e * x^(8(k+1)) * x^(8*504).
-// The four high-word lookups do not depend on u, so the per-lane chain is one lookup level per
-// 8 bytes instead of per 4.  LDS: the eight tables in the 64 KiB the 256-byte rows leave half empty
-// (row e = lo tables in bytes [0, 128), hi tables in [128, 256), 8 copies quarter-rotated as in
-// Braid32), so two workgroups still share a CU.  K_l = x^(-64 l) (engine.cpp get_braid_consts).
-constexpr uint32_t kRow8 = 512;
-constexpr int kRows8PerGroup = 8;  // 4 KiB per wave per ring slot
-
-template <uint32_t POLY>
-struct Braid8Basis {
-    uint32_t b[8][8];  // b[k][i] = T''_k[1 << i]
-    constexpr Braid8Basis() : b() {
-        const uint64_t skip = gf2_xpow8n(kRow8 - 8, POLY, 32);
-        for (int i = 0; i < 8; ++i)
-            for (int k = 0; k < 8; ++k) b[k][i] = (uint32_t)gf2_mulmod(gf2_table_entry(1u << i, k, POLY), skip, POLY, 32);
-    }
-};
-
-// basis value b[k][bit] for a per-lane k < 8 (opaque masks: no constant-table load, see basis_bit)
-template <uint32_t POLY>
-__device__ __forceinline__ uint32_t basis8_bit(uint32_t k, int bit) {
-    constexpr Braid8Basis<POLY> B{};
-    uint32_t r = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        uint32_t m = k == (uint32_t)c ? ~0u : 0u;
-        asm("" : "+v"(m));
-        r |= B.b[c][bit] & m;
-    }
-    return r;
-}
-
-template <uint32_t POLY>
-struct Braid8 {
-    using T = uint32_t;
-    static constexpr int W = 32;
-    const char *L;
-    uint32_t cst[4], sel[4];  // as Braid32: quarter << 5 | copy << 2, and the v_perm selector
-
-    __device__ void init(const char *lds, int lane) {
-        L = lds;
-        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t q = (k + j) & 3u;
-            cst[k] = (q << 5) | (cp << 2);
-            sel[k] = 0x0c0c0004u | (q << 8);
-        }
-    }
-    // (u ^ w) * x^(8*512) for the row word w = (lo, hi)
-    __device__ __forceinline__ uint32_t step(uint32_t u, uint32_t lo, uint32_t hi) const {
-        const uint32_t a = u ^ lo;
-        uint32_t l[4], h[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            h[k] = lds32(L + 128, __builtin_amdgcn_perm(cst[k], hi, sel[k]));
-            l[k] = lds32(L, __builtin_amdgcn_perm(cst[k], a, sel[k]));
-        }
-        return xor3(xor3(l[0], l[1], l[2]), xor3(l[3], h[0], h[1]), xor3(h[2], h[3], 0u));
-    }
-    __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-        return (s >> 8) ^ lds32(L, kT0Off + 4 * ((s ^ b) & 0xffu));
-    }
-    __device__ __forceinline__ const char *cbase() const { return L + kBKOff; }
-    __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint4 c = *(const uint4 *)(L + kBKOff + (g * 64 + lane) * 16);
-            acc = xor_and(acc, c.x, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 0), 1));
-            acc = xor_and(acc, c.y, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 1), 1));
-            acc = xor_and(acc, c.z, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 2), 1));
-            acc = xor_and(acc, c.w, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 3), 1));
-        }
-        return acc;
-    }
-};
-
-struct B8Group {
-    uint64_t w[kRows8PerGroup];
-};
-
-template <int R>
-__device__ __forceinline__ uint64_t gld_row8(uint32_t voff, uint64_t sbase) {
-    return __builtin_nontemporal_load((gu64 *)(sbase + voff + R * kRow8));
-}
-
-template <int R>
-__device__ __forceinline__ void stream8_issue(B8Group &g, uint32_t voff, uint64_t s) {
-    if constexpr (R < kRows8PerGroup) {
-        g.w[R] = gld_row8<R>(voff, s);
-        stream8_issue<R + 1>(g, voff, s);
-    }
-}
-
-template <int R, class B>
-__device__ __forceinline__ uint32_t stream8_rows(uint32_t u, B8Group &cur, B8Group &nxt, uint32_t voff, uint64_t snext, const B &eng) {
-    if constexpr (R < kRows8PerGroup) {
-        nxt.w[R] = gld_row8<R>(voff, snext);
-        u = eng.step(u, (uint32_t)cur.w[R], (uint32_t)(cur.w[R] >> 32));
-        __builtin_amdgcn_sched_barrier(0);
-        return stream8_rows<R + 1>(u, cur, nxt, voff, snext, eng);
-    } else {
-        return u;
-    }
-}
-
-template <uint32_t POLY>
-__global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream8_kernel(const ScanParams p) {
-    using B = Braid8<POLY>;
-    constexpr int DIAG = 0;
-    __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
-    const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
-    const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
-    const bool stamps = p.d_timeline != nullptr;
-    auto stamp = [&](int i) {
-        if (stamps && lane == 0) p.d_timeline[gw * 8 + i] = __builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
-    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
-    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = 8u * (uint32_t)lane;
-    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
-    const uint32_t gsh = __builtin_ctz(G);
-    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
-    const bool work = t0 < t1;
-    // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
-    uint32_t fq = 0;  // groups issued
-    uint64_t fb = t0 / T, fk = t0 - fb * T;
-    uint32_t fg = 0;
-    auto f_addr = [&]() -> uint64_t {
-        uint64_t a = fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kRow8 * kRows8PerGroup) : dummy;
-        if (!AMDCRC_GUARD_OK(fq >= nq || (a >= p.base + hoff && a + kRow8 * kRows8PerGroup <=
-                                                                 p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
-                             1, a))
-            a = dummy;
-        return rfl64(a);
-    };
-    auto f_next = [&]() {
-        ++fq;
-        if (++fg == G) {
-            fg = 0;
-            if (++fk == T) fk = 0, ++fb;
-        }
-    };
-    // K-image word and P columns of this thread (published to LDS after the first scan step), then the
-    // first group: both asm loads, complete once the first row wait of the first step has passed
-    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    v4u kq;
-    uint32_t pce0, pce1;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(kq) : "v"(16u * threadIdx.x), "s"(dummy) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce0) : "v"(8u * threadIdx.x), "s"(rfl64((uint64_t)pcs)) : "memory");
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(pce1) : "v"(8u * (threadIdx.x + kBraidBlock)), "s"(rfl64((uint64_t)pcs)) : "memory");
-    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
-    LocalBufs lb{0, 0};
-    if (T > 1 && T <= 32) {
-        const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
-        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
-    }
-    B8Group ra, rb, rc;
-    if (work) {
-        stream8_issue<0>(ra, voff, f_addr());
-        f_next();
-    }
-    if (!(DIAG & 1)) {
-        // row e: bytes [0, 128) the tables of the low word's bytes (quarter q = byte q: T_(7-q)),
-        // bytes [128, 256) the high word's (quarter q = byte 4+q: T_(3-q)); 8 copies per quarter
-        const uint32_t i = threadIdx.x;
-        const uint32_t q = (i >> 1) & 3u, h = i & 1u;
-        uint32_t blo[8], bhi[8];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) blo[b] = basis8_bit<POLY>(7 - q, b), bhi[b] = basis8_bit<POLY>(3 - q, b);
-#pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint32_t e = (i >> 3) + 64u * pass;
-            uint32_t tl = 0, th = 0;
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                tl ^= ((e >> b) & 1u) ? blo[b] : 0u;
-                th ^= ((e >> b) & 1u) ? bhi[b] : 0u;
-            }
-            *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(tl, tl, tl, tl);
-            *(uint4 *)(lds + (e << 8) + 128 + (q << 5) + (h << 4)) = make_uint4(th, th, th, th);
-        }
-        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
-    }
-    if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
-    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(lds + kLocalOff))[threadIdx.x] = 0ull;
-    stamp(4);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    B eng;
-    eng.init(lds, lane);
-    if (work) {
-        stream8_issue<0>(rb, voff, f_addr());
-        f_next();
-    }
-    stamp(1);
-    bool consts_ready = false, published = false;
-    auto publish_consts = [&]() {
-        if (published) return;
-        published = true;
-        *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
-        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
-        *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto await_consts = [&]() {
-        if (consts_ready) return;
-        while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)kBraidWaves)
-            __builtin_amdgcn_s_sleep(1);
-        consts_ready = true;
-    };
-    if (!work) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(kq), "+v"(pce0), "+v"(pce1)::"memory");
-        publish_consts();
-        return;
-    }
-
-    // scan cursor: tile d (buffer, index in buffer), group g, global group q
-    Tile d;
-    d.T = T;
-    d.b = t0 / T;
-    d.k = t0 - d.b * T;
-    d.tbase = d.b * T;
-    d.vbase = 0;
-    d.pad = 0;
-    d.ngroups = G;
-    uint32_t g = 0, u = 0;
-    uint32_t q = 0;  // groups scanned
-    BGroupAcc acc{};
-    acc.slot = ~0ull;
-    auto step = [&](B8Group &cur, B8Group &nxt) {
-        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
-        const uint64_t sn = f_addr();
-        f_next();
-        u = stream8_rows<0>(u, cur, nxt, voff, sn, eng);
-        if (!published) {
-            asm volatile("" : "+v"(kq), "+v"(pce0), "+v"(pce1));  // complete: older than the rows just awaited
-            publish_consts();
-        }
-        ++q;
-        if (++g == G) {
-            g = 0;
-            await_consts();
-            if (DIAG & 2) {
-                if (u == 0x9e3779b9u) p.d_timeline[lane] = u;  // keep the scan live
-            } else {
-                stream_finish(p, d, u, eng, lane, acc, lb);
-            }
-            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
-        }
-    };
-    // the first step is peeled: the loop header then sees the same two slots in flight from the
-    // prologue and from the back edge, and the compiler's row waits come out exact in every step
-    step(ra, rc);
-    while (q < nq) {
-        step(rb, ra);
-        if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
-        step(ra, rc);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing placeholder rows
-    stamp(2);
-    stream_publish(p, acc, eng, lane);
-    stamp(3);
-}
-
-
-// ------------------------------------------------------------------------------------------
 // W = 64 streaming scan (CRC64NVME) for uniform batches whose main region is a whole number of
 // tiles: crc32_stream_kernel's structure on crc64_braid_kernel's 512-byte rows.  A three-slot ring
 // of 8-row groups (4 KiB per wave per slot, 48 VGPRs) on one code path, placeholder rows past the
@@ -1809,89 +1490,9 @@ __device__ __forceinline__ void stream64_finish(const ScanParams &p, const Tile 
     }
 }
 
-template <uint64_t POLY>
-__global__ __launch_bounds__(kBlock, 1) void crc64_stream_kernel(const ScanParams p) {
-    using B = Braid64<POLY>;
-    __shared__ __attribute__((aligned(16))) char lds[kB64Lds];
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
-    // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint32_t gsh = __builtin_ctz(G);
-    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
-    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = 8u * (uint32_t)lane;
-    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
-    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
-    const bool work = t0 < t1;
-    uint32_t fq = 0;  // groups issued
-    uint64_t fb = t0 / T, fk = t0 - fb * T;
-    uint32_t fg = 0;
-    auto f_addr = [&]() -> uint64_t {
-        return rfl64(fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
-                             : dummy);
-    };
-    auto f_next = [&]() {
-        ++fq;
-        if (++fg == G) {
-            fg = 0;
-            if (++fk == T) fk = 0, ++fb;
-        }
-    };
-    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
-    B64Group ra, rb, rc;
-    if (work) {
-        stream64_issue<0>(ra, voff, f_addr());
-        f_next();
-    }
-    b64_build_tables<POLY>(lds);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    B eng;
-    eng.init(lds, lane);
-    eng.kl = kl;
-    if (!work) return;
-    stream64_issue<0>(rb, voff, f_addr());
-    f_next();
-
-    Tile d;
-    d.T = T;
-    d.b = t0 / T;
-    d.k = t0 - d.b * T;
-    d.tbase = d.b * T;
-    d.vbase = 0;
-    d.pad = 0;
-    d.ngroups = G;
-    uint32_t g = 0;
-    uint64_t u = 0;
-    uint32_t q = 0;  // groups scanned
-    auto step = [&](B64Group &cur, B64Group &nxt) {
-        if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0ull;
-        const uint64_t sn = f_addr();
-        f_next();
-        u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
-        ++q;
-        if (++g == G) {
-            g = 0;
-            stream64_finish(p, d, u, eng, lane);
-            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
-        }
-    };
-    for (;;) {
-        step(ra, rc);
-        if (q >= nq) break;
-        step(rb, ra);
-        if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
-    }
-}
-
 // The same scan on the 4-copy table layout (66 KiB of LDS) in 512-thread workgroups, two per CU, so
 // a launch queued on another stream co-resides with the running one.  The default W=64 streaming
-// scan: C5 pipelined 5500-5558 vs 5138-5143 GiB/s for the 8-copy kernel (AMDCRC_DEBUG bit 20), at a
+// scan: C5 pipelined 5500-5558 vs 5138-5143 GiB/s for an 8-copy kernel with one workgroup per CU, at a
 // 4 % slower isolated launch (2-way bank conflicts on the lookups).
 template <uint64_t POLY>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc64_stream4_kernel(const ScanParams p) {
@@ -2322,30 +1923,15 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
-            if (p->stream && !list && (p->dbg & 32768))  // diagnostics: 512-byte rows
-                launch(crc32_stream8_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->stream && !list) {  // DIAG bits (diagnostics): AMDCRC_DEBUG bits 16-18
-                switch ((p->dbg >> 16) & 7) {
-                    case 1: launch(crc32_stream_kernel<kPoly32C, 1>, nblocks, kBraidBlock, s, p, ev); break;
-                    case 2: launch(crc32_stream_kernel<kPoly32C, 2>, nblocks, kBraidBlock, s, p, ev); break;
-                    case 4: launch(crc32_stream_kernel<kPoly32C, 4>, nblocks, kBraidBlock, s, p, ev); break;
-                    case 7: launch(crc32_stream_kernel<kPoly32C, 7>, nblocks, kBraidBlock, s, p, ev); break;
-                    default: launch(crc32_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev); break;
-                }
-            }
+            if (p->stream && !list)
+                launch(crc32_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->dbg & 4)  // diagnostics: plain XOR chain instead of v_bitop3
-                launch(crc32_braid_kernel<kPoly32C, false, false>, nblocks, kBraidBlock, s, p, ev);
-            else if (p->dbg & 1024)  // diagnostics: cached (temporal) payload loads
-                launch(crc32_braid_kernel<kPoly32C, false, true, false>, nblocks, kBraidBlock, s, p, ev);
             else
                 launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (p->stream && !list && (p->dbg & 1048576))  // diagnostics: 8-copy tables, one workgroup per CU
-                launch(crc64_stream_kernel<kPoly64Nvme>, nblocks, kBlock, s, p, ev);
-            else if (p->stream && !list)  // 4-copy tables, two workgroups per CU
+            if (p->stream && !list)  // 4-copy tables, two workgroups per CU
                 launch(crc64_stream4_kernel<kPoly64Nvme>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);

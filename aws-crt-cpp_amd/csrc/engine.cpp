@@ -1,11 +1,15 @@
 // Host side of the MI355X checksum engine: device bring-up, constant tables, workspaces, batch
-// planning and the C ABI (include/aws_crt_amd/checksums_batch.h, include/aws/checksums/*.h).
+// planning and the batched C ABI (include/aws_crt_amd/checksums_batch.h).
 //
 // The reference's equivalent is one synchronous CPU call per buffer
-// (source/checksum/CRC.cpp:15-43 -> aws-checksums).  Here every checksum is computed by the gfx950
-// kernels in crc_kernels.hip; this file only plans work and moves descriptors.  There is no CPU
-// checksum path: when HIP has no usable device the batch entry points return
-// AWS_CRT_AMD_ERR_NO_DEVICE and the value-only single-buffer entry points abort.
+// (source/checksum/CRC.cpp:15-43 -> aws-checksums).  Here the checksums of device-resident batches
+// are computed by the gfx950 kernels in crc_kernels.hip / xxh3_kernels.hip; this file plans work and
+// moves descriptors.  The single-buffer aws-checksums ABI and its CPU / GPU dispatch live in
+// abi_single.cpp; the host path in csrc/cpu/.
+//
+// No library call synchronises the whole device.  Growing a cached table or workspace never frees
+// memory that queued kernels may still read: the old allocation is retired (kept until process
+// exit; growth is geometric, so retired memory is bounded by the live size).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,6 +25,7 @@
 
 #include <aws/crt/Types.h>
 
+#include "cpu/cpu_checksums.h"
 #include "engine.h"
 #include "gf2.h"
 
@@ -32,7 +37,7 @@ using namespace amdcrc;
 namespace {
 
 thread_local std::string g_last_error;
-// diagnostics (aws_crt_amd_debug_time_next_launch): events stamped by the next scan dispatch
+// measurement hook (aws_crt_amd_debug_time_next_launch): events stamped by the next scan dispatch
 thread_local void *g_time_events[2] = {nullptr, nullptr};
 
 int fail(int code, const std::string &msg) {
@@ -52,36 +57,47 @@ struct DevBuf {
 };
 
 // Per-stream cross-tile workspace.  Kernels on one stream are serialised, and each launch leaves
-// the words it touched at zero, so a workspace is reusable by the next launch on its stream.
+// the words it touched at zero, so a workspace is reusable by the next launch on its stream.  A
+// launch captured into a HIP graph keeps its capture stream's workspace: replay such a graph on the
+// capture stream, or while no eager launch of the capture stream runs.
 struct Workspace {
     unsigned long long *acc = nullptr;   // per buffer
     unsigned int *cnt = nullptr;         // per buffer
     unsigned long long *acc1 = nullptr;  // per tile (32-tile group slots of the braided scans)
     unsigned int *cnt1 = nullptr;        // per tile (W=64 group arrival counts)
-    unsigned int *claim = nullptr;       // dynamic tile pool: 2 words per shard
+    unsigned int *claim = nullptr;       // workgroup tile pools: 2 words per shard
     size_t cap = 0, cap_tiles = 0;
+};
+
+// Per-stream descriptor staging: three (pinned host, device) slots used round-robin, each with the
+// event of its last upload, so a call waits only for the upload of the call three before it.
+constexpr int kStageSlots = 3;
+struct Stage {
+    DevBuf dev[kStageSlots], host[kStageSlots];
+    hipEvent_t done[kStageSlots] = {nullptr, nullptr, nullptr};
+    int next = 0, cur = 0;
 };
 
 struct Device {
     int id = -1;
     int cus = 0;
     std::mutex mu;
-    std::map<std::pair<int, uint32_t>, DevBuf> kvals;           // (alg, seg) -> 64 x u64
-    std::map<int, DevBuf> braid;                                // alg -> W=32 braided-scan constants
-    std::map<std::pair<int, uint64_t>, DevBuf> pcols;           // (alg, tile) -> tmax x W x u64
+    std::map<int, DevBuf> braid;                       // alg -> W=32 braided-scan constants
+    std::map<int, DevBuf> braid64;                     // alg -> W=64 braided-scan constants
+    std::map<std::pair<int, uint64_t>, DevBuf> pcols;  // (alg, tile) -> tmax x W x u64
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
+    std::vector<DevBuf> retired;                       // outgrown buffers queued kernels may still read
     std::map<hipStream_t, Workspace> ws;
     std::map<hipStream_t, DevBuf> xsums;  // split XXH3 long path: per-block accumulator sums
-    DevBuf xpow2;                                               // per alg: 64 x x^(8*2^i)
-    // list-mode descriptor staging
-    std::map<hipStream_t, std::pair<DevBuf, DevBuf>> desc;      // (device, pinned host)
-    std::map<hipStream_t, hipEvent_t> desc_done;
-    // single-buffer / host path
+    std::map<hipStream_t, Stage> stage;
+    std::map<hipStream_t, DevBuf> mp_out;  // multipart part results
+    // single path (GPU-dispatched host buffers, device buffers through the aws-checksums ABI)
     hipStream_t own_stream = nullptr;
     void *pin[2] = {nullptr, nullptr};
     void *dbuf[2] = {nullptr, nullptr};
     hipEvent_t pin_free[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
+    DevBuf hash_stage;        // whole-buffer device copy for GPU-dispatched host xxHash
     void *d_small = nullptr;  // results / seeds for the single path
     std::mutex single_mu;
 };
@@ -90,25 +106,30 @@ std::mutex g_mu;
 std::map<int, std::unique_ptr<Device>> g_devices;
 
 int device_count_noinit() {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    static const int n = [] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        return c;
+    }();
     return n;
 }
 
 int get_device(Device **out) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(AWS_CRT_AMD_ERR_NO_DEVICE, "no HIP device visible");
+    if (device_count_noinit() <= 0) return fail(AWS_CRT_AMD_ERR_NO_DEVICE, "no HIP device visible");
     int id = 0;
     HIP_TRY(hipGetDevice(&id));
     std::lock_guard<std::mutex> g(g_mu);
     auto &slot = g_devices[id];
     if (!slot) {
-        auto d = std::make_unique<Device>();
-        d->id = id;
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, id));
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             return fail(AWS_CRT_AMD_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", engine is built for gfx950");
+        auto d = std::make_unique<Device>();
+        d->id = id;
         d->cus = prop.multiProcessorCount;
         slot = std::move(d);
     }
@@ -118,78 +139,52 @@ int get_device(Device **out) {
 
 inline int width_of(int alg) { return alg == ALG_CRC64NVME ? 64 : 32; }
 
-int upload(DevBuf &b, const void *host, size_t bytes) {
-    if (b.bytes < bytes) {
-        if (b.p) (void)hipFree(b.p);
-        b.p = nullptr;
-        b.bytes = 0;
-        HIP_TRY(hipMalloc(&b.p, bytes));
-        b.bytes = bytes;
+// hipStreamIsCapturing: paths that allocate or synchronise refuse captured streams (the caller
+// warms the engine up on the stream before capturing)
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
     }
-    HIP_TRY(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
-    return 0;
+    return st != hipStreamCaptureStatusNone;
 }
 
-// K_l = x^(8*seg*(63-l)) moves lane l's partial to the end of its tile.
-//   W=64: the 64 values K_l.
-//   W=32: the kernel's LDS image of the 32 matrix columns K_l * x^j, laid out [j/4][lane][j%4] as
-//         u32 so one ds_read_b128 fetches four columns conflict-free (8 KiB = 1024 threads x 8 B).
-int get_kvals(Device *d, int alg, uint32_t seg, const uint64_t **out) {
-    auto key = std::make_pair(alg, seg);
-    auto it = d->kvals.find(key);
-    if (it == d->kvals.end()) {
-        const uint64_t poly = alg_poly(alg);
-        const int w = width_of(alg);
-        std::vector<uint64_t> k(w == 64 ? 64 : kBlock, 0);
-        if (w == 64) {
-            for (int l = 0; l < 64; ++l) k[l] = gf2_xpow8n((uint64_t)seg * (63 - l), poly, w);
-        } else {
-            uint32_t *img = (uint32_t *)k.data();
-            for (int l = 0; l < 64; ++l) {
-                uint64_t col = gf2_xpow8n((uint64_t)seg * (63 - l), poly, w);
-                for (int j = 0; j < 32; ++j) {
-                    img[((j >> 2) * 64 + l) * 4 + (j & 3)] = (uint32_t)col;
-                    col = gf2_mulx(col, poly);
-                }
-            }
-        }
-        DevBuf b;
-        int rc = upload(b, k.data(), k.size() * 8);
-        if (rc) return rc;
-        it = d->kvals.emplace(key, b).first;
-    }
-    *out = (const uint64_t *)it->second.p;
+int upload_new(DevBuf &b, const void *host, size_t bytes) {
+    HIP_TRY(hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+    HIP_TRY(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
     return 0;
 }
 
 // x^-1 * t : inverse of gf2_mulx (the reflected polynomial's top bit is the x^0 coefficient, 1)
 inline uint32_t inv_mulx32(uint32_t t, uint32_t poly) { return (t & 0x80000000u) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
+inline uint64_t inv_mulx64(uint64_t t, uint64_t poly) { return (t >> 63) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 
-// W=32 braided-scan constants (layout: engine.h kBraidConstWords).  word_bytes: bytes per lane per
-// row (4: 256-byte rows, K_l = x^(-32 l); 8: the 512-byte-row streaming scan, K_l = x^(-64 l))
-int get_braid_consts(Device *d, int alg, const uint64_t **out, int word_bytes = 4) {
-    const int key = alg + (word_bytes == 8 ? 16 : 0);
-    auto it = d->braid.find(key);
+// W=32 braided-scan constants (layout: engine.h kBraidConstWords): the K image of x^(-32 l) (32 matrix
+// columns per lane), T' (the row step's slice-by-4 tables) and T0 (byte table)
+int get_braid_consts(Device *d, int alg, const uint64_t **out) {
+    auto it = d->braid.find(alg);
     if (it == d->braid.end()) {
         const uint32_t poly = (uint32_t)alg_poly(alg);
         std::vector<uint32_t> c(kBraidConstWords, 0);
-        uint32_t kl = 0x80000000u;  // x^0, then x^(-8 word_bytes l)
+        uint32_t kl = 0x80000000u;  // x^0, then x^(-32 l)
         for (int l = 0; l < 64; ++l) {
             uint32_t col = kl;
             for (int j = 0; j < 32; ++j) {
                 c[((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
                 col = (uint32_t)gf2_mulx(col, poly);
             }
-            for (int i = 0; i < 8 * word_bytes; ++i) kl = inv_mulx32(kl, poly);
+            for (int i = 0; i < 32; ++i) kl = inv_mulx32(kl, poly);
         }
         const uint64_t skip = gf2_xpow8n(kBraidRow - 4, poly, 32);
         for (int i = 0; i < 1024; ++i)
             c[2048 + i] = (uint32_t)gf2_mulmod(gf2_table_entry(i & 255, i >> 8, poly), skip, poly, 32);
         for (int e = 0; e < 256; ++e) c[3072 + e] = (uint32_t)gf2_table_entry(e, 0, poly);
         DevBuf b;
-        int rc = upload(b, c.data(), c.size() * 4);
+        int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
-        it = d->braid.emplace(key, b).first;
+        it = d->braid.emplace(alg, b).first;
     }
     *out = (const uint64_t *)it->second.p;
     return 0;
@@ -197,11 +192,9 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out, int word_bytes = 
 
 // W=64 braided-scan constants: K_l = x^(-64 l), l < 64, then zeros to 16 KiB (a wave without
 // payload primes its ring from this block: two groups of its words stay inside)
-inline uint64_t inv_mulx64(uint64_t t, uint64_t poly) { return (t >> 63) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
-    auto key = std::make_pair(alg, 0u);
-    auto it = d->kvals.find(key);
-    if (it == d->kvals.end()) {
+    auto it = d->braid64.find(alg);
+    if (it == d->braid64.end()) {
         const uint64_t poly = alg_poly(alg);
         std::vector<uint64_t> c(2048, 0);
         uint64_t kl = 1ull << 63;  // x^0
@@ -210,19 +203,20 @@ int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
             for (int i = 0; i < 64; ++i) kl = inv_mulx64(kl, poly);
         }
         DevBuf b;
-        int rc = upload(b, c.data(), c.size() * 8);
+        int rc = upload_new(b, c.data(), c.size() * 8);
         if (rc) return rc;
-        it = d->kvals.emplace(key, b).first;
+        it = d->braid64.emplace(alg, b).first;
     }
     *out = (const uint64_t *)it->second.p;
     return 0;
 }
 
 // column j of P_k = x^(8*tile*k) * x^j, k < tmax : moves tile k's partial to its buffer end
-int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t **out) {
+int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, hipStream_t s, const uint64_t **out) {
     auto key = std::make_pair(alg, tile);
     auto it = d->pcols_tmax.find(key);
     if (it == d->pcols_tmax.end() || it->second < tmax) {
+        if (capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "engine tables must be warmed up before stream capture");
         uint64_t want = std::max<uint64_t>(tmax, 64);
         if (it != d->pcols_tmax.end()) want = std::max(want, it->second * 2);
         const uint64_t poly = alg_poly(alg);
@@ -238,16 +232,11 @@ int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t *
             }
             pk = gf2_mulmod(pk, step, poly, w);
         }
-        DevBuf &b = d->pcols[key];
-        // the table may be in use by queued kernels on other streams: never shrink or free in place
         DevBuf nb;
-        HIP_TRY(hipMalloc(&nb.p, cols.size() * 8));
-        nb.bytes = cols.size() * 8;
-        HIP_TRY(hipMemcpy(nb.p, cols.data(), nb.bytes, hipMemcpyHostToDevice));
-        if (b.p) {
-            HIP_TRY(hipDeviceSynchronize());
-            (void)hipFree(b.p);
-        }
+        int rc = upload_new(nb, cols.data(), cols.size() * 8);
+        if (rc) return rc;
+        DevBuf &b = d->pcols[key];
+        if (b.p) d->retired.push_back(b);  // queued kernels on other streams may still read it
         b = nb;
         d->pcols_tmax[key] = want;
     }
@@ -255,44 +244,30 @@ int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, const uint64_t *
     return 0;
 }
 
+// zero-initialised device words, ordered before the stream's next kernel
+template <class T>
+int alloc_zero(T **p, size_t n, hipStream_t s) {
+    HIP_TRY(hipMalloc((void **)p, n * sizeof(T)));
+    HIP_TRY(hipMemsetAsync(*p, 0, n * sizeof(T), s));
+    return 0;
+}
+
 int get_workspace(Device *d, hipStream_t s, size_t nbuf, size_t ntiles, Workspace **out) {
     Workspace &w = d->ws[s];
+    const bool grow = w.cap_tiles < ntiles || !w.claim || w.cap < nbuf;
+    if (grow && capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "engine workspace must be warmed up before stream capture");
+    int rc;
     if (w.cap_tiles < ntiles) {
-        size_t cap = std::max<size_t>(ntiles, w.cap_tiles * 2);
-        if (w.acc1) {
-            HIP_TRY(hipStreamSynchronize(s));
-            (void)hipFree(w.acc1);
-            (void)hipFree(w.cnt1);
-            w.acc1 = nullptr;
-            w.cnt1 = nullptr;
-        }
-        HIP_TRY(hipMalloc((void **)&w.acc1, cap * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(w.acc1, 0, cap * sizeof(unsigned long long)));
-        HIP_TRY(hipMalloc((void **)&w.cnt1, cap * sizeof(unsigned int)));
-        HIP_TRY(hipMemset(w.cnt1, 0, cap * sizeof(unsigned int)));
-        HIP_TRY(hipDeviceSynchronize());
+        const size_t cap = std::max<size_t>(ntiles, w.cap_tiles * 2);
+        if (w.acc1) d->retired.push_back({w.acc1, 0}), d->retired.push_back({w.cnt1, 0});
+        if ((rc = alloc_zero(&w.acc1, cap, s)) || (rc = alloc_zero(&w.cnt1, cap, s))) return rc;
         w.cap_tiles = cap;
     }
-    if (!w.claim) {
-        const size_t words = 2 * 1024;  // >= 2 x (max workgroups / kShardBlocks)
-        HIP_TRY(hipMalloc((void **)&w.claim, words * sizeof(unsigned int)));
-        HIP_TRY(hipMemset(w.claim, 0, words * sizeof(unsigned int)));
-        HIP_TRY(hipDeviceSynchronize());
-    }
+    if (!w.claim && (rc = alloc_zero(&w.claim, 2 * 1024, s))) return rc;  // >= 2 x (max workgroups / kShardBlocks)
     if (w.cap < nbuf) {
-        size_t cap = std::max<size_t>(nbuf, w.cap * 2);
-        if (w.acc) {
-            HIP_TRY(hipStreamSynchronize(s));
-            (void)hipFree(w.acc);
-            (void)hipFree(w.cnt);
-            w.acc = nullptr;
-            w.cnt = nullptr;
-        }
-        HIP_TRY(hipMalloc((void **)&w.acc, cap * sizeof(unsigned long long)));
-        HIP_TRY(hipMalloc((void **)&w.cnt, cap * sizeof(unsigned int)));
-        HIP_TRY(hipMemset(w.acc, 0, cap * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(w.cnt, 0, cap * sizeof(unsigned int)));
-        HIP_TRY(hipDeviceSynchronize());
+        const size_t cap = std::max<size_t>(nbuf, w.cap * 2);
+        if (w.acc) d->retired.push_back({w.acc, 0}), d->retired.push_back({w.cnt, 0});
+        if ((rc = alloc_zero(&w.acc, cap, s)) || (rc = alloc_zero(&w.cnt, cap, s))) return rc;
         w.cap = cap;
     }
     *out = &w;
@@ -307,8 +282,8 @@ inline uint64_t main_len(uint64_t ptr, uint64_t n) {
 
 // Bytes per lane per tile.  A tile is 64*seg bytes; pick the largest seg (fewest partials to
 // combine) that still gives every wavefront slot on the chip a tile and does not exceed the
-// typical buffer.  per_slot: tiles wanted per wave slot (2 when a dynamic pool balances the waves);
-// waves_per_cu: the launch's wave slots per CU.
+// typical buffer.  per_slot: tiles wanted per wave slot (2 when a workgroup pool balances the
+// waves); waves_per_cu: the launch's wave slots per CU.
 uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main, uint64_t per_slot = 1,
                     uint64_t waves_per_cu = kWavesPerBlock) {
     const uint64_t slots = (uint64_t)d->cus * waves_per_cu * per_slot;
@@ -320,42 +295,26 @@ uint32_t choose_seg(const Device *d, uint64_t total_main, uint64_t typical_main,
 
 inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 
-// Launch geometry of the scan kernels.  The W=32 braided scan runs 512-thread workgroups (8 waves,
-// 77 KiB LDS), two of which fit a CU.  A small batch (under 256 MiB of main bytes) launches one per
-// CU: a single launch then takes 6 % longer (19.0 vs 17.9 us for 1024 x 64 KiB), but launches queued
-// on other streams find a free workgroup slot on every CU, so one launch's prologue and drain
-// overlap another's streaming (4950 vs 4290 GiB/s with 3 streams).  Large batches
-// are long enough to amortise their own ramp and use both slots.  The W=64 scan runs one
-// 1024-thread workgroup per CU (130 KiB LDS).
+// Launch geometry of the scan kernels.  The W=32 scans run 512-thread workgroups (8 waves, 77-80 KiB
+// LDS), two of which fit a CU.  A small batch (under 256 MiB of main bytes) launches one per CU: a
+// single launch then takes 6 % longer (19.0 vs 17.9 us for 1024 x 64 KiB), but launches queued on
+// other streams find a free workgroup slot on every CU, so one launch's prologue and drain overlap
+// another's streaming (4950 vs 4290 GiB/s with 3 streams).  Large batches are long
+// enough to amortise their own ramp and use both slots.  The W=64 streaming scan runs 512-thread
+// workgroups two per CU (66 KiB of LDS); the W=64 braided scan one 1024-thread workgroup per CU.
 constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 constexpr uint64_t kLaneMaxBytes = 4096;
 // Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
 constexpr uint64_t kXxh3SplitBlocks = 4096;
-uint32_t debug_flags();
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
 ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main, bool w64_half_blocks = false) {
-    // w64_half_blocks: crc64_stream4_kernel, 512-thread workgroups two per CU (66 KiB of LDS)
     const uint64_t wpb = width_of(alg) == 32 || w64_half_blocks ? 8 : (uint64_t)kWavesPerBlock;
-    static const int wpc = [] {  // diagnostics: AMDCRC_WG_PER_CU forces the W=32 workgroups per CU
-        const char *e = std::getenv("AMDCRC_WG_PER_CU");
-        return e ? std::atoi(e) : 0;
-    }();
-    const uint64_t per_cu = w64_half_blocks                       ? 2
-                            : width_of(alg) == 32 && wpc > 0         ? (uint64_t)wpc
-                            : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
-    uint64_t cap = (uint64_t)d->cus * per_cu;
-    static const double frac = [] {  // diagnostics: AMDCRC_GRID_FRAC caps the grid at a share of the slots
-        const char *e = std::getenv("AMDCRC_GRID_FRAC");
-        return e ? std::atof(e) : 1.0;
-    }();
-    if (frac > 0 && frac < 1) cap = std::max<uint64_t>(1, (uint64_t)(cap * frac));
-    // diagnostics: AMDCRC_DEBUG bit 22 spreads a W=64 small batch's tiles over twice the workgroups
-    // (every other wave idle), so every CU holds tiles instead of half of them
-    const uint64_t tpb = w64_half_blocks && total_main < kSmallBatchBytes && (debug_flags() & 4194304) ? wpb / 2 : wpb;
-    const uint64_t blocks = std::min<uint64_t>((ntiles + tpb - 1) / tpb, cap);
+    const uint64_t per_cu = w64_half_blocks ? 2 : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
+    const uint64_t cap = (uint64_t)d->cus * per_cu;
+    const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, cap);
     return {blocks, wpb};
 }
 
@@ -366,39 +325,9 @@ int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("hash kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
 
-uint32_t debug_flags() {
-    static const uint32_t f = [] {
-        const char *e = std::getenv("AMDCRC_DEBUG");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
-    }();
-    return f;
-}
-
-// Diagnostics only (AMDCRC_DEBUG bit 4): per-wave timeline of the last braided scan launch.
-struct Timeline {
-    unsigned long long *d = nullptr;
-    size_t cap = 0, waves = 0;
-} g_timeline;
-
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, uint64_t total_main, hipStream_t s) {
-    p.dbg = debug_flags();
-    p.d_timeline = nullptr;
-    if (p.dbg & 16) {
-        const size_t waves = (size_t)d->cus * kWavesPerBlock;
-        if (g_timeline.cap < waves) {
-            if (g_timeline.d) (void)hipFree(g_timeline.d);
-            HIP_TRY(hipMalloc((void **)&g_timeline.d, waves * 8 * sizeof(unsigned long long)));
-            g_timeline.cap = waves;
-        }
-        g_timeline.waves = waves;
-        p.d_timeline = g_timeline.d;
-    }
     const uint64_t tile = (uint64_t)p.seg * kWave;
-    const bool braided = width_of(alg) == 32 || !(p.dbg & 2048);  // dbg 2048: first-generation W=64 scan
-    const int word_bytes = p.stream && alg == ALG_CRC32C && (p.dbg & 32768) ? 8 : 4;  // crc32_stream8_kernel
-    int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals, word_bytes)
-             : braided           ? get_braid64_consts(d, alg, &p.d_kvals)
-                                 : get_kvals(d, alg, p.seg, &p.d_kvals);
+    int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals) : get_braid64_consts(d, alg, &p.d_kvals);
     if (rc) return rc;
     p.d_pcols = nullptr;
     p.pcols_tmax = 0;
@@ -408,17 +337,17 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     p.d_cnt1 = nullptr;
     p.d_claim = nullptr;
     if (tmax > 1 || p.nstatic) {
-        if ((rc = get_pcols(d, alg, tile, tmax, &p.d_pcols))) return rc;
+        if ((rc = get_pcols(d, alg, tile, tmax, s, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
         Workspace *w;
-        if ((rc = get_workspace(d, s, nbuf, braided ? p.ntiles : 0, &w))) return rc;
+        if ((rc = get_workspace(d, s, nbuf, p.ntiles, &w))) return rc;
         p.d_acc = w->acc;
         p.d_cnt = w->cnt;
         p.d_acc1 = w->acc1;
         p.d_cnt1 = w->cnt1;
         p.d_claim = w->claim;
     }
-    const bool w64_half = width_of(alg) == 64 && p.stream && !(p.dbg & 1048576);  // crc64_stream4_kernel
+    const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
     const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half).blocks;
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
@@ -441,19 +370,16 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         xp.seed_all = seed_all;
         xp.d_out = (uint64_t *)d_out;
         // XXH3 over long uniform buffers: a block-sum pass over all CUs, then one wave per buffer
-        // scrambles the 64-byte sums (xxh3_kernels.hip; AMDCRC_DEBUG bit 24 keeps one pass)
+        // scrambles the 64-byte sums (xxh3_kernels.hip)
         const uint64_t nb = len > 240 ? (len - 1) / 1024 : 0;
-        if (alg != AWS_CRT_AMD_XXH64 && nb >= kXxh3SplitBlocks && !(debug_flags() & 16777216)) {
+        if (alg != AWS_CRT_AMD_XXH64 && nb >= kXxh3SplitBlocks) {
             std::lock_guard<std::mutex> g(d->mu);
             DevBuf &xs = d->xsums[s];
             const size_t need = count * nb * 64;
             if (xs.bytes < need) {
-                if (xs.p) {
-                    HIP_TRY(hipStreamSynchronize(s));  // queued launches may still read the old sums
-                    (void)hipFree(xs.p);
-                    xs.p = nullptr;
-                    xs.bytes = 0;
-                }
+                if (capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "engine workspace must be warmed up before stream capture");
+                if (xs.p) d->retired.push_back(xs);  // queued launches may still read the old sums
+                xs = DevBuf{};
                 HIP_TRY(hipMalloc(&xs.p, need));
                 xs.bytes = need;
             }
@@ -469,32 +395,25 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     std::lock_guard<std::mutex> g(d->mu);
     const uint64_t ml = main_len(base, len);
     ScanParams p{};
-    // W=32: every wave scans one static tile, then claims tiles from its shard's pool, so waves the
-    // memory system serves late take less of the batch (dynamic tile pool)
-    // Only where the pool does not shrink the tiles: smaller tiles cost a tile finish per 8 KiB and
-    // measured slower on 1024 x 64 KiB (3704 vs 4380 GiB/s), while on 16 x 256 MiB and 131072 x 8 KiB
-    // the pool gains 3-4 % at equal tiles.
-    p.seg = choose_seg(d, ml * count, ml, 1);
-    // Batches whose main regions are whole tiles take the streaming scans (crc_kernels.hip
-    // crc32_stream_kernel / crc64_stream_kernel; AMDCRC_DEBUG bit 14 disables them).  Their tiles are
-    // sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C measured 5250-5315 GiB/s with
-    // one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
+    // Batches whose main regions are whole tiles take the streaming scans (crc32_stream_kernel,
+    // crc64_stream4_kernel), tiles sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C
+    // measured 5250-5315 GiB/s with one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
     // W=64 small batches: tiles for 4 waves per CU.  A tile that spans a whole buffer finishes without
     // the cross-tile combine (global atomics with return, pcol loads), which costs a W=64 wave more
     // than the idle slots do once other streams' launches fill them: 1024 x 64 KiB CRC64NVME measured
     // 2774 GiB/s with 16 KiB tiles (4 per buffer), 3930 with 32 KiB, 4010 with 64 KiB.
+    p.seg = choose_seg(d, ml * count, ml, 1);
     const bool w32 = width_of(alg) == 32;
     const bool small = ml * count < kSmallBatchBytes;
     const uint64_t wpc = w32 ? 8 * (small ? 1 : 2) : small ? 4 : (uint64_t)kWavesPerBlock;
     const uint32_t seg_stream = choose_seg(d, ml * count, ml, 1, wpc);
-    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0 && !(debug_flags() & 16384);
+    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0;
     if (stream) p.seg = seg_stream;
-    static const uint32_t seg_env = [] {  // diagnostics: AMDCRC_SEG forces bytes per lane per tile
-        const char *e = std::getenv("AMDCRC_SEG");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    if (seg_env >= (uint32_t)kGroupBytes && (seg_env & (seg_env - 1)) == 0) p.seg = seg_env;
-    const bool pool = w32 && ml > 0 && !(debug_flags() & 4096) && choose_seg(d, ml * count, ml, 2) == p.seg;
+    // W=32 braided scan: every wave scans one static tile, then claims tiles from its workgroup's
+    // pool, where the pool does not shrink the tiles (smaller tiles cost a tile finish per 8 KiB and
+    // measured slower on 1024 x 64 KiB: 3704 vs 4380 GiB/s; on 16 x 256 MiB and 131072 x 8 KiB the
+    // pool gains 3-4 % at equal tiles)
+    const bool pool = w32 && ml > 0 && choose_seg(d, ml * count, ml, 2) == p.seg;
     const uint64_t tile = (uint64_t)p.seg * kWave;
     const uint64_t T = ml ? (ml + tile - 1) / tile : 1;
     p.base = base;
@@ -515,37 +434,39 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     return launch_scan(d, alg, p, count, T, ml * count, s);
 }
 
-// Per-stream pinned -> device descriptor staging.  stage_begin returns host memory to fill;
-// stage_end queues its upload on the stream and returns the device copy.
+// Descriptor staging: returns pinned host memory to fill (slot `cur`); stage_end queues its upload
+// on the stream and returns the device copy.  The slot reused is the one three calls old.
 int stage_begin(Device *d, hipStream_t s, size_t bytes, void **host) {
-    auto &st = d->desc[s];
-    auto ev = d->desc_done.find(s);
-    if (ev == d->desc_done.end()) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ev = d->desc_done.emplace(s, e).first;
+    Stage &st = d->stage[s];
+    const int k = st.next;
+    st.cur = k;
+    st.next = (k + 1) % kStageSlots;
+    if (!st.done[k]) {
+        HIP_TRY(hipEventCreateWithFlags(&st.done[k], hipEventDisableTiming));
     } else {
-        HIP_TRY(hipEventSynchronize(ev->second));  // previous upload from this staging is done
+        HIP_TRY(hipEventSynchronize(st.done[k]));  // this slot's previous upload has been performed
     }
-    if (st.first.bytes < bytes) {
-        // the device copy may still be read by queued kernels of this stream
-        if (st.first.p) HIP_TRY(hipStreamSynchronize(s));
-        if (st.first.p) (void)hipFree(st.first.p);
-        if (st.second.p) (void)hipHostFree(st.second.p);
-        size_t cap = std::max<size_t>(bytes, st.first.bytes * 2);
-        HIP_TRY(hipMalloc(&st.first.p, cap));
-        HIP_TRY(hipHostMalloc(&st.second.p, cap, hipHostMallocDefault));
-        st.first.bytes = st.second.bytes = cap;
+    if (st.dev[k].bytes < bytes) {
+        if (capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "descriptor staging must be warmed up before stream capture");
+        if (st.dev[k].p) d->retired.push_back(st.dev[k]);  // the device copy may still be read by queued kernels
+        if (st.host[k].p) (void)hipHostFree(st.host[k].p);  // its upload has completed (event above)
+        const size_t cap = std::max<size_t>(bytes, st.dev[k].bytes * 2);
+        st.dev[k] = DevBuf{};
+        st.host[k] = DevBuf{};
+        HIP_TRY(hipMalloc(&st.dev[k].p, cap));
+        HIP_TRY(hipHostMalloc(&st.host[k].p, cap, hipHostMallocDefault));
+        st.dev[k].bytes = st.host[k].bytes = cap;
     }
-    *host = st.second.p;
+    *host = st.host[k].p;
     return 0;
 }
 
 int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
-    auto &st = d->desc[s];
-    HIP_TRY(hipMemcpyAsync(st.first.p, st.second.p, bytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipEventRecord(d->desc_done[s], s));
-    *dev = st.first.p;
+    Stage &st = d->stage[s];
+    const int k = st.cur;
+    HIP_TRY(hipMemcpyAsync(st.dev[k].p, st.host[k].p, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(st.done[k], s));
+    *dev = st.dev[k].p;
     return 0;
 }
 
@@ -564,9 +485,8 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         maxlen = std::max<uint64_t>(maxlen, lens[i]);
     }
     const bool xxh = is_hash(alg);
-    // lists of short buffers only (event-stream framing): one lane per buffer (crc_lanes_kernel);
-    // AMDCRC_DEBUG bit 23 keeps them on the wave-per-tile scan
-    if (!xxh && maxlen <= kLaneMaxBytes && !(debug_flags() & 8388608)) {
+    // lists of short buffers only (event-stream framing): one lane per buffer (crc_lanes_kernel)
+    if (!xxh && maxlen <= kLaneMaxBytes) {
         uint64_t *h;
         int rc1 = stage_begin(d, s, count * 16, (void **)&h);
         if (rc1) return rc1;
@@ -646,7 +566,7 @@ int ensure_stage(Device *d, size_t bytes) {
     if (d->stage_bytes >= bytes) return 0;
     for (int i = 0; i < 2; ++i) {
         if (d->pin[i]) {
-            HIP_TRY(hipStreamSynchronize(d->own_stream));
+            HIP_TRY(hipStreamSynchronize(d->own_stream));  // the engine's own stream only
             (void)hipHostFree(d->pin[i]);
             (void)hipFree(d->dbuf[i]);
         }
@@ -659,6 +579,7 @@ int ensure_stage(Device *d, size_t bytes) {
 }
 
 bool is_device_ptr(const void *p) {
+    if (!p || device_count_noinit() <= 0) return false;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
@@ -669,9 +590,9 @@ bool is_device_ptr(const void *p) {
 
 constexpr size_t kStageChunk = 16u << 20;
 
-// One buffer (host or device memory), synchronous.  Host data streams through two pinned slots;
-// chunk i+1 is seeded on the device with chunk i's result, so no host round trip sits between
-// chunks (the running-CRC semantics of CRC.h:20).
+// One buffer (host or device memory) on the GPU, synchronous.  Host data streams through two pinned
+// slots; chunk i+1 is seeded on the device with chunk i's result, so no host round trip sits
+// between chunks (the running-CRC semantics of CRC.h:20).
 int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t *result) {
     Device *d;
     int rc = get_device(&d);
@@ -681,23 +602,24 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
     hipStream_t s = d->own_stream;
     const size_t osz = alg == AWS_CRT_AMD_XXH3_128 ? 16 : (width_of(alg) == 64 || is_hash(alg)) ? 8 : 4;
     char *res = (char *)d->d_small;  // two result slots (ping-pong) + seed slot
-    if (len == 0 || !input) {
-        // CRC of nothing is the seed itself (state ~seed, complemented back); XXH64 still runs
-        if (!is_hash(alg)) {
-            *result = seed;
-            return 0;
-        }
+    if ((len == 0 || !input) && !is_hash(alg)) {
+        *result = seed;  // CRC of nothing is the seed itself
+        return 0;
     }
     if (is_hash(alg)) {
-        // xxHash is not chunkable by seed; stage the whole buffer if it is in host memory
+        // xxHash is not chunkable by seed: a host buffer is copied whole into a cached device buffer
         const void *dp = input;
-        DevBuf tmp;
         if (len && !is_device_ptr(input)) {
-            HIP_TRY(hipMalloc(&tmp.p, len));
-            HIP_TRY(hipMemcpyAsync(tmp.p, input, len, hipMemcpyHostToDevice, s));
-            dp = tmp.p;
+            if (d->hash_stage.bytes < len) {
+                if (d->hash_stage.p) (void)hipFree(d->hash_stage.p);  // own stream synchronised after every call
+                d->hash_stage = DevBuf{};
+                HIP_TRY(hipMalloc(&d->hash_stage.p, len));
+                d->hash_stage.bytes = len;
+            }
+            HIP_TRY(hipMemcpyAsync(d->hash_stage.p, input, len, hipMemcpyHostToDevice, s));
+            dp = d->hash_stage.p;
         }
-        uint64_t base = len ? (uint64_t)(uintptr_t)dp : 16;
+        const uint64_t base = len ? (uint64_t)(uintptr_t)dp : 16;
         rc = strided_impl(d, alg, base, len, len, 1, nullptr, seed, res, s);
         uint64_t out[2] = {0, 0};
         if (!rc) {
@@ -705,7 +627,6 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = fail(AWS_CRT_AMD_ERR_HIP, hipGetErrorString(e));
         }
-        if (tmp.p) (void)hipFree(tmp.p);
         result[0] = out[0];
         if (osz == 16) result[1] = out[1];
         return rc;
@@ -725,8 +646,6 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
             HIP_TRY(hipMemcpyAsync(d->dbuf[slot], d->pin[slot], n, hipMemcpyHostToDevice, s));
             HIP_TRY(hipEventRecord(d->pin_free[slot], s));
             const void *dseed = i == 0 ? nullptr : res + ((i - 1) & 1) * 8;
-            // data copied to dbuf[slot]: offset inside it matches src alignment mod 16? no -- dbuf is
-            // 256-aligned, so the main region is simply the aligned body of the chunk
             rc = strided_impl(d, alg, (uint64_t)(uintptr_t)d->dbuf[slot], n, n, 1, dseed, seed, res + slot * 8, s);
             if (rc) return rc;
             off += n;
@@ -741,19 +660,20 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
     return 0;
 }
 
-[[noreturn]] void die(const char *what) {
-    std::fprintf(stderr, "aws-crt-cpp_amd: %s failed: %s (no CPU fallback by design)\n", what, g_last_error.c_str());
-    std::fflush(stderr);
-    std::abort();
-}
-
-uint64_t single_or_die(int alg, const void *input, size_t len, uint64_t seed, const char *what) {
-    uint64_t r = 0;
-    if (single_impl(alg, input, len, seed, &r) != 0) die(what);
-    return r;
-}
-
 }  // namespace
+
+// ================================================================== internal (abi_single.cpp)
+extern "C" int amdcrc_gpu_usable(void) {
+    Device *d;
+    return get_device(&d) == 0 ? 1 : 0;
+}
+extern "C" int amdcrc_is_device_ptr(const void *p) { return is_device_ptr(p) ? 1 : 0; }
+extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_t seed, uint64_t *out) {
+    return single_impl(alg, input, len, seed, out);
+}
+extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n) {
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 
 // ================================================================== C ABI
 extern "C" {
@@ -767,27 +687,16 @@ AWS_CRT_AMD_API int aws_crt_amd_device_count(void) { return device_count_noinit(
 
 AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void) { return g_last_error.c_str(); }
 
-// Diagnostics (not part of the public headers): copies the per-wave timeline of the last scan
-// launched with AMDCRC_DEBUG bit 4 set -- 4 x u64 s_memrealtime stamps per wave -- after
-// synchronising the device.  Returns the number of waves written.
-AWS_CRT_AMD_API size_t aws_crt_amd_debug_timeline(unsigned long long *h_out, size_t max_waves) {
-    if (!g_timeline.d || !h_out) return 0;
-    if (hipDeviceSynchronize() != hipSuccess) return 0;
-    const size_t n = std::min(max_waves, g_timeline.waves);
-    if (hipMemcpy(h_out, g_timeline.d, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return n;
-}
-
-// Diagnostics (not part of the public headers): the next scan launched by this thread records the
-// dispatch's own start / end timestamps into these hipEvent_t (hipExtLaunchKernel), the interval a
-// kernel-trace profiler reports, without the marker packets of a hipEventRecord pair.
+// Measurement hook (not part of the public headers): the next scan launched by this thread records
+// the dispatch's own start / end timestamps into these hipEvent_t (hipExtLaunchKernel), the interval
+// a kernel-trace profiler reports, without the marker packets of a hipEventRecord pair.
 AWS_CRT_AMD_API void aws_crt_amd_debug_time_next_launch(void *start_event, void *stop_event) {
     g_time_events[0] = start_event;
     g_time_events[1] = stop_event;
 }
 
-// Diagnostics: elapsed milliseconds between two events stamped by aws_crt_amd_debug_time_next_launch
-// (torch's Event.elapsed_time refuses events it did not record itself).
+// Measurement hook: elapsed milliseconds between two events stamped by
+// aws_crt_amd_debug_time_next_launch (torch's Event.elapsed_time refuses events it did not record).
 AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_event) {
     float ms = -1.0f;
     if (hipEventSynchronize((hipEvent_t)stop_event) != hipSuccess) return -1.0f;
@@ -795,9 +704,9 @@ AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_e
     return ms;
 }
 
-// Diagnostics: one launch of the streaming-read ceiling kernel (crc_kernels.hip read_ceiling_kernel)
-// over [d_base, d_base + bytes), in the W=32 streaming scan's small-batch shape (one 512-thread
-// workgroup per CU).  Honours aws_crt_amd_debug_time_next_launch.
+// Measurement hook: one launch of the streaming-read ceiling kernel (crc_kernels.hip
+// read_ceiling_kernel) over [d_base, d_base + bytes), in the W=32 streaming scan's small-batch shape
+// (one 512-thread workgroup per CU).  Honours aws_crt_amd_debug_time_next_launch.
 AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t bytes, void *hip_stream) {
     Device *d;
     int rc = get_device(&d);
@@ -849,13 +758,17 @@ AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(const void *base, uint64_t limi
 AWS_CRT_AMD_API int aws_crt_amd_checksum_host(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                               const void *h_seeds, void *h_out) {
     if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+    if (count && (!h_ptrs || !lens || !h_out)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
     const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
+    const bool gpu = aws_crt_amd_get_dispatch() == AWS_CRT_AMD_DISPATCH_GPU;
     for (size_t i = 0; i < count; ++i) {
         uint64_t seed = 0;
         if (h_seeds) seed = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
         uint64_t r[2] = {0, 0};
-        int rc = single_impl(alg, h_ptrs[i], lens[i], seed, r);
-        if (rc) return rc;
+        if (!gpu || single_impl(alg, h_ptrs[i], lens[i], seed, r) != 0) {
+            const uint8_t *p = (const uint8_t *)h_ptrs[i];
+            (void)aws_crt_amd_cpu_batch(alg, (const void *const *)&p, &lens[i], 1, &seed, r, 1);
+        }
         if (alg == AWS_CRT_AMD_XXH3_128) {
             ((uint64_t *)h_out)[2 * i] = r[0];
             ((uint64_t *)h_out)[2 * i + 1] = r[1];
@@ -897,42 +810,6 @@ AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(int alg, const void *d_crc1, c
     return e ? fail(AWS_CRT_AMD_ERR_HIP, "combine launch failed") : 0;
 }
 
-// ---- aws-checksums single-buffer ABI (include/aws/checksums/crc.h)
-AWS_CRT_AMD_API void aws_checksums_library_init(struct aws_allocator *) { (void)aws_crt_amd_init(); }
-AWS_CRT_AMD_API void aws_checksums_library_clean_up(void) {}
-
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32_ex(const uint8_t *input, size_t length, uint32_t previous) {
-    return (uint32_t)single_or_die(ALG_CRC32, input, length, previous, "aws_checksums_crc32_ex");
-}
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32c_ex(const uint8_t *input, size_t length, uint32_t previous) {
-    return (uint32_t)single_or_die(ALG_CRC32C, input, length, previous, "aws_checksums_crc32c_ex");
-}
-AWS_CRT_AMD_API uint64_t aws_checksums_crc64nvme_ex(const uint8_t *input, size_t length, uint64_t previous) {
-    return single_or_die(ALG_CRC64NVME, input, length, previous, "aws_checksums_crc64nvme_ex");
-}
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32(const uint8_t *input, int length, uint32_t previous) {
-    return aws_checksums_crc32_ex(input, length < 0 ? 0 : (size_t)length, previous);
-}
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32c(const uint8_t *input, int length, uint32_t previous) {
-    return aws_checksums_crc32c_ex(input, length < 0 ? 0 : (size_t)length, previous);
-}
-AWS_CRT_AMD_API uint64_t aws_checksums_crc64nvme(const uint8_t *input, int length, uint64_t previous) {
-    return aws_checksums_crc64nvme_ex(input, length < 0 ? 0 : (size_t)length, previous);
-}
-
-// Combine is O(log len2) scalar GF(2) algebra on two 4/8-byte values (CRC.cpp:30-43): it carries
-// no payload bytes, so it is evaluated where it is called.  Batched combine on device:
-// aws_crt_amd_crc_combine_batch.
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
-    return (uint32_t)(gf2_mulmod(crc1, gf2_xpow8n(len2, kPoly32, 32), kPoly32, 32) ^ crc2);
-}
-AWS_CRT_AMD_API uint32_t aws_checksums_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
-    return (uint32_t)(gf2_mulmod(crc1, gf2_xpow8n(len2, kPoly32C, 32), kPoly32C, 32) ^ crc2);
-}
-AWS_CRT_AMD_API uint64_t aws_checksums_crc64nvme_combine(uint64_t crc1, uint64_t crc2, uint64_t len2) {
-    return gf2_mulmod(crc1, gf2_xpow8n(len2, kPoly64Nvme, 64), kPoly64Nvme, 64) ^ crc2;
-}
-
 // S3 multipart composition (checksums_batch.h): one batched scan over the parts, then the
 // Combine fold of the part values (4/8-byte scalars, no payload) into the full-object checksum.
 AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_parts, const size_t *lens, size_t count,
@@ -947,9 +824,19 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
     std::vector<uint64_t> part(count, 0);
     if (count) {
         const size_t osz = w / 8;
-        void *d_out = nullptr;
-        HIP_TRY(hipMalloc(&d_out, count * osz));
         hipStream_t s = (hipStream_t)hip_stream;
+        void *d_out;
+        {
+            std::lock_guard<std::mutex> g(d->mu);
+            DevBuf &ob = d->mp_out[s];
+            if (ob.bytes < count * osz) {
+                if (ob.p) d->retired.push_back(ob);
+                ob = DevBuf{};
+                HIP_TRY(hipMalloc(&ob.p, count * osz));
+                ob.bytes = count * osz;
+            }
+            d_out = ob.p;
+        }
         rc = list_impl(d, alg, d_parts, lens, count, nullptr, d_out, s);
         std::vector<uint8_t> h(count * osz);
         if (!rc && hipMemcpyAsync(h.data(), d_out, h.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -959,7 +846,6 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
         } else if (!rc) {
             rc = fail(AWS_CRT_AMD_ERR_HIP, "multipart: result copy failed");
         }
-        (void)hipFree(d_out);
         if (rc) return rc;
     }
     uint64_t obj = 0;  // CRC of zero bytes
@@ -984,14 +870,4 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
     return 0;
 }
 
-// internal: XXH64 of one buffer (host or device memory) for the xxhash ABI (xxhash.cpp)
-int aws_crt_amd_xxh64_single(const void *input, size_t len, uint64_t seed, uint64_t *out) {
-    return single_impl(AWS_CRT_AMD_XXH64, input, len, seed, out);
-}
-
 }  // extern "C"
-
-// internal: XXH3-64 / XXH3-128 of one buffer for the xxhash ABI; out = {hash} or {high, low}
-extern "C" int aws_crt_amd_xxh3_single(int bits, const void *input, size_t len, uint64_t seed, uint64_t *out) {
-    return single_impl(bits == 64 ? AWS_CRT_AMD_XXH3_64 : AWS_CRT_AMD_XXH3_128, input, len, seed, out);
-}

@@ -38,7 +38,6 @@ struct ScanParams {
     // ---- geometry and constants
     uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
     uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
-    uint32_t dbg;                  // diagnostics only (AMDCRC_DEBUG): bit0 skip tile finish, bit1 skip cross-tile combine
     uint32_t stream;               // W=32 strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel)
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
@@ -48,7 +47,6 @@ struct ScanParams {
     unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
     unsigned long long *d_acc1;    // braided scans: per tile (slot of each 32-tile group)
     unsigned int *d_cnt1;          // W=64 braided scan: per tile (arrivals of each 32-tile group)
-    unsigned long long *d_timeline; // diagnostics (AMDCRC_DEBUG bit 4): 4 s_memrealtime stamps per wave
     // ---- dynamic tile pool (W=32 braided scan, strided batches): tiles [0, nstatic) are split
     // statically over the waves; tiles [nstatic, ntiles) are claimed at run time, per shard of
     // kShardBlocks workgroups, from d_claim[2 * shard] (claims) / [2 * shard + 1] (waves done)

@@ -5,7 +5,9 @@
 #include <aws/checksums/crc.h>
 #include <aws/crt/Api.h>
 
-namespace Aws::Crt
+namespace Aws
+{
+namespace Crt
 {
     Allocator *g_allocator = nullptr;
 
@@ -53,4 +55,5 @@ namespace Aws::Crt
         return b;
     }
     void ByteBufDelete(ByteBuf &buf) { aws_byte_buf_clean_up(&buf); }
-} // namespace Aws::Crt
+} // namespace Crt
+} // namespace Aws

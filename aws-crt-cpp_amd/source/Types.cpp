@@ -6,7 +6,9 @@
  */
 #include <aws/crt/Types.h>
 
-namespace Aws::Crt
+namespace Aws
+{
+namespace Crt
 {
     namespace
     {
@@ -114,4 +116,5 @@ namespace Aws::Crt
     }
 
     Vector<uint8_t> Base64Decode(const String &decode) noexcept { return Base64Decode(ByteCursorFromString(decode)); }
-} // namespace Aws::Crt
+} // namespace Crt
+} // namespace Aws

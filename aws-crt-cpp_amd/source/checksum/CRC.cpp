@@ -6,7 +6,11 @@
 #include <aws/checksums/crc.h>
 #include <aws/crt/checksum/CRC.h>
 
-namespace Aws::Crt::Checksum
+namespace Aws
+{
+namespace Crt
+{
+namespace Checksum
 {
     uint32_t ComputeCRC32(ByteCursor input, uint32_t previousCRC32) noexcept
     {
@@ -37,4 +41,6 @@ namespace Aws::Crt::Checksum
     {
         return aws_checksums_crc64nvme_combine(crc1, crc2, len2);
     }
-} // namespace Aws::Crt::Checksum
+} // namespace Checksum
+} // namespace Crt
+} // namespace Aws

@@ -6,7 +6,11 @@
 #include <aws/crt/Api.h>
 #include <aws/crt/checksum/XXHash.h>
 
-namespace Aws::Crt::Checksum
+namespace Aws
+{
+namespace Crt
+{
+namespace Checksum
 {
     bool ComputeXXHash64(const ByteCursor &input, ByteBuf &output, uint64_t seed) noexcept
     {
@@ -65,4 +69,6 @@ namespace Aws::Crt::Checksum
         }
         return true;
     }
-} // namespace Aws::Crt::Checksum
+} // namespace Checksum
+} // namespace Crt
+} // namespace Aws

@@ -12,9 +12,12 @@
  *   aws_checksums_crc64nvme_combine <- source/checksum/CRC.cpp:42 (CombineCRC64NVME)
  *   aws_checksums_library_init / _clean_up <- source/Api.cpp:53 / :84
  *
- * `input` may be host memory (staged through the GPU) or a device address (scanned in place).
- * The *_ex functions have no error channel (CRC.h:20-51 are noexcept, value-only): if no usable
- * GPU exists the process aborts with a diagnostic rather than return a wrong value.
+ * `input` may be host memory or a device address.  Device-resident input is scanned in place by the
+ * gfx950 kernels; host input runs on the host path chosen from CPUID (AVX-512 VPCLMULQDQ /
+ * PCLMULQDQ folding, SSE4.2 crc32, tables), as aws-checksums does (CRC.h:17-19), unless
+ * aws_crt_amd_set_dispatch(AWS_CRT_AMD_DISPATCH_GPU) routes it through the GPU.  The *_ex functions
+ * have no error channel (CRC.h:20-51 are noexcept, value-only): any GPU failure, or no device at
+ * all, falls back to the host path; they never abort.
  */
 #include <stddef.h>
 #include <stdint.h>

@@ -3,7 +3,9 @@
 #include <aws/common/common.h>
 #include <aws/crt/Exports.h>
 
-namespace Aws::Crt
+namespace Aws
+{
+namespace Crt
 {
     using Allocator = aws_allocator;
 
@@ -12,4 +14,5 @@ namespace Aws::Crt
     AWS_CRT_CPP_API Allocator *DefaultAllocatorImplementation() noexcept;
     AWS_CRT_CPP_API Allocator *DefaultAllocator() noexcept;
     extern AWS_CRT_CPP_API Allocator *g_allocator;
-} // namespace Aws::Crt
+} // namespace Crt
+} // namespace Aws

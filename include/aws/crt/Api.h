@@ -8,7 +8,9 @@
 #include <aws/crt/Exports.h>
 #include <aws/crt/Types.h>
 
-namespace Aws::Crt
+namespace Aws
+{
+namespace Crt
 {
     class AWS_CRT_CPP_API ApiHandle
     {
@@ -27,4 +29,5 @@ namespace Aws::Crt
     /* last aws error raised on this thread (0 if none), reference Api.h:251 */
     AWS_CRT_CPP_API int LastError() noexcept;
     AWS_CRT_CPP_API int LastErrorOrUnknown() noexcept;
-} // namespace Aws::Crt
+} // namespace Crt
+} // namespace Aws

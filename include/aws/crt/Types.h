@@ -4,25 +4,29 @@
  * include/aws/crt/Types.h -- the ByteBuf / ByteCursor aliases (:30-31), ScopedResource (:168) and the
  * Base64 helpers that carry checksums on the S3 wire (:70-75).
  * The reference version also pulls in aws/io/socket.h and aws/mqtt/mqtt.h (:11-12), which are out
- * of scope here.  String / Vector use the standard allocator here (the
- * reference binds them to its StlAllocator, :44-48); source-level use is the same.
+ * of scope here.  String / Vector are bound to StlAllocator exactly as
+ * in the reference (:45-53), so their types and mangled names match a real aws-crt-cpp build.
+ * C++11, like the reference (CMakeLists.txt:34-36).
  */
 #include <aws/common/common.h>
 #include <aws/crt/Allocator.h>
 #include <aws/crt/Exports.h>
+#include <aws/crt/StlAllocator.h>
 
 #include <functional>
 #include <memory>
 #include <string>
 #include <vector>
 
-namespace Aws::Crt
+namespace Aws
+{
+namespace Crt
 {
     using ByteBuf = aws_byte_buf;
     using ByteCursor = aws_byte_cursor;
 
-    using String = std::string;
-    template <typename T> using Vector = std::vector<T>;
+    using String = std::basic_string<char, std::char_traits<char>, StlAllocator<char>>;
+    template <typename T> using Vector = std::vector<T, StlAllocator<T>>;
 
     template <typename T> using ScopedResource = std::unique_ptr<T, std::function<void(T *)>>;
 
@@ -42,4 +46,5 @@ namespace Aws::Crt
     AWS_CRT_CPP_API String Base64Encode(const Vector<uint8_t> &encode) noexcept;
     AWS_CRT_CPP_API String Base64Encode(ByteCursor encode) noexcept;
     AWS_CRT_CPP_API size_t Base64EncodedLength(ByteCursor encode) noexcept;
-} // namespace Aws::Crt
+} // namespace Crt
+} // namespace Aws

@@ -13,7 +13,11 @@
 #include <aws/crt/Exports.h>
 #include <aws/crt/Types.h>
 
-namespace Aws::Crt::Checksum
+namespace Aws
+{
+namespace Crt
+{
+namespace Checksum
 {
     uint32_t AWS_CRT_CPP_API ComputeCRC32(ByteCursor input, uint32_t previousCRC32 = 0) noexcept;
     uint32_t AWS_CRT_CPP_API ComputeCRC32C(ByteCursor input, uint32_t previousCRC32C = 0) noexcept;
@@ -22,4 +26,6 @@ namespace Aws::Crt::Checksum
     uint32_t AWS_CRT_CPP_API CombineCRC32(uint32_t crc1, uint32_t crc2, uint64_t len2) noexcept;
     uint32_t AWS_CRT_CPP_API CombineCRC32C(uint32_t crc1, uint32_t crc2, uint64_t len2) noexcept;
     uint64_t AWS_CRT_CPP_API CombineCRC64NVME(uint64_t crc1, uint64_t crc2, uint64_t len2) noexcept;
-} // namespace Aws::Crt::Checksum
+} // namespace Checksum
+} // namespace Crt
+} // namespace Aws

@@ -10,7 +10,11 @@
 
 struct aws_xxhash;
 
-namespace Aws::Crt::Checksum
+namespace Aws
+{
+namespace Crt
+{
+namespace Checksum
 {
     bool AWS_CRT_CPP_API ComputeXXHash64(const ByteCursor &input, ByteBuf &output, uint64_t seed = 0) noexcept;
     bool AWS_CRT_CPP_API ComputeXXHash3_64(const ByteCursor &input, ByteBuf &output, uint64_t seed = 0) noexcept;
@@ -41,4 +45,6 @@ namespace Aws::Crt::Checksum
         ScopedResource<struct aws_xxhash> m_hash;
         int m_lastError;
     };
-} // namespace Aws::Crt::Checksum
+} // namespace Checksum
+} // namespace Crt
+} // namespace Aws

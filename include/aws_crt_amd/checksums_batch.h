@@ -23,7 +23,9 @@
  * asynchronous on `hip_stream` (a hipStream_t; NULL = the legacy default stream).  Inputs must stay
  * valid until the stream reaches the work.  Every call returns 0 on success or a negative
  * aws_crt_amd_status; aws_crt_amd_last_error() describes the last failure on the calling thread.
- * There is no CPU fallback: without a usable gfx950 device every call fails.
+ * The device-pointer batch calls need a usable gfx950 device (AWS_CRT_AMD_ERR_NO_DEVICE otherwise);
+ * the host-memory calls (aws_checksums_*, aws_xxhash_*, aws_crt_amd_checksum_host,
+ * aws_crt_amd_cpu_batch) always complete, on the host path when there is no device.
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -54,6 +56,39 @@ enum aws_crt_amd_status {
     AWS_CRT_AMD_ERR_HIP = -3,
     AWS_CRT_AMD_ERR_OOM = -4,
 };
+
+/*
+ * Where the single-buffer ABI (aws_checksums_*_ex, aws_xxhash*_compute) runs host-memory input.
+ * Device-resident input always runs on the GPU.  The mode never changes the arithmetic, only the
+ * processor: AUTO (default) = host path for host memory; CPU = host path; GPU = host memory is
+ * staged through the gfx950 kernels.  A GPU failure falls back to the host path in every mode and
+ * is counted by aws_crt_amd_fallback_count().  Initial value from the environment variable
+ * AWS_CRT_AMD_DISPATCH=auto|cpu|gpu.
+ */
+enum aws_crt_amd_dispatch {
+    AWS_CRT_AMD_DISPATCH_AUTO = 0,
+    AWS_CRT_AMD_DISPATCH_CPU = 1,
+    AWS_CRT_AMD_DISPATCH_GPU = 2,
+};
+AWS_CRT_AMD_API int aws_crt_amd_set_dispatch(int mode);
+AWS_CRT_AMD_API int aws_crt_amd_get_dispatch(void);
+AWS_CRT_AMD_API unsigned long long aws_crt_amd_fallback_count(void);
+/* The host CRC tier chosen from CPUID: "avx512-vpclmulqdq", "pclmulqdq" or "slice-by-8". */
+AWS_CRT_AMD_API const char *aws_crt_amd_cpu_tier(void);
+
+/*
+ * Host path over a batch of HOST buffers, `threads` std::threads (buffers round-robin).  out: one
+ * uint64_t per buffer (CRC32/32C values zero-extended; XXH3_128: two words, high then low).
+ * seeds: uint64_t per buffer or NULL.  Needs no device.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_cpu_batch(
+    int algorithm,
+    const void *const *h_ptrs,
+    const size_t *lens,
+    size_t count,
+    const uint64_t *seeds,
+    uint64_t *out,
+    int threads);
 
 /* Bring up the engine on the current device (idempotent; called implicitly by every entry point). */
 AWS_CRT_AMD_API int aws_crt_amd_init(void);

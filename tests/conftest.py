@@ -41,9 +41,27 @@ def gpu_available() -> bool:
 
 @pytest.fixture(scope="session")
 def engine():
+    """The engine with the single-buffer ABI forced onto the GPU: host buffers passed to
+    aws_checksums_*_ex / checksum_host run through the gfx950 kernels (the dispatch mode selects the
+    processor only, never the arithmetic)."""
     import aws_crt_amd
 
     if not gpu_available():
         pytest.fail("gpu test selected but no HIP device is visible")
     aws_crt_amd.init()
+    aws_crt_amd.set_dispatch(aws_crt_amd.DISPATCH_GPU)
     return aws_crt_amd
+
+
+@pytest.fixture(autouse=True)
+def _no_silent_cpu_fallback(request):
+    """GPU tests must be served by the kernels: a GPU failure that the dispatch absorbed by falling
+    back to the host path fails the test."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import aws_crt_amd
+
+    before = aws_crt_amd.fallback_count()
+    yield
+    assert aws_crt_amd.fallback_count() == before, "a GPU call fell back to the host path"

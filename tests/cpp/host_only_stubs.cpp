@@ -1,8 +1,13 @@
-// Host-only sanitizer build of the C++ surface (tests/test_host_sanitizers.py): the Types / Api /
-// aws-c-common shim sources are compiled straight into the test binary under ASan + UBSan, without
-// the HIP engine.  Api.cpp's ApiHandle calls the engine's library init / clean-up; these two no-ops
-// stand in for them here only -- no checksum is computed in this binary.
-#include <aws/checksums/crc.h>
+// Host-only sanitizer builds (tests/test_host_sanitizers.py): the whole host side of the engine --
+// the C++ surface, the aws-c-common shim, the single-buffer ABI with its dispatch (abi_single.cpp)
+// and the host checksum path (csrc/cpu/) -- is compiled straight into the test binary under
+// ASan + UBSan or TSan.  The HIP engine is not linked: these stand-ins report "no usable device",
+// which is exactly the dispatch the host path takes on a machine without a gfx950 GPU.
+#include <stddef.h>
+#include <stdint.h>
 
-extern "C" void aws_checksums_library_init(struct aws_allocator *) {}
-extern "C" void aws_checksums_library_clean_up(void) {}
+extern "C" int amdcrc_gpu_usable(void) { return 0; }
+extern "C" int amdcrc_is_device_ptr(const void *) { return 0; }
+extern "C" int amdcrc_gpu_single(int, const void *, size_t, uint64_t, uint64_t *) { return -1; }
+extern "C" int amdcrc_copy_to_host(void *, const void *, size_t) { return -1; }
+extern "C" const char *aws_crt_amd_last_error(void) { return "no device (host-only build)"; }

@@ -4,6 +4,7 @@
 //   ./checksum_tests NAME ...   run the named tests
 #include <aws/common/common.h>
 #include <aws/testing/aws_test_harness.h>
+#include <aws_crt_amd/checksums_batch.h>
 
 #include <cstdio>
 #include <cstring>
@@ -25,5 +26,7 @@ int main(int argc, char **argv)
             ++failed;
     }
     std::printf("%d ran, %d failed\n", ran, failed);
+    // where the single-buffer ABI ran (tests/test_cpp_dropin.py checks a forced-GPU run fell back 0 times)
+    std::printf("dispatch %d, gpu fallbacks %llu\n", aws_crt_amd_get_dispatch(), aws_crt_amd_fallback_count());
     return failed ? 1 : (ran ? 0 : 2);
 }

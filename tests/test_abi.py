@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
@@ -75,7 +76,8 @@ def test_combine_scalar_abi_matches_oracle():
 
 
 def test_no_device_fails_loudly():
-    """Without a device the batch ABI returns AWS_CRT_AMD_ERR_NO_DEVICE (no silent CPU fallback)."""
+    """Without a device the device-pointer batch ABI returns AWS_CRT_AMD_ERR_NO_DEVICE (device
+    addresses cannot be read by the host path)."""
     L = ctypes.CDLL(LIB)
     if L.aws_crt_amd_device_count() > 0:
         import pytest
@@ -100,3 +102,32 @@ def test_eventstream_abi_argument_checks():
     if L.aws_crt_amd_device_count() == 0:
         rc = f(vp(0x1000), 64, vp(0x1800), 4, vp(0x2000), vp(0x3000), vp(0x4000), None)
         assert rc == -1 and b"no HIP device" in L.aws_crt_amd_last_error()
+
+
+def test_release_library_has_no_diagnostics():
+    """The shipped library carries no environment-driven diagnostics (no AMDCRC_* variables that could
+    change geometry or results) and none of the measured-and-removed kernel variants."""
+    strings = subprocess.run(["strings", "-a", LIB], capture_output=True, text=True, check=True).stdout
+    assert "AMDCRC_" not in strings
+    syms = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True, check=True).stdout
+    for gone in ("crc32_stream8_kernel", "crc64_stream_kernel<", "debug_timeline"):
+        assert gone not in syms, gone
+    # the only getenv in the product selects the processor for host memory, never the arithmetic
+    assert "AWS_CRT_AMD_DISPATCH" in strings
+
+
+def test_value_abi_never_aborts_without_device():
+    """aws_checksums_*_ex are value-only and noexcept (CRC.h:20-51): with no usable device they are
+    served by the host path (never abort, never a wrong value), even with the GPU dispatch forced."""
+    from oracle import oracle
+    code = (
+        "import ctypes,sys\n"
+        f"L=ctypes.CDLL({LIB!r})\n"
+        "f=L.aws_checksums_crc32c_ex; f.restype=ctypes.c_uint32; f.argtypes=[ctypes.c_void_p,ctypes.c_size_t,ctypes.c_uint32]\n"
+        "b=ctypes.create_string_buffer(b'123456789',9)\n"
+        "print(f(b,9,0))\n")
+    for mode in ("auto", "cpu", "gpu"):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                           env=dict(os.environ, AWS_CRT_AMD_DISPATCH=mode, HIP_VISIBLE_DEVICES="-1"))
+        assert r.returncode == 0, r.stderr
+        assert int(r.stdout.split()[-1]) == oracle.crc("crc32c", b"123456789") == 0xE3069283

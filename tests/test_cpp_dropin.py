@@ -1,10 +1,13 @@
 """The reference's own checksum test files and our C++ drop-in tests, built against the drop-in
-headers (include/aws/...) and linked to the engine library.
+headers (include/aws/..., C++11 like the reference, CMakeLists.txt:34-36) and linked to the engine
+library.
 
-CPU: compile and link -- tests/cpp/checksum_dropin_test.cpp always; the reference's
-tests/CRCTest.cpp and tests/XXHashTest.cpp unmodified when /root/reference is present (proof that
-they drop in; nothing of the reference is copied into this repo).
-GPU: run the binaries (they compute on the device through the C ABI).
+CPU suite: build and RUN them -- on a machine without a GPU the single-buffer ABI takes the host path
+(BASELINE config 1: the reference's CRCTest.cpp / XXHashTest.cpp known answers on the CPU).  The
+reference files are compiled unmodified from /root/reference when it is present; nothing of the
+reference is copied into this repo.
+GPU suite: the same binaries with AWS_CRT_AMD_DISPATCH=gpu, which routes host buffers through the
+gfx950 kernels; the driver prints the fallback count, which must be 0 (every value came from the GPU).
 """
 import os
 import subprocess
@@ -14,44 +17,60 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CPP = os.path.join(REPO, "tests", "cpp")
 REF_TESTS = "/root/reference/tests"
+REF_CASES = ("CRC32Piping", "CRC32CPiping", "CRC64NVMEPiping", "XXHash64Piping", "XXHash3_64Piping",
+             "XXHash3_128Piping")
 
 
 def _make(*extra):
     subprocess.run(["make", "-s", "-C", CPP, *extra], check=True, capture_output=True, text=True)
 
 
-def test_dropin_tests_build():
+def _run(name, env_extra=None):
+    exe = os.path.join(CPP, "build", name)
+    env = dict(os.environ, **(env_extra or {}))
+    return subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+
+
+def test_dropin_tests_build_and_run_cpu():
     _make()
-    assert os.path.exists(os.path.join(CPP, "build", "checksum_tests"))
+    r = _run("checksum_tests", {"AWS_CRT_AMD_DISPATCH": "cpu"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "6 ran, 0 failed" in r.stdout, r.stdout
 
 
 @pytest.mark.skipif(not os.path.isdir(REF_TESTS), reason="reference checkout not mounted")
-def test_reference_test_files_compile_unmodified():
+def test_reference_test_files_compile_unmodified_and_pass_on_cpu():
+    """BASELINE config 1 plumbing: tests/CRCTest.cpp + tests/XXHashTest.cpp of the reference,
+    unmodified, C++11, every known answer computed by the engine's host path."""
     _make(f"REF_TESTS={REF_TESTS}")
-    assert os.path.exists(os.path.join(CPP, "build", "reference_tests"))
+    r = _run("reference_tests", {"AWS_CRT_AMD_DISPATCH": "cpu"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in REF_CASES:
+        assert f"[PASS] {name}" in r.stdout, r.stdout
 
 
 @pytest.mark.gpu
-def test_dropin_tests_run(engine):
+def test_dropin_tests_run_on_gpu(engine):
     _make()
-    r = subprocess.run([os.path.join(CPP, "build", "checksum_tests")], capture_output=True, text=True, timeout=300)
+    r = _run("checksum_tests", {"AWS_CRT_AMD_DISPATCH": "gpu"})
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "0 failed" in r.stdout
+    assert "6 ran, 0 failed" in r.stdout
+    assert "dispatch 2, gpu fallbacks 0" in r.stdout, r.stdout
 
 
 @pytest.mark.gpu
 def test_reference_test_files_run_on_gpu(engine):
-    """tests/CRCTest.cpp + tests/XXHashTest.cpp of the reference, compiled unmodified in the build
-    container (test_reference_test_files_compile_unmodified) and shipped as a binary: every
-    CRC32/CRC32C/CRC64NVME/XXH64/XXH3 known answer computed by the gfx950 engine."""
+    """The reference's CRCTest.cpp / XXHashTest.cpp (compiled unmodified in the build container and
+    shipped as a binary) with the host buffers routed through the gfx950 kernels: every
+    CRC32/CRC32C/CRC64NVME/XXH64/XXH3 known answer computed on the GPU, zero fallbacks."""
     exe = os.path.join(CPP, "build", "reference_tests")
     if not os.path.exists(exe):
         pytest.skip("reference_tests binary not built (needs the reference checkout at build time)")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    r = _run("reference_tests", {"AWS_CRT_AMD_DISPATCH": "gpu"})
     assert r.returncode == 0, r.stdout + r.stderr
-    for name in ("CRC32Piping", "CRC32CPiping", "CRC64NVMEPiping", "XXHash64Piping", "XXHash3_64Piping",
-                 "XXHash3_128Piping"):
+    for name in REF_CASES:
         assert f"[PASS] {name}" in r.stdout, r.stdout
+    assert "dispatch 2, gpu fallbacks 0" in r.stdout, r.stdout
 
 
 def test_types_base64_cpu():
@@ -59,6 +78,6 @@ def test_types_base64_cpu():
     (tests/TypesTest.cpp:17-31), RFC 4648 vectors, S3 wire forms of the CRC check values and
     malformed inputs.  Host code; no device needed."""
     _make()
-    r = subprocess.run([os.path.join(CPP, "build", "types_tests")], capture_output=True, text=True, timeout=60)
+    r = _run("types_tests")
     assert r.returncode == 0, r.stdout + r.stderr
     assert "4 ran, 0 failed" in r.stdout, r.stdout
