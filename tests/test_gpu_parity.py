@@ -242,31 +242,31 @@ def test_fuzz_strided_shapes(engine, alg):
         assert engine.as_unsigned(out) == want, (L, count, off, stride)
 
 
-@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
-def test_config3_chunked_running_crc(engine, alg):
-    """BASELINE config 3 shape (256 MiB buffers, 8 MiB chunks): one-shot == chained == combine."""
+def test_config3_full_chunked_running_crc(engine):
+    """BASELINE config 3 at full size: 16 x 256 MiB, CRC32 and CRC32C.  One-shot == chained running
+    CRC over 8 MiB chunks (seeded on device) == Combine of the chunk CRCs, and the oracle on all 16."""
     import torch
 
-    L, chunk, nbuf = 256 << 20, 8 << 20, 2
+    L, chunk, nbuf = 256 << 20, 8 << 20, 16
     d = dev_random(L * nbuf, 9)
-    one = engine.as_unsigned(engine.checksum_strided(ALG[alg], d, L, L, nbuf))
-    # chained: chunk c of every buffer seeded on device with chunk c-1's result
-    prev = None
-    parts = []
-    for c in range(L // chunk):
-        prev = engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, seeds=prev, base_offset=c * chunk)
-        parts.append(engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, base_offset=c * chunk))
-    torch.cuda.synchronize()
-    chained = engine.as_unsigned(prev)
-    assert chained == one
-    for b in range(nbuf):
-        acc = engine.as_unsigned(parts[0])[b]
-        for p in parts[1:]:
-            acc = engine.combine(alg, acc, engine.as_unsigned(p)[b], chunk)
-        assert acc == one[b]
     h = host_bytes(d)
-    want = [oracle.crc(alg, h[b * L:(b + 1) * L]) for b in range(nbuf)]
-    assert one == want
+    for alg in ("crc32", "crc32c"):
+        one = engine.as_unsigned(engine.checksum_strided(ALG[alg], d, L, L, nbuf))
+        prev = None
+        parts = []
+        for c in range(L // chunk):
+            prev = engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, seeds=prev, base_offset=c * chunk)
+            parts.append(engine.checksum_strided(ALG[alg], d, L, chunk, nbuf, base_offset=c * chunk))
+        torch.cuda.synchronize()
+        assert engine.as_unsigned(prev) == one
+        pv = [engine.as_unsigned(p) for p in parts]
+        for b in range(nbuf):
+            acc = pv[0][b]
+            for p in pv[1:]:
+                acc = engine.combine(alg, acc, p[b], chunk)
+            assert acc == one[b]
+        want = oracle.batch(alg, [h.ctypes.data + b * L for b in range(nbuf)], [L] * nbuf, 16)
+        assert one == want, alg
 
 
 def test_combine_batch_device(engine):
@@ -312,27 +312,37 @@ def test_repeat_and_concurrent_streams(engine):
         assert engine.as_unsigned(o) == want
 
 
-def test_config4_shape_one_shard(engine):
-    """BASELINE config 4 per-GPU shard at reduced count: 8 KiB parts, round-robin shard 0 of 8."""
+def test_config4_full_shard(engine):
+    """BASELINE config 4's per-GPU shard at full size: 1M x 8 KiB round-robin over 8 GPUs leaves
+    131072 x 8 KiB (1 GiB) on each; the batch is checked buffer by buffer against the oracle (CRC32C),
+    and a CRC64NVME pass (S3's default algorithm) on the same shard."""
     import torch
 
-    total, L, G = 16384, 8192, 8
-    d = dev_random((total // G) * L, 13)
-    out = engine.checksum_strided(ALG["crc32c"], d, L, L, total // G)
+    total, L, G = 1 << 20, 8192, 8
+    n = total // G
+    d = dev_random(n * L, 13)
+    out = engine.checksum_strided(ALG["crc32c"], d, L, L, n)
+    out64 = engine.checksum_strided(ALG["crc64nvme"], d, L, L, n)
     torch.cuda.synchronize()
     h = host_bytes(d)
-    want = oracle.batch("crc32c", [h.ctypes.data + i * L for i in range(total // G)], [L] * (total // G), 8)
-    assert engine.as_unsigned(out) == want
+    ptrs = [h.ctypes.data + i * L for i in range(n)]
+    assert engine.as_unsigned(out) == oracle.batch("crc32c", ptrs, [L] * n, 16)
+    assert engine.as_unsigned(out64) == oracle.batch("crc64nvme", ptrs, [L] * n, 16)
 
 
-def test_config5_crc64_xxh64_64mib(engine):
+def test_config5_crc64_xxh64_8x64mib(engine):
+    """BASELINE config 5: a batch of 8 x 64 MiB buffers, CRC64NVME and XXH64 (and XXH3-64 on the
+    split path), against the oracle on all 8."""
     import torch
 
-    L, n = 64 << 20, 2
+    L, n = 64 << 20, 8
     d = dev_random(L * n, 14)
     crc = engine.as_unsigned(engine.checksum_strided(ALG["crc64nvme"], d, L, L, n))
     xx = engine.as_unsigned(engine.checksum_strided(ALG["xxh64"], d, L, L, n))
+    x3 = engine.as_unsigned(engine.checksum_strided(ALG["xxh3_64"], d, L, L, n))
     torch.cuda.synchronize()
     h = host_bytes(d)
-    assert crc == [oracle.crc("crc64nvme", h[i * L:(i + 1) * L]) for i in range(n)]
-    assert xx == [oracle.xxh64(h[i * L:(i + 1) * L]) for i in range(n)]
+    ptrs = [h.ctypes.data + i * L for i in range(n)]
+    assert crc == oracle.batch("crc64nvme", ptrs, [L] * n, 8)
+    assert xx == oracle.batch("xxh64", ptrs, [L] * n, 8)
+    assert x3 == [oracle.xxh3_64(h[i * L:(i + 1) * L]) for i in range(n)]
