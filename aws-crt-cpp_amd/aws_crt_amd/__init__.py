@@ -165,6 +165,25 @@ def checksum_strided(alg: int, base, stride: int, length: int, count: int, seeds
     return out
 
 
+class _Batch(ctypes.Structure):
+    _fields_ = [("d_base", ctypes.c_void_p), ("d_seeds", ctypes.c_void_p), ("d_out", ctypes.c_void_p)]
+
+
+def checksum_batches(alg: int, batches, stride: int, length: int, count: int, stream=None) -> None:
+    """Several uniform batches of one shape, each (base address, seeds tensor or None, out tensor),
+    coalesced into as few launches as the engine allows (aws_crt_amd_checksum_batches)."""
+    n = len(batches)
+    arr = (_Batch * max(n, 1))()
+    for i, (base, seeds, out) in enumerate(batches):
+        arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+        arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
+        arr[i].d_out = out.data_ptr()
+    L = lib()
+    L.aws_crt_amd_checksum_batches.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+    _check(L.aws_crt_amd_checksum_batches(alg, arr, n, stride, length, count, _stream_handle(stream)))
+
+
 def checksum_list(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, out=None, stream=None, device=None):
     """Ragged batch of device buffers given by raw device addresses and lengths (host lists)."""
     import torch

@@ -100,6 +100,20 @@ struct Walker {  // list mode: running position in the tile prefix
     uint64_t b, lo, hi;
 };
 
+// strided launches: batch j and index i of buffer b (wave-uniform; the division runs on the scalar
+// unit, once per buffer at its head and at its finish)
+struct BatchPos {
+    uint64_t j, i;
+};
+__device__ __forceinline__ BatchPos batch_pos(const ScanParams &p, uint64_t b) {
+    if (p.nbatch <= 1) return {0, b};
+    const uint64_t j = b / p.bcount;
+    return {j, b - j * p.bcount};
+}
+// the kernel-argument arrays, indexed with a wave-uniform j (ordinary reads of the kernarg segment:
+// the compiler emits scalar loads; the build checks that no kernel uses scratch)
+__device__ __forceinline__ uint64_t karg64(const uint64_t *a, uint64_t j) { return a[j]; }
+
 template <bool LIST>
 __device__ __forceinline__ Edges buffer_edges(const ScanParams &p, uint64_t b) {
     uint64_t ptr, n;
@@ -107,7 +121,8 @@ __device__ __forceinline__ Edges buffer_edges(const ScanParams &p, uint64_t b) {
         ptr = sload64(p.d_ptrs + b);
         n = sload64(p.d_lens + b);
     } else {
-        ptr = p.base + b * p.stride;
+        const BatchPos bp = batch_pos(p, b);
+        ptr = karg64(p.bbase, bp.j) + bp.i * p.stride;
         n = p.len;
     }
     const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
@@ -166,8 +181,15 @@ template <bool LIST, class E>
 __device__ __forceinline__ typename E::T head_state(const ScanParams &p, uint64_t b, const E &eng) {
     using T = typename E::T;
     uint64_t seed = p.seed_all;
-    if (p.d_seeds)
-        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)p.d_seeds + b) : sload64((const uint64_t *)p.d_seeds + b);
+    const void *seeds = p.d_seeds;
+    uint64_t si = b;
+    if (!LIST) {
+        const BatchPos bp = batch_pos(p, b);
+        seeds = (const void *)karg64(p.bseed, bp.j);
+        si = bp.i;
+    }
+    if (seeds)
+        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)seeds + si) : sload64((const uint64_t *)seeds + si);
     T s = (T)~seed;
     const Edges e = buffer_edges<LIST>(p, b);
     if (e.headend > e.ptr) s = fold_bytes(s, e.ptr, e.headend, eng);
@@ -180,12 +202,19 @@ __device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typena
     const Edges e = buffer_edges<LIST>(p, b);
     if (e.end > e.tail) fin = fold_bytes(fin, e.tail, e.end, eng);
     fin = ~fin;
+    void *out = p.d_out;
+    uint64_t oi = b;
+    if (!LIST) {
+        const BatchPos bp = batch_pos(p, b);
+        out = (void *)karg64(p.bout, bp.j);
+        oi = bp.i;
+    }
     // result stores are inline asm: a compiler-visible store inside a scan loop makes the loop-header
     // merge of the compiler's wait counts pessimistic (it then drains the payload ring early)
     if (E::W == 32)
-        asm volatile("global_store_dword %0, %1, off" : : "v"((uint32_t *)p.d_out + b), "v"((uint32_t)fin) : "memory");
+        asm volatile("global_store_dword %0, %1, off" : : "v"((uint32_t *)out + oi), "v"((uint32_t)fin) : "memory");
     else
-        asm volatile("global_store_dwordx2 %0, %1, off" : : "v"((uint64_t *)p.d_out + b), "v"((uint64_t)fin) : "memory");
+        asm volatile("global_store_dwordx2 %0, %1, off" : : "v"((uint64_t *)out + oi), "v"((uint64_t)fin) : "memory");
 }
 
 // r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time
@@ -922,13 +951,16 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     const uint32_t gsh = __builtin_ctz(G);
     const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
     const bool work = t0 < t1;
-    // prefetch cursor: the next group to issue, as (buffer, tile, group) and its address
+    // prefetch cursor: the next group to issue, as (buffer, tile, group); fbuf is the main-region
+    // address of buffer fb, which walks batch by batch (fj, fi)
     uint32_t fq = 0;  // groups issued
     uint64_t fb = t0 / T, fk = t0 - fb * T;
     uint32_t fg = 0;
+    BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
+    uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
-        uint64_t a = fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
-        if (!AMDCRC_GUARD_OK(fq >= nq || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
+        uint64_t a = fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
+        if (!AMDCRC_GUARD_OK(fq >= nq || p.nbatch > 1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
                                                                  p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
                              1, a))
             a = dummy;
@@ -938,7 +970,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         ++fq;
         if (++fg == G) {
             fg = 0;
-            if (++fk == T) fk = 0, ++fb;
+            if (++fk == T) {
+                fk = 0, ++fb;
+                if (++fpos.i == p.bcount && fq < nq) {
+                    fpos.i = 0, ++fpos.j;
+                    fbuf = karg64(p.bbase, fpos.j) + hoff;
+                } else {
+                    fbuf += p.stride;
+                }
+            }
         }
     };
     // K-image word and P columns of this thread, published to LDS after the first scan step (ordinary
@@ -1515,15 +1555,24 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc64_stream4_kernel(const Sca
     uint32_t fq = 0;  // groups issued
     uint64_t fb = t0 / T, fk = t0 - fb * T;
     uint32_t fg = 0;
+    BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
+    uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
-        return rfl64(fq < nq ? p.base + fb * p.stride + hoff + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup)
-                             : dummy);
+        return rfl64(fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup) : dummy);
     };
     auto f_next = [&]() {
         ++fq;
         if (++fg == G) {
             fg = 0;
-            if (++fk == T) fk = 0, ++fb;
+            if (++fk == T) {
+                fk = 0, ++fb;
+                if (++fpos.i == p.bcount && fq < nq) {
+                    fpos.i = 0, ++fpos.j;
+                    fbuf = karg64(p.bbase, fpos.j) + hoff;
+                } else {
+                    fbuf += p.stride;
+                }
+            }
         }
     };
     const uint64_t kl = *(gu64 *)(p.d_kvals + lane);

@@ -356,11 +356,25 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     return 0;
 }
 
+// One uniform batch of a strided launch
+struct Batch {
+    uint64_t base;
+    const void *seeds;
+    void *out;
+};
+
+int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, size_t len, size_t count, uint64_t seed_all,
+                 hipStream_t s);
+
 int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, size_t count, const void *d_seeds,
                  uint64_t seed_all, void *d_out, hipStream_t s) {
     if (count == 0) return 0;
     if (!d_out || (len && !base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
-    if (is_hash(alg)) {
+    if (!is_hash(alg)) {
+        const Batch b{base, d_seeds, d_out};
+        return scan_batches(d, alg, &b, 1, stride, len, count, seed_all, s);
+    }
+    {
         XxhParams xp{};
         xp.base = base;
         xp.stride = stride;
@@ -390,11 +404,27 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         }
         return launch_hash(alg, xp, s);
     }
+}
+
+// CRC scan of nb uniform batches (same stride / len / count; bases of one alignment mod 16) in one
+// launch: buffer b of the launch is buffer b % count of batch b / count (ScanParams::bbase etc.)
+int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, size_t len, size_t count, uint64_t seed_all,
+                 hipStream_t s) {
     if (count > 1 && (stride % 16) != 0)
         return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
+    if (nb == 0 || nb > (size_t)kMaxBatches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad batch count");
     std::lock_guard<std::mutex> g(d->mu);
+    const uint64_t base = bs[0].base;
     const uint64_t ml = main_len(base, len);
     ScanParams p{};
+    p.nbatch = (uint32_t)nb;
+    p.bcount = count;
+    for (size_t j = 0; j < nb; ++j) {
+        p.bbase[j] = bs[j].base;
+        p.bout[j] = (uint64_t)(uintptr_t)bs[j].out;
+        p.bseed[j] = (uint64_t)(uintptr_t)bs[j].seeds;
+    }
+    count *= nb;  // buffers of the launch
     // Batches whose main regions are whole tiles take the streaming scans (crc32_stream_kernel,
     // crc64_stream4_kernel), tiles sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C
     // measured 5250-5315 GiB/s with one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
@@ -422,9 +452,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     p.tiles_per_buf = T;
     p.nbuf = count;
     p.ntiles = T * count;
-    p.d_seeds = d_seeds;
     p.seed_all = seed_all;
-    p.d_out = d_out;
     p.stream = stream && ml % tile == 0 ? 1u : 0u;
     if (pool && !p.stream) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
@@ -549,6 +577,8 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     ScanParams p{};
     p.seg = seg;
     p.list_mode = 1;
+    p.nbatch = 1;
+    p.bcount = count;
     p.d_ptrs = dd;
     p.d_lens = dd + count;
     p.d_tile_prefix = dd + 2 * count;
@@ -729,6 +759,38 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, si
     if (rc) return rc;
     if (count == 1) stride = len;
     return strided_impl(d, alg, (uint64_t)(uintptr_t)d_base, stride, len, count, d_seeds, 0, d_out, (hipStream_t)hip_stream);
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(int alg, const struct aws_crt_amd_batch *batches, size_t nbatches,
+                                                 size_t stride, size_t len, size_t count, void *hip_stream) {
+    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+    if (nbatches && !batches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null batches");
+    Device *d;
+    int rc = get_device(&d);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (count == 1) stride = len;
+    for (size_t j = 0; j < nbatches; ++j)
+        if (!batches[j].d_out || (len && !batches[j].d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
+    if (count == 0 || nbatches == 0) return 0;
+    if (is_hash(alg)) {  // the hash kernels run one launch per batch
+        for (size_t j = 0; j < nbatches && !rc; ++j)
+            rc = strided_impl(d, alg, (uint64_t)(uintptr_t)batches[j].d_base, stride, len, count, batches[j].d_seeds, 0,
+                              batches[j].d_out, s);
+        return rc;
+    }
+    // one launch per run of up to kMaxBatches batches whose bases share their alignment mod 16
+    std::vector<Batch> run;
+    for (size_t j = 0; j <= nbatches && !rc; ++j) {
+        const bool flush = j == nbatches || run.size() == (size_t)kMaxBatches ||
+                           (!run.empty() && ((uint64_t)(uintptr_t)batches[j].d_base & 15) != (run[0].base & 15));
+        if (flush && !run.empty()) {
+            rc = scan_batches(d, alg, run.data(), run.size(), stride, len, count, 0, s);
+            run.clear();
+        }
+        if (j < nbatches) run.push_back({(uint64_t)(uintptr_t)batches[j].d_base, batches[j].d_seeds, batches[j].d_out});
+    }
+    return rc;
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,

@@ -19,6 +19,8 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kGroupBytes = 64;  // bytes per lane per prefetch group (4 x 16-byte loads)
 constexpr int kVecPerGroup = kGroupBytes / 16;
 
+constexpr int kMaxBatches = 16;  // batches per strided launch (kernel arguments, SMEM-loaded)
+
 struct ScanParams {
     // ---- batch description: strided (base != 0) or list (d_ptrs != 0)
     uint64_t base;                 // strided: device address of buffer 0
@@ -47,6 +49,13 @@ struct ScanParams {
     unsigned int *d_cnt;           // per buffer (used when T > 32 or W = 64)
     unsigned long long *d_acc1;    // braided scans: per tile (slot of each 32-tile group)
     unsigned int *d_cnt1;          // W=64 braided scan: per tile (arrivals of each 32-tile group)
+    // ---- strided launches over several batches (aws_crt_amd_checksum_batches): buffer b is buffer
+    // i = b % bcount of batch j = b / bcount, at bbase[j] + i * stride, seed bseed[j][i] (bseed[j] == 0:
+    // seed_all), result bout[j][i].  A plain strided launch is nbatch = 1.  All bases share their
+    // alignment mod 16 (the host splits the launch otherwise).
+    uint32_t nbatch;
+    uint64_t bcount;
+    uint64_t bbase[kMaxBatches], bout[kMaxBatches], bseed[kMaxBatches];
     // ---- dynamic tile pool (W=32 braided scan, strided batches): tiles [0, nstatic) are split
     // statically over the waves; tiles [nstatic, ntiles) are claimed at run time, per shard of
     // kShardBlocks workgroups, from d_claim[2 * shard] (claims) / [2 * shard + 1] (waves done)

@@ -1,43 +1,47 @@
 #!/usr/bin/env python3
-"""Headline benchmark: GiB/s of CRC32C over device-resident buffers (BASELINE.json `metric`),
-on BASELINE.json configs[1]: batches of 1024 x 64 KiB independent buffers per GPU.
+"""Headline benchmark: GiB/s of CRC32C over device-resident buffers (BASELINE.json `metric`), on
+BASELINE.json configs[1] (C2): batches of 1024 x 64 KiB independent buffers per GPU.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU)
 
-A step = one launch of the batched CRC32C scan over one 64 MiB batch already resident in HBM.
-Each rank scans its own batches (buffers shard across GPUs with no collective: weak scaling).
-Steps rotate over --batches distinct batches (default 8 = 512 MiB per GPU, twice the 256 MiB
-Infinity Cache) so every launch streams from HBM, not from the on-die cache.
+A step = one C2 batch (1024 x 64 KiB, its own base and its own 1024 results) checksummed on the GPU,
+inputs already resident in HBM.  Each rank scans its own batches (buffers shard across GPUs with no
+collective: weak scaling).  Steps rotate over --batches distinct batches (8 = 512 MiB per GPU, twice
+the 256 MiB Infinity Cache) so every launch streams from HBM.
 
-Timed region: K eager launches, alternating over --branches HIP streams so that a launch's
-workgroups start on CUs as the previous launch's workgroups retire (its prologue overlaps the other
-launch.s tail; 3 streams by default).  --mode graph replays a captured HIP graph instead (one
-launch per batch, batches split over graph branches; measured slower on ROCm 7.2: every replay
-starts with a ~20 us bubble).  Kernel duration for the roofline: a separate pass queues
---timing-launches eager launches on one stream behind a GPU-side hold; each launch stamps HIP
-events with its own dispatch start / end (hipExtLaunchKernel through the engine's diagnostics
-hook), the interval rocprofv3's kernel trace reports for the same dispatches.
+Launches: steps are submitted through aws_crt_amd_checksum_batches, which puts up to --coalesce
+queued batches (same shape, separate bases / results) into ONE launch, so back-to-back batches do
+not each pay a launch's ramp and tail (DESIGN.md §3 "multi-batch launches"); the K steps are split
+into ceil(K / coalesce) near-equal launches, alternating over --branches HIP streams.  --coalesce 1 is
+one launch per batch.
 
-End-to-end (PCIe-inclusive): the same batches start in pinned host memory; H2D copies
-on a copy stream overlap the scans on a compute stream through a 3-slot device ring, results come
-back D2H.  Reported as `e2e_pinned` next to `value`, never as `value`.
+Roofline (`roofline`): the dominant kernel's algorithmic bytes per launch (1 byte read per payload
+byte) / its mean dispatch duration, from HIP events stamped by the dispatch itself
+(hipExtLaunchKernel via the engine's measurement hook) over --timing-launches launches serialised on
+one stream -- the interval rocprofv3's kernel trace reports.  `single_batch` gives the same figures
+for one-batch launches.  `traffic` is HBM bytes per launch from the committed rocprofv3 --pmc pass
+named in `traffic_source` (not measured in this run).
 
-North-star shape (`target_shape`, rank 0 at N=1): BASELINE.json's target, CRC32C over batches of
-16 x 64 MiB device-resident buffers (>= 80 % of HBM peak), measured the same two ways; reported
-beside `value`, never as `value`.  The profiling passes run with --target-buffers 0.
+Config legs (rank 0, N = 1; `configs`): C3 (16 x 256 MiB, CRC32 and CRC32C), C5 (8 x 64 MiB,
+CRC64NVME and XXH64) and the north-star target shape (16 x 64 MiB CRC32C), each with value, kernel
+duration, roofline and cpu_baseline.  Never `value`.
 
-Prints one JSON line (rank 0).  `roofline.achieved` = algorithmic bytes per launch (1 byte read per
-payload byte) / mean kernel duration from HIP events recorded on the launch stream.
-`roofline.read_ceiling` = the same two measurements for a read-only XOR-reduce kernel of the same
-launch shape over the same batches (the achievable streaming read for this bytes-per-launch).
-`cpu_baseline` = the oracle's SSE4.2 crc32q 3-way path (the technique class of aws-checksums)
-timed on this host over a bounded sample, rank 0 at N=1 only.
+CPU baseline (`cpu_baseline`): the engine's own host path (csrc/cpu/: AVX-512
+VPCLMULQDQ / PCLMULQDQ folding, SSE4.2 crc32, vectorised XXH3 -- aws-checksums' technique class;
+aws-checksums itself cannot be built here) over a bounded sample of the same buffers, 1 thread and
+the box's CPU share (std::threads, buffers round-robin), median of >= 5 reps, CPU model stated,
+results checked against the GPU's.  The oracle's hw tier is reported beside it.
+
+End-to-end (`e2e_pinned`): the same batches start in pinned host memory; H2D copies on
+a copy stream overlap the scans through a 3-slot device ring, results come back D2H.  Never `value`.
+
+Prints one JSON line (rank 0).
 """
 import argparse
 import json
-import math
 import os
+import statistics
 import sys
 import time
 
@@ -47,6 +51,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md chip table
 ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
+WIDE = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
 
 
 def parse():
@@ -58,47 +63,151 @@ def parse():
     ap.add_argument("--buffers", type=int, default=1024)
     ap.add_argument("--buffer-bytes", type=int, default=65536)
     ap.add_argument("--batches", type=int, default=8)
+    ap.add_argument("--coalesce", type=int, default=8, help="queued batches per launch (1..16)")
     ap.add_argument("--branches", type=int, default=3)
-    ap.add_argument("--mode", default="eager", choices=["graph", "eager"])
-    ap.add_argument("--timing-launches", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--timing-launches", type=int, default=32)
+    ap.add_argument("--cpu-seconds", type=float, default=1.0, help="per CPU-baseline rep")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-read-ceiling", action="store_true", help="skip the streaming-read ceiling kernel")
+    ap.add_argument("--no-read-ceiling", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C3 / C5 / target-shape legs")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
-    ap.add_argument("--target-buffers", type=int, default=16,
-                    help="north-star shape leg: batches of this many 64 MiB buffers (0: skip)")
     return ap.parse_args()
 
 
-def cpu_baseline(alg, host_batch, count, L, gpu_results, seconds, threads):
-    """Oracle (kind "port") on a bounded sample: one batch, repeated passes for ~`seconds`."""
-    from oracle import oracle
+def cpu_share():
+    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, set by the pool) capped by
+    the affinity mask; the model and the machine's logical CPU count are reported beside it."""
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, share) if share > 0 else aff
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return threads, model, aff
 
-    base = host_batch.ctypes.data
+
+def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
+    """Engine host path (kind "port") on a bounded sample: `count` buffers of L bytes from `host`
+    (numpy), 1 thread and the box's CPU share, median of `reps` reps of >= rep_seconds each."""
+    from oracle import oracle  # checker and secondary figure only
+
+    threads, model, aff = cpu_share()
+    base = host.ctypes.data
     ptrs = [base + i * L for i in range(count)]
     lens = [L] * count
-    first = oracle.batch(alg, ptrs, lens, threads)
-    parity = first == gpu_results
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        oracle.batch(alg, ptrs, lens, threads)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    rate = passes * count * L / el / 2**30
-    # single-thread rate on a smaller slice, for reference
-    t1, n1 = time.perf_counter(), 0
-    while time.perf_counter() - t1 < min(2.0, seconds / 5):
-        oracle.batch(alg, ptrs[:64], lens[:64], 1)
-        n1 += 1
-    rate1 = n1 * 64 * L / (time.perf_counter() - t1) / 2**30
-    return {"value": round(rate, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} passes over one {count} x {L // 1024} KiB batch ({count * L >> 20} MiB) "
-                      f"copied to host, {threads} threads, oracle SSE4.2 crc32q 3-way "
-                      f"({'PCLMUL fold' if alg != 'crc32c' else 'crc32q'}) tier",
-            "single_thread_gibs": round(rate1, 3), "parity_with_gpu": parity}
+    first = eng.cpu_batch(ALG[alg], ptrs, lens, threads=threads)
+    parity = first == gpu_results[:count]
+
+    def rate(fn, nbytes):
+        fn()  # warm-up
+        rs = []
+        for _ in range(reps):
+            passes, t0 = 0, time.perf_counter()
+            while True:
+                fn()
+                passes += 1
+                el = time.perf_counter() - t0
+                if el >= rep_seconds:
+                    break
+            rs.append(passes * nbytes / el / 2**30)
+        return statistics.median(rs)
+
+    n1 = max(1, min(count, (64 << 20) // L))
+    v = rate(lambda: eng.cpu_batch(ALG[alg], ptrs, lens, threads=threads), count * L)
+    v1 = rate(lambda: eng.cpu_batch(ALG[alg], ptrs[:n1], lens[:n1], threads=1), n1 * L)
+    ov = None
+    if alg in oracle.ALG_INDEX:
+        ov = rate(lambda: oracle.batch(alg, ptrs, lens, threads), count * L)
+    return {"value": round(v, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "impl": f"engine host path ({eng.cpu_tier()} tier)",
+            "sample": f"{count} x {L >> 10} KiB ({count * L >> 20} MiB) copied to host, median of {reps} reps "
+                      f"of >= {rep_seconds:g} s, {threads} std::threads round-robin",
+            "single_thread_gibs": round(v1, 2), "cpu_model": model, "logical_cpus_visible": aff,
+            "oracle_hw_tier_gibs": round(ov, 2) if ov is not None else None, "parity_with_gpu": parity}
+
+
+def time_launches(eng, launch, st, nt):
+    """Mean dispatch duration (ms) of nt launches serialised on stream st behind a GPU-side hold."""
+    import torch
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(int(40e6))
+    for i in range(nt):
+        starts[i].record(st)  # creates the events; the launch below re-stamps them
+        ends[i].record(st)
+        eng.time_next_launch(starts[i], ends[i])
+        launch(i, st)
+    torch.cuda.synchronize()
+    durs = sorted(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends))
+    return sum(durs) / nt, durs[nt // 2]
+
+
+def roofline(bytes_per_launch, kernel_ms, kernel_name):
+    ach = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": kernel_name, "kernel_ms": round(kernel_ms, 5),
+            "bytes_per_launch": bytes_per_launch}
+
+
+def split(k, g):
+    """k steps into ceil(k / g) near-equal consecutive launches"""
+    n = max(1, -(-k // max(1, g)))
+    return [k * i // n for i in range(n + 1)]
+
+
+KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc64nvme": "crc64_stream4_kernel",
+          "xxh64": "xxh64_quad_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
+
+
+def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=4,
+               cpu_seconds=0.5, do_cpu=True):
+    """One BASELINE config: `steps` steps of `nbuf` x L bytes (nb rotating batches), pipelined over
+    the streams; roofline from `timing` serialised launches; CPU baseline on `cpu_bufs` buffers."""
+    import torch
+
+    step_bytes = nbuf * L
+    g = torch.Generator(device=dev)
+    g.manual_seed(hash(name) & 0xFFFF)
+    data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
+    odt = torch.int64 if alg in WIDE else torch.int32
+    outs = [torch.empty(nbuf, dtype=odt, device=dev) for _ in range(nb)]
+
+    def launch_group(i0, i1, st):
+        eng.checksum_batches(ALG[alg], [(data.data_ptr() + (i % nb) * step_bytes, None, outs[i % nb]) for i in range(i0, i1)],
+                             L, L, nbuf, stream=st)
+
+    cuts = split(steps, coalesce)
+    for j in range(len(cuts) - 1):
+        launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(len(cuts) - 1):
+        launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    per = cuts[1] - cuts[0]
+    kms, _ = time_launches(eng, lambda i, st: launch_group(i * per, i * per + per, st), streams[0], timing)
+    gibs = steps * step_bytes / el / 2**30
+    rec = {"workload": f"{name}: {nbuf} x {L >> 20 if L >= 1 << 20 else L >> 10} {'MiB' if L >= 1 << 20 else 'KiB'} "
+                       f"{alg.upper()}, device-resident, {nb} rotating batches, {per} per launch",
+           "value": round(gibs, 2), "unit": "GiB/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
+           "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
+           "roofline": roofline(per * step_bytes, kms, KERNEL.get(alg, alg))}
+    if do_cpu:
+        torch.cuda.synchronize()
+        gpu0 = eng.as_unsigned(outs[0])
+        host = data[: cpu_bufs * L].cpu().numpy()
+        rec["cpu_baseline"] = cpu_baseline(eng, alg, host, cpu_bufs, L, gpu0, cpu_seconds)
+    del data
+    torch.cuda.empty_cache()
+    return rec
 
 
 def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
@@ -110,9 +219,8 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     host.copy_(dev_data[: nb * step])
     odt = torch.int64 if wide else torch.int32
     slots = [torch.empty(step, dtype=torch.uint8, device=dev_data.device) for _ in range(3)]
-    per = 2 if alg_id == 5 else 1
-    outs = [torch.empty(count * per, dtype=odt, device=dev_data.device) for _ in range(3)]
-    hres = torch.empty((iters, count * per), dtype=odt, pin_memory=True)
+    outs = [torch.empty(count, dtype=odt, device=dev_data.device) for _ in range(3)]
+    hres = torch.empty((iters, count), dtype=odt, pin_memory=True)
     cs, ks = torch.cuda.Stream(device=dev_data.device), torch.cuda.Stream(device=dev_data.device)
     copied = [torch.cuda.Event() for _ in range(3)]
     freed = [torch.cuda.Event() for _ in range(3)]
@@ -137,7 +245,6 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     run(iters)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    # H2D alone through the same pinned buffers (the PCIe ceiling of this pipeline)
     t1 = time.perf_counter()
     with torch.cuda.stream(cs):
         for i in range(iters):
@@ -147,51 +254,6 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     return {"value": round(iters * step / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(iters * step / el_h2d / 2**30, 2),
             "sample": f"{iters} batches of {count} x {L // 1024} KiB from {nb * step >> 20} MiB pinned host memory, "
                       f"H2D on a copy stream overlapped with the scans, results D2H"}
-
-
-def target_shape(eng, alg_id, dev, streams, nbuf, steps=20, nb=2, timing=6):
-    """BASELINE.json north_star target shape, reported beside `value` (never as `value`): CRC32C over
-    batches of `nbuf` device-resident 64 MiB buffers, pipelined over the same streams as the headline
-    leg, plus the dispatch-stamped duration of `timing` serialized launches."""
-    import torch
-
-    L = 64 << 20
-    step_bytes = nbuf * L
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x7A26)
-    data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
-    outs = [torch.empty(nbuf, dtype=torch.int32, device=dev) for _ in range(nb)]
-
-    def launch(i, st):
-        eng.checksum_strided(alg_id, data, L, L, nbuf, out=outs[i % nb], stream=st, base_offset=(i % nb) * step_bytes)
-
-    for i in range(max(nb * len(streams), 3)):
-        launch(i, streams[i % len(streams)])
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        launch(i, streams[i % len(streams)])
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    st = streams[0]
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(timing)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(timing)]
-    with torch.cuda.stream(st):
-        torch.cuda._sleep(int(40e6))
-    for i in range(timing):
-        starts[i].record(st)
-        ends[i].record(st)
-        eng.time_next_launch(starts[i], ends[i])
-        launch(i, st)
-    torch.cuda.synchronize()
-    kms = sum(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends)) / timing
-    gibs = steps * step_bytes / el / 2**30
-    del data
-    return {"workload": f"{nbuf} x 64 MiB buffers per step, CRC32C, device-resident, {nb} rotating batches",
-            "value": round(gibs, 2), "unit": "GiB/s", "steps": steps,
-            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
-            "kernel_ms": round(kms, 4), "roofline_frac": round(step_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "target_pct": 80.0}
 
 
 def main():
@@ -212,56 +274,44 @@ def main():
     eng.init()
 
     alg, count, L = args.alg, args.buffers, args.buffer_bytes
+    G = max(1, min(16, args.coalesce))
     step_bytes = count * L
     nb = max(1, args.batches)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
-    wide = alg in ("crc64nvme", "xxh64", "xxh3_64", "xxh3_128")
-    per = 2 if alg == "xxh3_128" else 1  # XXH3-128: {high, low} per buffer
+    wide = alg in WIDE
+    per = 2 if alg == "xxh3_128" else 1
     outs = [torch.empty(count * per, dtype=torch.int64 if wide else torch.int32, device=dev) for _ in range(nb)]
     streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.branches))]
 
-    def launch(i, st=None):
+    def batch(i):
         b = i % nb
-        st = st or streams[i % len(streams)]
-        eng.checksum_strided(ALG[alg], data, L, L, count, out=outs[b], stream=st, base_offset=b * step_bytes)
+        return (data.data_ptr() + b * step_bytes, None, outs[b])
+
+    def launch_group(i0, i1, st):
+        eng.checksum_batches(ALG[alg], [batch(i) for i in range(i0, i1)], L, L, count, stream=st)
+
+    def run_steps(k, g_):
+        cuts = split(k, g_)
+        for j in range(len(cuts) - 1):
+            launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
 
     torch.cuda.synchronize()
-    # every batch once and, when there is a timed region, every stream (per-stream workspaces are
-    # allocated on first use); with --steps 0 (profiling the timing pass) stream 0 only, so every
-    # launch of the run is a serialized one
-    for i in range(max(args.warmup, nb if args.steps == 0 else nb * len(streams))):
-        launch(i, streams[0] if args.steps == 0 else None)
+    # every batch and every stream once (per-stream workspaces are allocated on first use), then the
+    # requested warm-up steps the same way as the timed ones
+    for j in range(nb * len(streams)):
+        launch_group(j, j + 1, streams[j % len(streams)])
+    if args.warmup > 0:
+        run_steps(args.warmup, G)
     torch.cuda.synchronize()
-
-    graph = None
-    if args.mode == "graph":
-        graph = torch.cuda.CUDAGraph()
-        cap = streams[0]
-        with torch.cuda.graph(graph, stream=cap):
-            for st in streams[1:]:
-                st.wait_stream(cap)
-            for i in range(nb):
-                launch(i, streams[i % len(streams)])
-            for st in streams[1:]:
-                cap.wait_stream(st)
-        for _ in range(2):
-            graph.replay()
-        torch.cuda.synchronize()
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if graph is not None:
-        for _ in range(args.steps // nb):
-            graph.replay()
-        for i in range(args.steps % nb):
-            launch(i)
-    else:
-        for i in range(args.steps):
-            launch(i)
+    if args.steps > 0:
+        run_steps(args.steps, G)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -271,78 +321,56 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    value = world * args.steps * step_bytes / elapsed / 2**30
+    value = world * args.steps * step_bytes / max(elapsed, 1e-9) / 2**30
 
-    # kernel duration: eager launches on one stream, each between two HIP events, queued while
-    # the stream is held by a GPU sleep so the events bracket back-to-back kernels
-    st = streams[0]
+    # dominant kernel: launches of G batches (the timed region's launch shape), then one-batch launches
     nt = max(1, args.timing_launches)
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
-    with torch.cuda.stream(st):
-        torch.cuda._sleep(int(40e6))
-    for i in range(nt):
-        starts[i].record(st)  # creates the events; the launch below re-stamps them
-        ends[i].record(st)
-        eng.time_next_launch(starts[i], ends[i])  # hipExtLaunchKernel: the dispatch's own timestamps
-        launch(i, st)
-    torch.cuda.synchronize()
-    durs = sorted(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends))
-    kernel_ms = sum(durs) / nt
-    achieved_gbs = step_bytes / (kernel_ms * 1e-3) / 1e9
-
-    # secondary denominator: the streaming-read ceiling of this launch shape -- the
-    # same batches read by an XOR-reduce kernel with the W=32 scan's geometry, timed the same two ways
-    ceiling = None
-    if not args.no_read_ceiling:
-        with torch.cuda.stream(st):
-            torch.cuda._sleep(int(40e6))
-        for i in range(nt):
-            starts[i].record(st)
-            ends[i].record(st)
-            eng.time_next_launch(starts[i], ends[i])
-            eng.read_ceiling(data, step_bytes, stream=st, base_offset=(i % nb) * step_bytes)
-        torch.cuda.synchronize()
-        rc_ms = sum(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends)) / nt
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for i in range(args.steps):
-            eng.read_ceiling(data, step_bytes, stream=streams[i % len(streams)], base_offset=(i % nb) * step_bytes)
-        torch.cuda.synchronize()
-        rc_el = time.perf_counter() - t1
-        rc_gbs = step_bytes / (rc_ms * 1e-3) / 1e9
-        ceiling = {"kernel_ms": round(rc_ms, 5), "achieved": round(rc_gbs, 1), "unit": "GB/s",
-                   "pipelined_gibs": round(args.steps * step_bytes / max(rc_el, 1e-9) / 2**30, 2),
-                   "scan_frac_of_ceiling": round(achieved_gbs / rc_gbs, 4),
-                   "kernel": "read_ceiling_kernel: same launch shape, 256-B non-temporal rows XOR-reduced"}
-
-    traffic = None
+    gsz = split(max(args.steps, 1), G)[1]  # batches per launch in the timed region
+    kms, kmed = time_launches(eng, lambda i, st: launch_group(i * gsz, i * gsz + gsz, st), streams[0], nt)
+    kms1, _ = time_launches(eng, lambda i, st: launch_group(i, i + 1, st), streams[0], nt)
+    roof = roofline(gsz * step_bytes, kms, KERNEL.get(alg, alg))
+    roof["kernel_ms_median"] = round(kmed, 5)
+    roof["timing_launches"] = nt
+    roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(step_bytes, kms1, "")["frac"],
+                            "bytes_per_launch": step_bytes}
+    roof["traffic"] = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
-            if rec.get("workload") == f"{alg}:{count}x{L}":
-                traffic = rec.get("hbm_bytes_per_launch")
+            if rec.get("workload") == f"{alg}:{count}x{L}" and rec.get("batches_per_launch", 1) == gsz:
+                roof["traffic"] = rec.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = rec.get("source", "profiles/pmc_traffic.json")
         except Exception:
-            traffic = None
+            pass
 
-    e2e = None
-    if rank == 0 and world == 1 and args.e2e_batches > 0:
-        e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
+    # secondary denominator: the streaming-read ceiling of a one-batch launch
+    if not args.no_read_ceiling:
+        rc_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, step_bytes, stream=st,
+                                                                     base_offset=(i % nb) * step_bytes), streams[0], nt)
+        roof["single_batch"]["read_ceiling_kernel_ms"] = round(rc_ms, 5)
+        roof["single_batch"]["read_ceiling_frac"] = roofline(step_bytes, rc_ms, "")["frac"]
 
-    target = None
-    if rank == 0 and world == 1 and alg == "crc32c" and args.target_buffers > 0:
-        target = target_shape(eng, ALG[alg], dev, streams, args.target_buffers)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and alg in ("crc32", "crc32c", "crc64nvme", "xxh64"):
-        host = data[:step_bytes].cpu().numpy()
-        torch.cuda.synchronize()
-        gpu0 = eng.as_unsigned(outs[0])
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
-        cpu = cpu_baseline(alg, host, count, L, gpu0, args.cpu_seconds, threads)
+    cpu = e2e = None
+    configs = {}
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            torch.cuda.synchronize()
+            host = data[:step_bytes].cpu().numpy()
+            cpu = cpu_baseline(eng, alg, host, count, L, eng.as_unsigned(outs[0]), args.cpu_seconds)
+        if args.e2e_batches > 0:
+            e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
+        if not args.no_configs:
+            del data
+            torch.cuda.empty_cache()
+            do_cpu = not args.no_cpu_baseline
+            configs["C3_crc32c"] = config_leg(eng, "C3", "crc32c", 16, 256 << 20, streams, dev, do_cpu=do_cpu)
+            configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, do_cpu=do_cpu)
+            configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, do_cpu=do_cpu)
+            configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, do_cpu=do_cpu)
+            configs["target_16x64MiB_crc32c"] = config_leg(eng, "north-star target", "crc32c", 16, 64 << 20, streams, dev,
+                                                           steps=20, do_cpu=do_cpu)
+            configs["target_16x64MiB_crc32c"]["target_pct"] = 80.0
 
     if rank == 0:
         rec = {
@@ -359,20 +387,19 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint bytes on device)",
-            "config": {"workload": f"C2: {count} x {L // 1024} KiB independent buffers, {alg.upper()}, "
-                                   f"device-resident, per GPU per step",
+            "config": {"workload": f"C2: {count} x {L // 1024} KiB independent buffers per step, {alg.upper()}, "
+                                   f"device-resident, per GPU",
                        "buffers_per_step": count, "buffer_bytes": L, "rotating_batches": nb,
-                       "resident_bytes_per_gpu": nb * step_bytes, "launch": args.mode,
+                       "resident_bytes_per_gpu": nb * step_bytes,
+                       "launch": f"aws_crt_amd_checksum_batches, up to {G} queued batches per launch "
+                                 f"({len(split(max(args.steps, 1), G)) - 1} launches for {args.steps} steps)",
                        "streams": len(streams),
                        "parallelism": f"buffers sharded over {world} GPU(s), no collective"},
             "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kernel_ms, 5), "kernel_ms_median": round(durs[nt // 2], 5),
-                         "bytes_per_launch": step_bytes, "timing_launches": nt, "read_ceiling": ceiling},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_pinned": e2e,
-            "target_shape": target,
+            "configs": configs or None,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -112,6 +112,27 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(
     void *hip_stream);
 
 /*
+ * Several uniform batches of the same shape (stride, len, count), each with its own base, seeds and
+ * results -- e.g. successive queued part batches.  CRC algorithms: up to 16 batches whose bases share
+ * their alignment mod 16 go into ONE launch, so back-to-back batches do not each pay a launch's ramp
+ * and tail; xxHash: one launch per batch.  Same per-buffer semantics as
+ * aws_crt_amd_checksum_strided.  `batches` is a HOST array.
+ */
+struct aws_crt_amd_batch {
+    const void *d_base;  /* buffer i = [d_base + i*stride, + len) */
+    const void *d_seeds; /* count seeds, or NULL for seed 0 */
+    void *d_out;         /* count results */
+};
+AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(
+    int algorithm,
+    const struct aws_crt_amd_batch *batches,
+    size_t nbatches,
+    size_t stride,
+    size_t len,
+    size_t count,
+    void *hip_stream);
+
+/*
  * Ragged batch: buffer i = [d_ptrs[i], + lens[i]).  d_ptrs and lens are HOST arrays describing
  * device buffers (any alignment, any length including 0).  The engine uploads a compact
  * descriptor (16 B per buffer + tile prefix) per call.  d_seeds as above.

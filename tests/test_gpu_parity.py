@@ -173,6 +173,31 @@ def test_fuzz_lengths_alignments_seeds(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
+def test_checksum_batches(engine, alg):
+    """aws_crt_amd_checksum_batches: 37 batches of one shape (more than one launch holds), each with its
+    own base, seeds (some none) and results; bases of mixed alignment mod 16 split the launches.
+    Shapes: whole-tile buffers (streaming scans), ragged lengths (braided scans), C2's 64 KiB."""
+    import torch
+
+    rng = random.Random(0xBA7C + ALG[alg])
+    for L, count in [(65536, 64), (8192, 200), (4096 * 3 + 20, 33), (100, 7)]:
+        stride = (L + 15) // 16 * 16 + 16
+        nb = 37
+        d = dev_random(nb * (stride * count + 64), 41 + L % 13)
+        offs = [j * (stride * count + 64) + (0 if j % 5 else rng.choice([0, 16, 3, 8])) for j in range(nb)]
+        seeds = [[rng.getrandbits(64 if alg in W64 else 32) for _ in range(count)] if j % 3 else None for j in range(nb)]
+        outs = [torch.full((count,), 7, dtype=torch.int64 if alg in W64 else torch.int32, device="cuda") for _ in range(nb)]
+        batches = [(d.data_ptr() + o, seeds_tensor(alg, sd) if sd else None, out) for o, sd, out in zip(offs, seeds, outs)]
+        engine.checksum_batches(ALG[alg], batches, stride, L, count)
+        torch.cuda.synchronize()
+        h = host_bytes(d)
+        for j in range(nb):
+            want = [oracle.checksum(alg, h[offs[j] + i * stride: offs[j] + i * stride + L], seeds[j][i] if seeds[j] else 0)
+                    for i in range(count)]
+            assert engine.as_unsigned(outs[j]) == want, (L, j)
+
+
 @pytest.mark.parametrize("alg", ["xxh3_64", "xxh3_128"])
 def test_xxh3_split_long_strided(engine, alg):
     """Strided XXH3 over buffers of >= 4096 full blocks takes the split path (block-sum pass, then
