@@ -76,16 +76,24 @@ def check_frames(base, offsets, limit=None, stream=None):
     """Device-side framing check (aws_crt_amd_eventstream_crcs): `base` is a torch uint8 device tensor
     holding the messages, `offsets` a device int64 tensor of message starts.  Each message's length
     comes from its own prelude.  Returns (prelude_crc, message_crc, status) int32 device tensors;
-    status bits: STATUS_PRELUDE_OK, STATUS_MESSAGE_OK, STATUS_MALFORMED."""
+    status bits: STATUS_PRELUDE_OK, STATUS_MESSAGE_OK, STATUS_MALFORMED (length outside the buffer,
+    total_length < 16, or headers_length > total_length - 16)."""
     import torch
 
     L = lib()
     f = L.aws_crt_amd_eventstream_crcs
     vp = ctypes.c_void_p
     f.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_size_t, vp, vp, vp, vp]
+    if offsets.dtype != torch.int64 or not offsets.is_contiguous():
+        raise TypeError("offsets must be a contiguous int64 tensor (the kernel reads u64 offsets)")
+    if not base.is_contiguous():
+        raise TypeError("base must be contiguous")
+    if offsets.device != base.device:
+        raise ValueError("base and offsets must be on the same device")
     n = offsets.numel()
     pre, msg, st = (torch.empty(n, dtype=torch.int32, device=base.device) for _ in range(3))
-    lim = base.numel() if limit is None else min(int(limit), base.numel())
+    nbytes = base.numel() * base.element_size()
+    lim = nbytes if limit is None else min(int(limit), nbytes)
     _check(f(base.data_ptr(), lim, offsets.data_ptr(), n, pre.data_ptr(), msg.data_ptr(), st.data_ptr(),
              _stream_handle(stream)))
     return pre, msg, st

@@ -1844,8 +1844,8 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
 }
 
 // Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads
-// total_length from the message's prelude (big-endian), refuses lengths outside [16, limit - offset]
-// before touching the body, then folds the prelude (-> prelude CRC) and continues over the headers
+// total_length and headers_length from the message's prelude (big-endian), refuses lengths outside
+// [16, limit - offset] and headers longer than total - 16 before touching the body, then folds the prelude (-> prelude CRC) and continues over the headers
 // and payload (-> message CRC, the running form of CRC32 over [0, total - 4)), and compares both
 // with the big-endian values stored at offset 8 and total - 4.
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
@@ -1860,8 +1860,10 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
     uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
     if (off <= p.limit && p.limit - off >= 16) {
         const uint8_t *q = p.base + off;
-        const uint64_t total = be32(q);
-        if (total >= 16 && total <= p.limit - off) {
+        const uint64_t total = be32(q), headers = be32(q + 4);
+        // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
+        // (headers_length > total_length - 16): malformed, whatever the CRCs say
+        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
             uint32_t s = lane_scan<uint32_t>(~0u, q, 8, tab);
             pre = ~s;
             s = lane_scan<uint32_t>(s, q + 8, total - 12, tab);

@@ -153,8 +153,8 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list(
  * bytes).  Its prelude is total_length (u32 BE) | headers_length (u32 BE) | prelude_crc (u32 BE), its
  * last 4 bytes the message CRC (u32 BE) over bytes [0, total_length - 4).  Writes the computed
  * prelude and message CRC32s and d_status[i]: bit 0 = stored prelude CRC matches, bit 1 = stored
- * message CRC matches, bit 2 = malformed (total_length < 16 or past `limit`; nothing beyond the
- * first 16 bytes is read then, and both CRCs are 0).  One lane per message: for many short
+ * message CRC matches, bit 2 = malformed (total_length < 16 or past `limit`, or headers_length >
+ * total_length - 16; nothing beyond the first 16 bytes is read then, and both CRCs are 0).  One lane per message: for many short
  * messages; a message of megabytes is better checked with aws_crt_amd_checksum_strided.
  */
 AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(

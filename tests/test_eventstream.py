@@ -142,6 +142,13 @@ def test_check_frames_device(engine):
         extra.append(len(blob))
         blob += struct.pack(">II", total, 0) + bytes(8)
         want.append((0, 0, STATUS_MALFORMED))
+    # headers_length > total_length - 16 (aws-c-event-stream refuses it), even with both CRCs right
+    extra.append(len(blob))
+    bad = struct.pack(">II", 40, 25) + bytes(28)
+    bad = bad[:8] + struct.pack(">I", oracle.crc("crc32", bad[:8])) + bad[12:36]
+    bad += struct.pack(">I", oracle.crc("crc32", bad))
+    blob += bad
+    want.append((0, 0, STATUS_MALFORMED))
     extra.append(len(blob) - 4)  # fewer than 16 bytes left
     want.append((0, 0, STATUS_MALFORMED))
     d = torch.from_numpy(np.frombuffer(bytes(blob), dtype=np.uint8).copy()).cuda()
@@ -150,3 +157,17 @@ def test_check_frames_device(engine):
     torch.cuda.synchronize()
     got = list(zip(engine.as_unsigned(pre), engine.as_unsigned(msg), engine.as_unsigned(st)))
     assert got == want
+
+
+def test_check_frames_argument_types():
+    """check_frames refuses offsets that are not int64 (the kernel reads u64 offsets) before any
+    device work; the byte limit is taken from the buffer's size in bytes, not its element count."""
+    import torch
+
+    from aws_crt_amd.eventstream import check_frames
+
+    base = torch.zeros(64, dtype=torch.uint8)
+    with pytest.raises(TypeError):
+        check_frames(base, torch.zeros(2, dtype=torch.int32))
+    with pytest.raises(TypeError):
+        check_frames(base, torch.zeros(4, dtype=torch.int64)[::2])
