@@ -184,6 +184,86 @@ def checksum_batches(alg: int, batches, stride: int, length: int, count: int, st
     _check(L.aws_crt_amd_checksum_batches(alg, arr, n, stride, length, count, _stream_handle(stream)))
 
 
+def host_job(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):
+    """aws_crt_amd_host_submit + aws_crt_amd_job_wait over host buffers given by raw addresses; returns
+    the results (XXH3_128: 128-bit ints).  Synchronous from Python's point of view."""
+    L = lib()
+    n = len(ptrs)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.aws_crt_amd_host_submit.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp, ctypes.c_int,
+                                          ctypes.POINTER(vp)]
+    L.aws_crt_amd_job_wait.argtypes = [vp]
+    L.aws_crt_amd_job_last_error.restype = ctypes.c_char_p
+    P = (vp * max(n, 1))(*ptrs)
+    S = (sz * max(n, 1))(*lens)
+    T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
+    out = (T * max(n * (2 if alg == XXH3_128 else 1), 1))()
+    sd = (T * max(n, 1))(*seeds) if seeds is not None else None
+    job = vp()
+    rc = L.aws_crt_amd_host_submit(alg, P, S, n, ctypes.cast(sd, vp) if sd is not None else None, ctypes.cast(out, vp),
+                                   ndevices, ctypes.byref(job))
+    if rc == 0:
+        rc = L.aws_crt_amd_job_wait(job)
+    if rc != 0:
+        raise EngineError(f"host job failed ({rc}): {L.aws_crt_amd_job_last_error().decode()}")
+    if alg == XXH3_128:
+        return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
+    return [int(out[i]) for i in range(n)]
+
+
+def register_host(addr: int, nbytes: int) -> None:
+    L = lib()
+    L.aws_crt_amd_register_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    _check(L.aws_crt_amd_register_host(addr, nbytes))
+
+
+def unregister_host(addr: int) -> None:
+    L = lib()
+    L.aws_crt_amd_unregister_host.argtypes = [ctypes.c_void_p]
+    _check(L.aws_crt_amd_unregister_host(addr))
+
+
+def checksum_list_devices(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None) -> list:
+    """Device buffers on any visible devices (raw addresses) -> results in caller order (host)."""
+    L = lib()
+    n = len(ptrs)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.aws_crt_amd_checksum_list_devices.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp]
+    P = (vp * max(n, 1))(*ptrs)
+    S = (sz * max(n, 1))(*lens)
+    T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
+    out = (T * max(n * (2 if alg == XXH3_128 else 1), 1))()
+    sd = (T * max(n, 1))(*seeds) if seeds is not None else None
+    _check(L.aws_crt_amd_checksum_list_devices(alg, P, S, n, ctypes.cast(sd, vp) if sd is not None else None,
+                                               ctypes.cast(out, vp)))
+    if alg == XXH3_128:
+        return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
+    return [int(out[i]) for i in range(n)]
+
+
+class _DeviceBatch(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("d_base", ctypes.c_void_p), ("stride", ctypes.c_size_t),
+                ("len", ctypes.c_size_t), ("count", ctypes.c_size_t), ("d_seeds", ctypes.c_void_p),
+                ("d_out", ctypes.c_void_p), ("hip_stream", ctypes.c_void_p)]
+
+
+def checksum_devices(alg: int, entries) -> None:
+    """aws_crt_amd_checksum_devices: entries of (device, base tensor/address, stride, len, count, seeds
+    tensor or None, out tensor, stream or None); all devices at once, returns when all are done."""
+    L = lib()
+    n = len(entries)
+    arr = (_DeviceBatch * max(n, 1))()
+    for i, (dev, base, stride, ln, cnt, seeds, out, st) in enumerate(entries):
+        arr[i].device = dev
+        arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+        arr[i].stride, arr[i].len, arr[i].count = stride, ln, cnt
+        arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
+        arr[i].d_out = out.data_ptr()
+        arr[i].hip_stream = st.cuda_stream if st is not None else None
+    L.aws_crt_amd_checksum_devices.argtypes = [ctypes.c_int, ctypes.POINTER(_DeviceBatch), ctypes.c_size_t]
+    _check(L.aws_crt_amd_checksum_devices(alg, arr, n))
+
+
 def checksum_list(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, out=None, stream=None, device=None):
     """Ragged batch of device buffers given by raw device addresses and lengths (host lists)."""
     import torch

@@ -1,0 +1,488 @@
+// Host ingest and in-process multi-device fan-out (include/aws_crt_amd/checksums_batch.h).
+//
+// the CRT's part buffers (S3BufferTicket, include/aws/crt/s3/S3BufferTicket.h:20-30;
+// async S3MetaRequest::Write, source/s3/S3.cpp:1133-1149) start in host memory.  A host job shards
+// the caller's buffers round-robin over the visible GPUs (north_star: one HIP stream per GPU, no
+// collective) and, per device, runs a three-slot pipeline on two streams:
+//
+//     copy stream     H2D slot k+1   (DMA straight from registered / pinned memory; pageable bytes are
+//                                     first copied into the slot's pinned mirror by the worker thread)
+//     compute stream  scan slot k    (one ragged list launch over the pieces packed into the slot)
+//                     D2H piece results
+//
+// Buffers longer than a slot are cut into pieces; every piece is scanned from seed 0 (the caller's
+// seed for a buffer's first piece) and the pieces of a buffer are folded on the host with Combine
+// (CRC.h:41-51), O(log n) scalar algebra per piece.  xxHash cannot be split that way and is a serial
+// chain per buffer, so a job's xxHash buffers run on the engine's host path (one std::thread per
+// device slot of the job) while the CRCs run on the GPUs.
+//
+// Device-resident lists spanning several devices (aws_crt_amd_checksum_list_devices) are grouped by
+// the device that owns each buffer; one host thread per device stages and launches that device's
+// list and copies its results back, and the results are scattered in caller order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cpu/cpu_checksums.h"
+#include "gf2.h"
+
+#define AWS_CRT_AMD_BUILD 1
+#include <aws_crt_amd/checksums_batch.h>
+
+using namespace amdcrc;
+
+namespace {
+
+thread_local std::string t_err;
+
+constexpr size_t kSlotBytes = 32u << 20;  // device slot / pinned mirror per pipeline stage
+constexpr int kSlots = 3;
+constexpr size_t kMaxPiecesPerSlot = 8192;
+
+inline bool is_crc(int alg) { return alg <= AWS_CRT_AMD_CRC64NVME; }
+inline int out_words(int alg) { return alg == AWS_CRT_AMD_XXH3_128 ? 2 : 1; }
+
+bool host_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;  // hipHostMalloc'd or hipHostRegister'ed
+}
+
+struct Piece {
+    size_t buf;          // caller's buffer index
+    size_t off, len;     // bytes [off, off + len) of that buffer
+    uint64_t seed;       // the caller's seed for the first piece, 0 otherwise
+};
+
+// One device's pipeline state
+struct Lane {
+    int dev = -1;
+    hipStream_t copy = nullptr, comp = nullptr;
+    void *dslot[kSlots] = {};
+    void *hmirror[kSlots] = {};
+    void *dres[kSlots] = {}, *dseed[kSlots] = {};
+    void *hres[kSlots] = {}, *hseed[kSlots] = {};
+    hipEvent_t copied[kSlots] = {}, done[kSlots] = {};
+    bool used[kSlots] = {};
+};
+
+struct JobImpl {
+    int alg = 0;
+    const void *const *ptrs = nullptr;
+    const size_t *lens = nullptr;
+    size_t count = 0;
+    std::vector<uint64_t> seeds;  // per buffer (0 when none)
+    void *h_out = nullptr;
+    std::vector<Piece> pieces;
+    std::vector<uint64_t> piece_val;  // per piece (CRC jobs)
+    std::vector<std::thread> workers;
+    std::atomic<int> rc{0};
+    std::string err;
+    std::mutex err_mu;
+    void set_error(int code, const std::string &m) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (rc.load() == 0) {
+            rc.store(code);
+            err = m;
+        }
+    }
+};
+
+#define LANE_TRY(expr)                                                                                     \
+    do {                                                                                                   \
+        hipError_t e_ = (expr);                                                                            \
+        if (e_ != hipSuccess) {                                                                            \
+            job->set_error(AWS_CRT_AMD_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));           \
+            return;                                                                                        \
+        }                                                                                                  \
+    } while (0)
+
+void lane_free(Lane &L) {
+    // nothing may still be queued on the lane's streams when its buffers go (an early error return)
+    if (L.copy) (void)hipStreamSynchronize(L.copy);
+    if (L.comp) (void)hipStreamSynchronize(L.comp);
+    for (int k = 0; k < kSlots; ++k) {
+        if (L.dslot[k]) (void)hipFree(L.dslot[k]);
+        if (L.dres[k]) (void)hipFree(L.dres[k]);
+        if (L.dseed[k]) (void)hipFree(L.dseed[k]);
+        if (L.hmirror[k]) (void)hipHostFree(L.hmirror[k]);
+        if (L.hres[k]) (void)hipHostFree(L.hres[k]);
+        if (L.hseed[k]) (void)hipHostFree(L.hseed[k]);
+        if (L.copied[k]) (void)hipEventDestroy(L.copied[k]);
+        if (L.done[k]) (void)hipEventDestroy(L.done[k]);
+    }
+    if (L.copy) (void)hipStreamDestroy(L.copy);
+    if (L.comp) (void)hipStreamDestroy(L.comp);
+}
+
+// Worker for one device: pieces `mine` (indices into job->pieces, in order) through the 3-slot ring
+void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) {
+    Lane L;
+    L.dev = dev;
+    struct Guard {
+        Lane &l;
+        ~Guard() { lane_free(l); }
+    } guard{L};
+    LANE_TRY(hipSetDevice(dev));
+    LANE_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
+    LANE_TRY(hipStreamCreateWithFlags(&L.comp, hipStreamNonBlocking));
+    const size_t osz = job->alg == AWS_CRT_AMD_CRC64NVME ? 8 : 4;
+    for (int k = 0; k < kSlots; ++k) {
+        LANE_TRY(hipMalloc(&L.dslot[k], kSlotBytes));
+        LANE_TRY(hipHostMalloc(&L.hmirror[k], kSlotBytes, hipHostMallocDefault));
+        LANE_TRY(hipMalloc(&L.dres[k], kMaxPiecesPerSlot * 8));
+        LANE_TRY(hipMalloc(&L.dseed[k], kMaxPiecesPerSlot * 8));
+        LANE_TRY(hipHostMalloc(&L.hres[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
+        LANE_TRY(hipHostMalloc(&L.hseed[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
+        LANE_TRY(hipEventCreateWithFlags(&L.copied[k], hipEventDisableTiming));
+        LANE_TRY(hipEventCreateWithFlags(&L.done[k], hipEventDisableTiming));
+    }
+    std::vector<const void *> dptrs;
+    std::vector<size_t> dlens;
+    std::vector<size_t> slot_pieces[kSlots];
+    // copy a slot's results back into the job once its scan has completed
+    auto harvest = [&](int k) {
+        if (!L.used[k]) return true;
+        if (hipEventSynchronize(L.done[k]) != hipSuccess) return false;
+        const std::vector<size_t> &ps = slot_pieces[k];
+        for (size_t j = 0; j < ps.size(); ++j)
+            job->piece_val[ps[j]] = osz == 8 ? ((const uint64_t *)L.hres[k])[j] : ((const uint32_t *)L.hres[k])[j];
+        L.used[k] = false;
+        return true;
+    };
+    size_t next = 0;
+    int k = 0;
+    while (next < mine.size() && job->rc.load() == 0) {
+        if (!harvest(k)) {
+            job->set_error(AWS_CRT_AMD_ERR_HIP, "slot results");
+            return;
+        }
+        // pack pieces into slot k: contiguous in the slot, in order
+        std::vector<size_t> &ps = slot_pieces[k];
+        ps.clear();
+        size_t fill = 0;
+        while (next < mine.size() && ps.size() < kMaxPiecesPerSlot) {
+            const Piece &pc = job->pieces[mine[next]];
+            if (fill + pc.len > kSlotBytes && !ps.empty()) break;
+            ps.push_back(mine[next]);
+            fill += pc.len;
+            ++next;
+        }
+        // H2D: runs of host-contiguous pinned pieces go straight from the caller's memory; the rest
+        // through the pinned mirror (memcpy by this thread, then one DMA per run)
+        size_t off = 0;
+        dptrs.clear();
+        dlens.clear();
+        uint8_t *slot = (uint8_t *)L.dslot[k], *mir = (uint8_t *)L.hmirror[k];
+        size_t run_dev = 0, run_len = 0;
+        const uint8_t *run_src = nullptr;
+        auto flush = [&]() -> bool {
+            if (run_len && hipMemcpyAsync(slot + run_dev, run_src, run_len, hipMemcpyHostToDevice, L.copy) != hipSuccess) return false;
+            run_len = 0;
+            return true;
+        };
+        // pinned or not is asked once per run of host-contiguous pieces (it only decides between a
+        // direct DMA and the mirror: hipMemcpyAsync is correct from pageable memory too)
+        bool cur_pinned = false;
+        const uint8_t *src_end = nullptr;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            const Piece &pc = job->pieces[ps[j]];
+            const uint8_t *src = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
+            if (src != src_end) cur_pinned = pc.len && host_pinned(src);
+            src_end = src + pc.len;
+            const uint8_t *from = src;
+            if (pc.len && !cur_pinned) {
+                std::memcpy(mir + off, src, pc.len);
+                from = mir + off;
+            }
+            if (run_len && run_src + run_len == from && run_dev + run_len == off) {
+                run_len += pc.len;
+            } else {
+                if (!flush()) {
+                    job->set_error(AWS_CRT_AMD_ERR_HIP, "host-to-device copy");
+                    return;
+                }
+                run_src = from, run_dev = off, run_len = pc.len;
+            }
+            dptrs.push_back(slot + off);
+            dlens.push_back(pc.len);
+            if (osz == 8)
+                ((uint64_t *)L.hseed[k])[j] = pc.seed;
+            else
+                ((uint32_t *)L.hseed[k])[j] = (uint32_t)pc.seed;
+            off += pc.len;
+        }
+        if (!flush()) {
+            job->set_error(AWS_CRT_AMD_ERR_HIP, "host-to-device copy");
+            return;
+        }
+        LANE_TRY(hipMemcpyAsync(L.dseed[k], L.hseed[k], ps.size() * osz, hipMemcpyHostToDevice, L.copy));
+        LANE_TRY(hipEventRecord(L.copied[k], L.copy));
+        LANE_TRY(hipStreamWaitEvent(L.comp, L.copied[k], 0));
+        const int rc = aws_crt_amd_checksum_list(job->alg, dptrs.data(), dlens.data(), ps.size(), L.dseed[k], L.dres[k], L.comp);
+        if (rc) {
+            job->set_error(rc, aws_crt_amd_last_error());
+            return;
+        }
+        LANE_TRY(hipMemcpyAsync(L.hres[k], L.dres[k], ps.size() * osz, hipMemcpyDeviceToHost, L.comp));
+        LANE_TRY(hipEventRecord(L.done[k], L.comp));
+        // the slot's copy stream must not overwrite it before the scan has read it: the next use of
+        // slot k waits on done[k] in harvest(); the copy stream also waits for it explicitly
+        L.used[k] = true;
+        k = (k + 1) % kSlots;
+        LANE_TRY(hipStreamWaitEvent(L.copy, L.done[k], 0));  // slot k (next) free on the device side
+    }
+    for (int j = 0; j < kSlots; ++j)
+        if (!harvest(j)) job->set_error(AWS_CRT_AMD_ERR_HIP, "slot results");
+}
+
+// A job's buffers on the host path (xxHash, or no device): buffers round-robin over `threads`
+void host_worker(JobImpl *job, size_t t, size_t threads) {
+    for (size_t i = t; i < job->count; i += threads) {
+        uint64_t r[2] = {0, 0};
+        const uint8_t *p = (const uint8_t *)job->ptrs[i];
+        const size_t n = job->lens[i];
+        const uint64_t sd = job->seeds[i];
+        switch (job->alg) {
+            case AWS_CRT_AMD_CRC32: ((uint32_t *)job->h_out)[i] = cpu::crc32(p, n, (uint32_t)sd); continue;
+            case AWS_CRT_AMD_CRC32C: ((uint32_t *)job->h_out)[i] = cpu::crc32c(p, n, (uint32_t)sd); continue;
+            case AWS_CRT_AMD_CRC64NVME: ((uint64_t *)job->h_out)[i] = cpu::crc64nvme(p, n, sd); continue;
+            case AWS_CRT_AMD_XXH64: r[0] = cpu::xxh64(p, n, sd); break;
+            case AWS_CRT_AMD_XXH3_64: r[0] = cpu::xxh3_64(p, n, sd); break;
+            default: cpu::xxh3_128(p, n, sd, r); break;
+        }
+        uint64_t *o = (uint64_t *)job->h_out;
+        if (job->alg == AWS_CRT_AMD_XXH3_128)
+            o[2 * i] = r[0], o[2 * i + 1] = r[1];
+        else
+            o[i] = r[0];
+    }
+}
+
+int visible_devices() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+}  // namespace
+
+struct aws_crt_amd_job {
+    JobImpl impl;
+};
+
+extern "C" {
+
+AWS_CRT_AMD_API int aws_crt_amd_register_host(void *p, size_t n) {
+    if (!p || !n) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    if (visible_devices() <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
+    // portable: the registration is visible to every device's DMA engines
+    return hipHostRegister(p, n, hipHostRegisterPortable) == hipSuccess ? 0 : AWS_CRT_AMD_ERR_HIP;
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_unregister_host(void *p) {
+    if (!p) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    return hipHostUnregister(p) == hipSuccess ? 0 : AWS_CRT_AMD_ERR_HIP;
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
+                                            const void *h_seeds, void *h_out, int ndevices, struct aws_crt_amd_job **job_out) {
+    if (!job_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    *job_out = nullptr;
+    if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    if (count && (!h_ptrs || !lens || !h_out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    for (size_t i = 0; i < count; ++i)
+        if (lens[i] && !h_ptrs[i]) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    std::unique_ptr<aws_crt_amd_job> job(new (std::nothrow) aws_crt_amd_job);
+    if (!job) return AWS_CRT_AMD_ERR_OOM;
+    JobImpl &J = job->impl;
+    J.alg = alg;
+    J.ptrs = h_ptrs;
+    J.lens = lens;
+    J.count = count;
+    J.h_out = h_out;
+    const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
+    J.seeds.assign(count, 0);
+    for (size_t i = 0; h_seeds && i < count; ++i)
+        J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+    const int vis = visible_devices();
+    int G = ndevices <= 0 ? vis : std::min(ndevices, vis);
+    if (!is_crc(alg) || G <= 0) {
+        // xxHash (or no device): the host path, one thread per device the job would have used
+        const size_t threads = (size_t)std::max(1, std::min(G > 0 ? G : 1, 16));
+        for (size_t t = 0; t < threads; ++t) J.workers.emplace_back(host_worker, &J, t, threads);
+        *job_out = job.release();
+        return 0;
+    }
+    // pieces, buffer by buffer; buffer i goes to device i % G
+    std::vector<std::vector<size_t>> per_dev((size_t)G);
+    for (size_t i = 0; i < count; ++i) {
+        size_t off = 0;
+        do {
+            const size_t n = std::min(kSlotBytes, lens[i] - off);
+            per_dev[i % (size_t)G].push_back(J.pieces.size());
+            J.pieces.push_back({i, off, n, off == 0 ? J.seeds[i] : 0});
+            off += n;
+        } while (off < lens[i]);
+    }
+    J.piece_val.assign(J.pieces.size(), 0);
+    for (int g = 0; g < G; ++g)
+        if (!per_dev[(size_t)g].empty()) J.workers.emplace_back(device_worker, &J, g, std::move(per_dev[(size_t)g]));
+    *job_out = job.release();
+    return 0;
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
+    if (!job) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    JobImpl &J = job->impl;
+    for (auto &t : J.workers) t.join();
+    int rc = J.rc.load();
+    if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
+        // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
+        const uint64_t poly = alg_poly(J.alg);
+        const int w = alg_width(J.alg);
+        size_t p = 0;
+        for (size_t i = 0; i < J.count; ++i) {
+            uint64_t acc = J.piece_val[p++];
+            while (p < J.pieces.size() && J.pieces[p].buf == i) {
+                acc = gf2_mulmod(acc, gf2_xpow8n(J.pieces[p].len, poly, w), poly, w) ^ J.piece_val[p];
+                ++p;
+            }
+            if (w == 64)
+                ((uint64_t *)J.h_out)[i] = acc;
+            else
+                ((uint32_t *)J.h_out)[i] = (uint32_t)acc;
+        }
+    }
+    if (rc) t_err = J.err;
+    delete job;
+    return rc;
+}
+
+AWS_CRT_AMD_API const char *aws_crt_amd_job_last_error(void) { return t_err.c_str(); }
+
+// Device-resident buffers on any of the visible devices: grouped by owning device, one host thread
+// per device stages and launches that device's list on its own stream and copies the results back;
+// results are scattered in caller order into h_out.  Synchronous.
+AWS_CRT_AMD_API int aws_crt_amd_checksum_list_devices(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,
+                                                      const void *h_seeds, void *h_out) {
+    if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    if (!count) return 0;
+    if (!d_ptrs || !lens || !h_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    const int vis = visible_devices();
+    if (vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
+    std::vector<std::vector<size_t>> by_dev((size_t)vis);
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
+    for (size_t i = 0; i < count; ++i) {
+        int dev = cur;  // zero-length entries may carry any pointer
+        if (lens[i]) {
+            hipPointerAttribute_t a;
+            if (!d_ptrs[i] || hipPointerGetAttributes(&a, d_ptrs[i]) != hipSuccess || a.type != hipMemoryTypeDevice) {
+                (void)hipGetLastError();
+                t_err = "aws_crt_amd_checksum_list_devices: buffer " + std::to_string(i) + " is not device memory";
+                return AWS_CRT_AMD_ERR_INVALID_ARG;
+            }
+            dev = a.device;
+        }
+        by_dev[(size_t)dev].push_back(i);
+    }
+    const int per = out_words(alg);
+    const size_t osz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8 * (size_t)per;
+    const size_t ssz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8;
+    std::atomic<int> rc{0};
+    std::vector<std::thread> pool;
+    for (int g = 0; g < vis; ++g) {
+        if (by_dev[(size_t)g].empty()) continue;
+        pool.emplace_back([&, g] {
+            const std::vector<size_t> &ix = by_dev[(size_t)g];
+            const size_t n = ix.size();
+            std::vector<const void *> ptrs(n);
+            std::vector<size_t> ls(n);
+            std::vector<uint8_t> seeds(n * ssz), res(n * osz);
+            for (size_t j = 0; j < n; ++j) {
+                ptrs[j] = d_ptrs[ix[j]];
+                ls[j] = lens[ix[j]];
+                if (h_seeds) std::memcpy(seeds.data() + j * ssz, (const uint8_t *)h_seeds + ix[j] * ssz, ssz);
+            }
+            hipStream_t st = nullptr;
+            void *dbuf = nullptr;
+            int e = hipSetDevice(g) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+                            hipMalloc(&dbuf, n * (osz + ssz)) == hipSuccess
+                        ? 0
+                        : AWS_CRT_AMD_ERR_HIP;
+            void *dseed = dbuf ? (uint8_t *)dbuf + n * osz : nullptr;
+            if (!e && h_seeds && hipMemcpyAsync(dseed, seeds.data(), n * ssz, hipMemcpyHostToDevice, st) != hipSuccess)
+                e = AWS_CRT_AMD_ERR_HIP;
+            if (!e) e = aws_crt_amd_checksum_list(alg, ptrs.data(), ls.data(), n, h_seeds ? dseed : nullptr, dbuf, st);
+            if (!e && (hipMemcpyAsync(res.data(), dbuf, n * osz, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                       hipStreamSynchronize(st) != hipSuccess))
+                e = AWS_CRT_AMD_ERR_HIP;
+            if (!e)
+                for (size_t j = 0; j < n; ++j) std::memcpy((uint8_t *)h_out + ix[j] * osz, res.data() + j * osz, osz);
+            if (dbuf) (void)hipFree(dbuf);
+            if (st) (void)hipStreamDestroy(st);
+            if (e) {
+                int z = 0;
+                rc.compare_exchange_strong(z, e);
+            }
+        });
+    }
+    for (auto &t : pool) t.join();
+    (void)hipSetDevice(cur);
+    return rc.load();
+}
+
+// Per-device uniform batches, all devices at once: each entry is launched on its device (one stream
+// per device: the entry's, or one the call creates), then every device is awaited.  Synchronous.
+AWS_CRT_AMD_API int aws_crt_amd_checksum_devices(int alg, const struct aws_crt_amd_device_batch *b, size_t n) {
+    if (alg < 0 || alg > 5 || (n && !b)) return AWS_CRT_AMD_ERR_INVALID_ARG;
+    const int vis = visible_devices();
+    if (n && vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
+    std::vector<hipStream_t> own(n, nullptr);
+    int rc = 0;
+    for (size_t i = 0; i < n && !rc; ++i) {
+        if (b[i].device < 0 || b[i].device >= vis) {
+            rc = AWS_CRT_AMD_ERR_INVALID_ARG;
+            break;
+        }
+        if (hipSetDevice(b[i].device) != hipSuccess) {
+            rc = AWS_CRT_AMD_ERR_HIP;
+            break;
+        }
+        hipStream_t st = (hipStream_t)b[i].hip_stream;
+        if (!st) {
+            if (hipStreamCreateWithFlags(&own[i], hipStreamNonBlocking) != hipSuccess) {
+                rc = AWS_CRT_AMD_ERR_HIP;
+                break;
+            }
+            st = own[i];
+        }
+        rc = aws_crt_amd_checksum_strided(alg, b[i].d_base, b[i].stride, b[i].len, b[i].count, b[i].d_seeds, b[i].d_out, st);
+    }
+    for (size_t i = 0; i < n; ++i) {  // await every device (also after a failure: nothing stays queued)
+        if (hipSetDevice(b[i].device) != hipSuccess) continue;
+        hipStream_t st = own[i] ? own[i] : (hipStream_t)b[i].hip_stream;
+        if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = AWS_CRT_AMD_ERR_HIP;
+        if (own[i]) (void)hipStreamDestroy(own[i]);
+    }
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+}  // extern "C"

@@ -195,6 +195,61 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_host(
     void *h_out);
 
 /*
+ * Host ingest (S3 part buffers, S3BufferTicket.h:20-30 / S3MetaRequest::Write,
+ * S3.cpp:1133-1149).  Asynchronous: checksums `count` HOST buffers and writes one result per buffer
+ * to the HOST array h_out (u32 CRC32/32C, u64 CRC64NVME/XXH64/XXH3_64, two u64 {high, low}
+ * XXH3_128) once aws_crt_amd_job_wait(job) returns 0.  Buffers, seeds and h_out must stay valid
+ * until then.  CRCs: buffers round-robin over `ndevices` GPUs (0 = all visible), each device a
+ * three-slot pipeline (H2D on a copy stream overlapping the scans; 32 MiB slots; longer buffers cut
+ * into pieces folded with Combine).  Registered / pinned memory is DMA'd in place; pageable memory
+ * goes through pinned mirrors.  xxHash (a serial chain per buffer), and every algorithm when no
+ * device is visible, run on the host path.  h_seeds: u32 (CRC32/32C) or u64 per buffer, or NULL.
+ */
+struct aws_crt_amd_job;
+AWS_CRT_AMD_API int aws_crt_amd_host_submit(
+    int algorithm,
+    const void *const *h_ptrs,
+    const size_t *lens,
+    size_t count,
+    const void *h_seeds,
+    void *h_out,
+    int ndevices,
+    struct aws_crt_amd_job **job);
+/* Wait for a job and release it; returns its status (aws_crt_amd_job_last_error() on failure). */
+AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job);
+AWS_CRT_AMD_API const char *aws_crt_amd_job_last_error(void);
+/* Page-lock (hipHostRegister, portable to every device) / release a host range, e.g. a part-buffer
+ * pool, so host jobs DMA from it directly. */
+AWS_CRT_AMD_API int aws_crt_amd_register_host(void *p, size_t n);
+AWS_CRT_AMD_API int aws_crt_amd_unregister_host(void *p);
+
+/*
+ * In-process multi-device fan-out (north_star: batches sharded over the node's GPUs, one HIP stream
+ * per GPU, no collective).
+ *   aws_crt_amd_checksum_list_devices: device buffers living on any visible devices (HOST arrays
+ *     d_ptrs / lens); grouped by owning device, one thread + stream per device, results (and the
+ *     optional HOST seeds) in caller order in HOST h_out.  Synchronous.
+ *   aws_crt_amd_checksum_devices: one uniform batch per entry, each on its device, all devices at
+ *     once (the entry's stream, or one the call creates); returns when every device is done.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_checksum_list_devices(
+    int algorithm,
+    const void *const *d_ptrs,
+    const size_t *lens,
+    size_t count,
+    const void *h_seeds,
+    void *h_out);
+struct aws_crt_amd_device_batch {
+    int device;
+    const void *d_base; /* buffer i = [d_base + i*stride, + len) on `device` */
+    size_t stride, len, count;
+    const void *d_seeds; /* on `device`, or NULL */
+    void *d_out;         /* on `device` */
+    void *hip_stream;    /* a stream of `device`, or NULL */
+};
+AWS_CRT_AMD_API int aws_crt_amd_checksum_devices(int algorithm, const struct aws_crt_amd_device_batch *batches, size_t n);
+
+/*
  * S3 multipart checksum composition (the aws-c-s3 layer the reference's
  * S3ChecksumConfig selects, S3.cpp:380-428, default CRC64NVME at S3.cpp:31-36).
  *

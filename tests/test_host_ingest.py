@@ -1,0 +1,109 @@
+"""Host ingest (aws_crt_amd_host_submit / aws_crt_amd_job_wait) and the
+in-process multi-device fan-out (aws_crt_amd_checksum_list_devices / aws_crt_amd_checksum_devices),
+against the oracle.
+
+CPU suite: with no device visible a host job runs on the engine's host path (the API never needs a
+GPU for host memory).  GPU suite: pinned (torch pin_memory / hipHostRegister'ed) and pageable
+buffers, buffers longer than a 32 MiB pipeline slot (pieces folded with Combine), seeds, xxHash
+routed to the host path, and device-resident lists over every visible device."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
+W64 = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
+
+
+def _bufs(rng, sizes):
+    return [np.frombuffer(rng.randbytes(n), dtype=np.uint8) if n else np.zeros(0, dtype=np.uint8) for n in sizes]
+
+
+def _addr(a):
+    return a.ctypes.data if a.size else 0
+
+
+def test_host_job_without_device_uses_host_path():
+    import aws_crt_amd as eng
+
+    if eng.device_count() > 0:
+        pytest.skip("device present: covered by the gpu tests")
+    rng = random.Random(21)
+    bufs = _bufs(rng, [0, 1, 100, 4096, 70000, 1 << 20])
+    for alg in ALG:
+        seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
+        got = eng.host_job(ALG[alg], [_addr(b) for b in bufs], [b.size for b in bufs], seeds)
+        assert got == [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)], alg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", list(ALG))
+def test_host_job_pageable(engine, alg):
+    rng = random.Random(0x1A + ALG[alg])
+    sizes = [0, 1, 15, 4096, 65536, 65537, (32 << 20) - 3, (32 << 20) + 17, (70 << 20) + 5] + \
+            [rng.randrange(1, 300000) for _ in range(200)]
+    bufs = _bufs(rng, sizes)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
+    got = engine.host_job(ALG[alg], [_addr(b) for b in bufs], [b.size for b in bufs], seeds)
+    assert got == [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+def test_host_job_pinned_and_registered(engine, alg):
+    """A pinned batch (one allocation, contiguous parts: one DMA per slot) and a registered pageable
+    part pool (hipHostRegister through aws_crt_amd_register_host)."""
+    import torch
+
+    count, L = 2048, 65536
+    host = torch.randint(0, 256, (count * L,), dtype=torch.uint8).pin_memory()
+    a = host.numpy()
+    ptrs = [host.data_ptr() + i * L for i in range(count)]
+    got = engine.host_job(ALG[alg], ptrs, [L] * count)
+    assert got == oracle.batch(alg, [a.ctypes.data + i * L for i in range(count)], [L] * count, 16)
+    pool = np.frombuffer(random.Random(5).randbytes(48 << 20), dtype=np.uint8).copy()
+    engine.register_host(pool.ctypes.data, pool.nbytes)
+    try:
+        parts = [(0, 8 << 20), (8 << 20, 40 << 20), (1, 1000), (3, (48 << 20) - 3)]
+        got = engine.host_job(ALG[alg], [pool.ctypes.data + o for o, _ in parts], [n for _, n in parts])
+        assert got == [oracle.crc(alg, pool[o:o + n]) for o, n in parts]
+    finally:
+        engine.unregister_host(pool.ctypes.data)
+
+
+@pytest.mark.gpu
+def test_list_devices_and_devices_batches(engine):
+    """Buffers on every visible device in one call, results in caller order; per-device uniform
+    batches all at once (one stream per device)."""
+    import torch
+
+    ndev = torch.cuda.device_count()
+    rng = random.Random(99)
+    datas = []
+    ptrs, lens, want = [], [], []
+    for dev in range(ndev):
+        d = torch.randint(0, 256, (4 << 20,), dtype=torch.uint8, device=f"cuda:{dev}")
+        h = d.cpu().numpy()
+        datas.append((d, h))
+    for i in range(600):
+        dev = rng.randrange(ndev)
+        d, h = datas[dev]
+        o, n = rng.randrange(0, 1 << 20), rng.choice([0, 5, 4096, 65536, rng.randrange(1, 3 << 20)])
+        ptrs.append(d.data_ptr() + o)
+        lens.append(n)
+        want.append(h[o:o + n])
+    for alg in ("crc32c", "crc64nvme", "xxh64"):
+        seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in ptrs]
+        got = engine.checksum_list_devices(ALG[alg], ptrs, lens, seeds)
+        assert got == [oracle.checksum(alg, w, s) for w, s in zip(want, seeds)], alg
+    entries, outs = [], []
+    for dev, (d, h) in enumerate(datas):
+        out = torch.empty(64, dtype=torch.int32, device=f"cuda:{dev}")
+        outs.append(out)
+        entries.append((dev, d, 65536, 65536, 64, None, out, None))
+    engine.checksum_devices(ALG["crc32c"], entries)
+    for dev, (d, h) in enumerate(datas):
+        assert engine.as_unsigned(outs[dev]) == [oracle.crc("crc32c", h[i * 65536:(i + 1) * 65536]) for i in range(64)]

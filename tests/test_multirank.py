@@ -1,6 +1,8 @@
 """CPU, world_size 2 over gloo: the round-robin sharding and result gather used for multi-GPU
-batches (BASELINE.json config 4).  Each rank 'computes' its shard with the oracle standing in for
-its GPU (test infrastructure); the gathered, re-ordered results must equal a single-rank run."""
+batches (BASELINE.json config 4).  Each rank computes its shard through the engine's own C ABI
+(aws_crt_amd_host_submit / aws_checksums_*_ex: with no device visible the library serves host memory
+on its host path, exactly as it would on a rank whose GPU failed); the gathered, re-ordered results
+must equal the oracle's single-rank answer."""
 import os
 import random
 
@@ -22,7 +24,11 @@ def test_shard_partition_is_exact():
 
 
 def _worker(rank, world, port, q):
+    import ctypes
+
     import torch.distributed as dist
+
+    import aws_crt_amd as eng
     from oracle import oracle
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -30,7 +36,13 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rng = random.Random(1234)  # same buffers on every rank
     bufs = [rng.randbytes(rng.choice([0, 5, 100, 8192])) for _ in range(101)]
-    got = sharding.sharded_checksums(len(bufs), lambda idx: [oracle.crc("crc32c", bufs[i]) for i in idx])
+    keep = [ctypes.create_string_buffer(b, max(len(b), 1)) for b in bufs]
+
+    def shard(idx):
+        idx = list(idx)
+        return eng.host_job(eng.CRC32C, [ctypes.addressof(keep[i]) for i in idx], [len(bufs[i]) for i in idx])
+
+    got = sharding.sharded_checksums(len(bufs), shard)
     want = [oracle.crc("crc32c", b) for b in bufs]
     q.put((rank, got == want))
     dist.destroy_process_group()
@@ -47,6 +59,8 @@ def test_slice_bounds_partition_is_exact():
 
 def _split_worker(rank, world, port, q):
     import torch.distributed as dist
+
+    import aws_crt_amd as eng
     from oracle import oracle
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -55,15 +69,15 @@ def _split_worker(rank, world, port, q):
     data = random.Random(99).randbytes(3 * 1000 * 1000 + 17)  # same buffer on every rank
     ok = []
     for alg in ("crc32", "crc32c", "crc64nvme"):
-        got = sharding.split_buffer_crc(alg, len(data), lambda sl: oracle.crc(alg, data[sl.start:sl.stop]))
+        got = sharding.split_buffer_crc(alg, len(data), lambda sl: eng.crc(alg, data[sl.start:sl.stop]))
         ok.append(got == oracle.crc(alg, data))
     q.put((rank, all(ok)))
     dist.destroy_process_group()
 
 
 def test_gloo_world2_split_buffer_combine():
-    """One huge buffer split into contiguous per-rank slices, slice CRCs folded with the engine's
-    host-side Combine; the oracle stands in for each rank's GPU."""
+    """One huge buffer split into contiguous per-rank slices, slice CRCs (the engine's
+    aws_checksums_*_ex) folded with the engine's host-side Combine."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 30600 + random.Random().randrange(1000)
