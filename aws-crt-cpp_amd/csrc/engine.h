@@ -19,7 +19,7 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kGroupBytes = 64;  // bytes per lane per prefetch group (4 x 16-byte loads)
 constexpr int kVecPerGroup = kGroupBytes / 16;
 
-constexpr int kMaxBatches = 16;  // batches per strided launch (kernel arguments, SMEM-loaded)
+constexpr int kMaxBatches = 32;  // batches per strided launch (kernel arguments, 768 bytes)
 
 struct ScanParams {
     // ---- batch description: strided (base != 0) or list (d_ptrs != 0)

@@ -113,7 +113,7 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(
 
 /*
  * Several uniform batches of the same shape (stride, len, count), each with its own base, seeds and
- * results -- e.g. successive queued part batches.  CRC algorithms: up to 16 batches whose bases share
+ * results -- e.g. successive queued part batches.  CRC algorithms: up to 32 batches whose bases share
  * their alignment mod 16 go into ONE launch, so back-to-back batches do not each pay a launch's ramp
  * and tail; xxHash: one launch per batch.  Same per-buffer semantics as
  * aws_crt_amd_checksum_strided.  `batches` is a HOST array.
