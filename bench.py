@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-read-ceiling", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C3 / C5 / target-shape legs")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
+    ap.add_argument("--only-coalesced", action="store_true",
+                    help="profiling runs: every scan launch has the timed region's shape (no one-batch warm-up or timing "
+                         "launches), so a kernel-trace average is the dominant kernel's duration")
     return ap.parse_args()
 
 
@@ -290,8 +293,9 @@ def main():
     torch.cuda.synchronize()
     # every batch and every stream once (per-stream workspaces are allocated on first use), then the
     # requested warm-up steps the same way as the timed ones
-    for j in range(nb * len(streams)):
-        launch_group(j, j + 1, streams[j % len(streams)])
+    if not args.only_coalesced:
+        for j in range(nb * len(streams)):
+            launch_group(j, j + 1, streams[j % len(streams)])
     if args.warmup > 0:
         run_steps(args.warmup, G)
     torch.cuda.synchronize()
@@ -317,12 +321,13 @@ def main():
     nt = max(1, args.timing_launches)
     gsz = split(max(args.steps, 1), G)[1]  # batches per launch in the timed region
     kms, kmed = time_launches(eng, lambda i, st: launch_group(i * gsz, i * gsz + gsz, st), streams[0], nt)
-    kms1, _ = time_launches(eng, lambda i, st: launch_group(i, i + 1, st), streams[0], nt)
     roof = roofline(gsz * step_bytes, kms, KERNEL.get(alg, alg))
     roof["kernel_ms_median"] = round(kmed, 5)
     roof["timing_launches"] = nt
-    roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(step_bytes, kms1, "")["frac"],
-                            "bytes_per_launch": step_bytes}
+    if not args.only_coalesced:
+        kms1, _ = time_launches(eng, lambda i, st: launch_group(i, i + 1, st), streams[0], nt)
+        roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(step_bytes, kms1, "")["frac"],
+                                "bytes_per_launch": step_bytes}
     roof["traffic"] = None
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
@@ -335,7 +340,7 @@ def main():
             pass
 
     # secondary denominator: the streaming-read ceiling of a one-batch launch
-    if not args.no_read_ceiling:
+    if not args.no_read_ceiling and not args.only_coalesced:
         rc_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, step_bytes, stream=st,
                                                                      base_offset=(i % nb) * step_bytes), streams[0], nt)
         roof["single_batch"]["read_ceiling_kernel_ms"] = round(rc_ms, 5)
