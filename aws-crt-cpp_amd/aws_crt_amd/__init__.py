@@ -169,19 +169,34 @@ class _Batch(ctypes.Structure):
     _fields_ = [("d_base", ctypes.c_void_p), ("d_seeds", ctypes.c_void_p), ("d_out", ctypes.c_void_p)]
 
 
+class BatchSet:
+    """A prepared submission of several uniform batches of one shape (aws_crt_amd_checksum_batches):
+    the descriptor array is built once, like a producer filling a submission queue, and `run()` only
+    submits it.  `batches`: (base address / tensor, seeds tensor or None, out tensor) per batch."""
+
+    def __init__(self, alg: int, batches, stride: int, length: int, count: int):
+        self.n = len(batches)
+        self.arr = (_Batch * max(self.n, 1))()
+        for i, (base, seeds, out) in enumerate(batches):
+            self.arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+            self.arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
+            self.arr[i].d_out = out.data_ptr()
+        self.args = (alg, self.arr, self.n, stride, length, count)
+        L = lib()
+        self.fn = L.aws_crt_amd_checksum_batches
+        self.fn.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
+                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+
+    def run(self, stream=None) -> None:
+        rc = self.fn(*self.args, _stream_handle(stream))
+        if rc != 0:
+            _check(rc)
+
+
 def checksum_batches(alg: int, batches, stride: int, length: int, count: int, stream=None) -> None:
     """Several uniform batches of one shape, each (base address, seeds tensor or None, out tensor),
     coalesced into as few launches as the engine allows (aws_crt_amd_checksum_batches)."""
-    n = len(batches)
-    arr = (_Batch * max(n, 1))()
-    for i, (base, seeds, out) in enumerate(batches):
-        arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
-        arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
-        arr[i].d_out = out.data_ptr()
-    L = lib()
-    L.aws_crt_amd_checksum_batches.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
-                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
-    _check(L.aws_crt_amd_checksum_batches(alg, arr, n, stride, length, count, _stream_handle(stream)))
+    BatchSet(alg, batches, stride, length, count).run(stream)
 
 
 def host_job(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):

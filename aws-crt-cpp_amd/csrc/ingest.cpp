@@ -107,6 +107,32 @@ struct JobImpl {
         }                                                                                                  \
     } while (0)
 
+// Lanes are cached per device and reused by later jobs: pinning 96 MiB of mirrors and allocating the
+// device slots costs tens of milliseconds, as much as moving a few GiB over PCIe.
+std::mutex g_lane_mu;
+std::vector<std::vector<Lane *>> g_free_lanes;
+
+void lane_free(Lane &L);
+
+Lane *lane_take(int dev) {
+    std::lock_guard<std::mutex> g(g_lane_mu);
+    if ((int)g_free_lanes.size() <= dev) g_free_lanes.resize((size_t)dev + 1);
+    auto &v = g_free_lanes[(size_t)dev];
+    if (v.empty()) return new Lane;
+    Lane *l = v.back();
+    v.pop_back();
+    return l;
+}
+void lane_give(Lane *l, bool healthy) {
+    if (!healthy) {
+        lane_free(*l);
+        delete l;
+        return;
+    }
+    std::lock_guard<std::mutex> g(g_lane_mu);
+    g_free_lanes[(size_t)l->dev].push_back(l);
+}
+
 void lane_free(Lane &L) {
     // nothing may still be queued on the lane's streams when its buffers go (an early error return)
     if (L.copy) (void)hipStreamSynchronize(L.copy);
@@ -127,25 +153,28 @@ void lane_free(Lane &L) {
 
 // Worker for one device: pieces `mine` (indices into job->pieces, in order) through the 3-slot ring
 void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) {
-    Lane L;
-    L.dev = dev;
+    Lane *lp = lane_take(dev);
+    Lane &L = *lp;
     struct Guard {
-        Lane &l;
-        ~Guard() { lane_free(l); }
-    } guard{L};
+        Lane *l;
+        JobImpl *job;
+        ~Guard() { lane_give(l, job->rc.load() == 0); }
+    } guard{lp, job};
     LANE_TRY(hipSetDevice(dev));
-    LANE_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
-    LANE_TRY(hipStreamCreateWithFlags(&L.comp, hipStreamNonBlocking));
     const size_t osz = job->alg == AWS_CRT_AMD_CRC64NVME ? 8 : 4;
-    for (int k = 0; k < kSlots; ++k) {
-        LANE_TRY(hipMalloc(&L.dslot[k], kSlotBytes));
-        LANE_TRY(hipHostMalloc(&L.hmirror[k], kSlotBytes, hipHostMallocDefault));
-        LANE_TRY(hipMalloc(&L.dres[k], kMaxPiecesPerSlot * 8));
-        LANE_TRY(hipMalloc(&L.dseed[k], kMaxPiecesPerSlot * 8));
-        LANE_TRY(hipHostMalloc(&L.hres[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
-        LANE_TRY(hipHostMalloc(&L.hseed[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
-        LANE_TRY(hipEventCreateWithFlags(&L.copied[k], hipEventDisableTiming));
-        LANE_TRY(hipEventCreateWithFlags(&L.done[k], hipEventDisableTiming));
+    if (L.dev < 0) {  // a new lane (the pinned mirrors are allocated on first pageable use)
+        L.dev = dev;
+        LANE_TRY(hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking));
+        LANE_TRY(hipStreamCreateWithFlags(&L.comp, hipStreamNonBlocking));
+        for (int k = 0; k < kSlots; ++k) {
+            LANE_TRY(hipMalloc(&L.dslot[k], kSlotBytes));
+            LANE_TRY(hipMalloc(&L.dres[k], kMaxPiecesPerSlot * 8));
+            LANE_TRY(hipMalloc(&L.dseed[k], kMaxPiecesPerSlot * 8));
+            LANE_TRY(hipHostMalloc(&L.hres[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
+            LANE_TRY(hipHostMalloc(&L.hseed[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
+            LANE_TRY(hipEventCreateWithFlags(&L.copied[k], hipEventDisableTiming));
+            LANE_TRY(hipEventCreateWithFlags(&L.done[k], hipEventDisableTiming));
+        }
     }
     std::vector<const void *> dptrs;
     std::vector<size_t> dlens;
@@ -202,6 +231,10 @@ void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) {
             src_end = src + pc.len;
             const uint8_t *from = src;
             if (pc.len && !cur_pinned) {
+                if (!mir) {
+                    LANE_TRY(hipHostMalloc(&L.hmirror[k], kSlotBytes, hipHostMallocDefault));
+                    mir = (uint8_t *)L.hmirror[k];
+                }
                 std::memcpy(mir + off, src, pc.len);
                 from = mir + off;
             }

@@ -32,10 +32,13 @@ def main():
     ap.add_argument("--kernel", default="crc32_stream_kernel")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--bytes-per-launch", type=int, required=True)
+    ap.add_argument("--batches-per-launch", type=int, default=1)
+    ap.add_argument("--source", default="", help="where the counter CSV came from (recorded in the output)")
     a = ap.parse_args()
     f = per_dispatch(a.fetch, a.kernel)["FETCH_SIZE"]
     fetch_bytes = 2 * 1024 * statistics.median(f)
-    rec = {"workload": a.workload, "kernel": a.kernel, "dispatches": len(f),
+    rec = {"workload": a.workload, "batches_per_launch": a.batches_per_launch, "source": a.source,
+           "kernel": a.kernel, "dispatches": len(f),
            "hbm_bytes_per_launch": round(fetch_bytes), "algorithmic_bytes_per_launch": a.bytes_per_launch,
            "traffic_over_algorithmic": round(fetch_bytes / a.bytes_per_launch, 4),
            "method": "2 x 1024 x median FETCH_SIZE per dispatch (gfx950 half-count correction)"}

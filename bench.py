@@ -285,10 +285,16 @@ def main():
     def launch_group(i0, i1, st):
         eng.checksum_batches(ALG[alg], [batch(i) for i in range(i0, i1)], L, L, count, stream=st)
 
-    def run_steps(k, g_):
+    def prepare(k, g_):
+        """the submissions of k steps in launches of <= g_ batches (descriptors built up front, as a
+        producer fills a submission queue), alternating over the streams"""
         cuts = split(k, g_)
-        for j in range(len(cuts) - 1):
-            launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
+        return [(eng.BatchSet(ALG[alg], [batch(i) for i in range(cuts[j], cuts[j + 1])], L, L, count),
+                 streams[j % len(streams)]) for j in range(len(cuts) - 1)]
+
+    def run_steps(k, g_):
+        for bs, st in prepare(k, g_):
+            bs.run(st)
 
     torch.cuda.synchronize()
     # every batch and every stream once (per-stream workspaces are allocated on first use), then the
@@ -302,10 +308,11 @@ def main():
 
     if world > 1:
         dist.barrier()
+    subs = prepare(args.steps, G) if args.steps > 0 else []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if args.steps > 0:
-        run_steps(args.steps, G)
+    for bs, st in subs:
+        bs.run(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
