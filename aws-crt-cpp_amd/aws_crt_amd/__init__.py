@@ -199,31 +199,50 @@ def checksum_batches(alg: int, batches, stride: int, length: int, count: int, st
     BatchSet(alg, batches, stride, length, count).run(stream)
 
 
+class HostJob:
+    """A prepared host-ingest job (aws_crt_amd_host_submit / aws_crt_amd_job_wait) over host buffers
+    given by raw addresses: the argument arrays are built once; `run()` submits and waits (the C
+    calls only); `results()` reads them back (XXH3_128: 128-bit ints)."""
+
+    def __init__(self, alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):
+        L = lib()
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.aws_crt_amd_host_submit.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp,
+                                              ctypes.c_int, ctypes.POINTER(vp)]
+        L.aws_crt_amd_job_wait.argtypes = [vp]
+        L.aws_crt_amd_job_last_error.restype = ctypes.c_char_p
+        self.L, self.alg, self.n, self.ndevices = L, alg, len(ptrs), ndevices
+        n = self.n
+        self.P = (vp * max(n, 1))(*ptrs)
+        self.S = (sz * max(n, 1))(*lens)
+        T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
+        self.out = (T * max(n * (2 if alg == XXH3_128 else 1), 1))()
+        self.sd = (T * max(n, 1))(*seeds) if seeds is not None else None
+
+    def run(self) -> None:
+        vp = ctypes.c_void_p
+        job = vp()
+        rc = self.L.aws_crt_amd_host_submit(self.alg, self.P, self.S, self.n,
+                                            ctypes.cast(self.sd, vp) if self.sd is not None else None,
+                                            ctypes.cast(self.out, vp), self.ndevices, ctypes.byref(job))
+        if rc == 0:
+            rc = self.L.aws_crt_amd_job_wait(job)
+        if rc != 0:
+            raise EngineError(f"host job failed ({rc}): {self.L.aws_crt_amd_job_last_error().decode()}")
+
+    def results(self) -> list:
+        out, n = self.out, self.n
+        if self.alg == XXH3_128:
+            return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
+        return list(out[:n]) if n else []
+
+
 def host_job(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):
     """aws_crt_amd_host_submit + aws_crt_amd_job_wait over host buffers given by raw addresses; returns
     the results (XXH3_128: 128-bit ints).  Synchronous from Python's point of view."""
-    L = lib()
-    n = len(ptrs)
-    vp, sz = ctypes.c_void_p, ctypes.c_size_t
-    L.aws_crt_amd_host_submit.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp, ctypes.c_int,
-                                          ctypes.POINTER(vp)]
-    L.aws_crt_amd_job_wait.argtypes = [vp]
-    L.aws_crt_amd_job_last_error.restype = ctypes.c_char_p
-    P = (vp * max(n, 1))(*ptrs)
-    S = (sz * max(n, 1))(*lens)
-    T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
-    out = (T * max(n * (2 if alg == XXH3_128 else 1), 1))()
-    sd = (T * max(n, 1))(*seeds) if seeds is not None else None
-    job = vp()
-    rc = L.aws_crt_amd_host_submit(alg, P, S, n, ctypes.cast(sd, vp) if sd is not None else None, ctypes.cast(out, vp),
-                                   ndevices, ctypes.byref(job))
-    if rc == 0:
-        rc = L.aws_crt_amd_job_wait(job)
-    if rc != 0:
-        raise EngineError(f"host job failed ({rc}): {L.aws_crt_amd_job_last_error().decode()}")
-    if alg == XXH3_128:
-        return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
-    return [int(out[i]) for i in range(n)]
+    job = HostJob(alg, ptrs, lens, seeds, ndevices)
+    job.run()
+    return job.results()
 
 
 def register_host(addr: int, nbytes: int) -> None:
