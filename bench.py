@@ -169,7 +169,7 @@ KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc6
           "xxh64": "xxh64_quad_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
 
 
-def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=4,
+def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,
                cpu_seconds=0.5, do_cpu=True):
     """One BASELINE config: `steps` steps of `nbuf` x L bytes (nb rotating batches), pipelined over
     the streams; roofline from `timing` serialised launches; CPU baseline on `cpu_bufs` buffers."""
@@ -204,6 +204,9 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
            "roofline": roofline(per * step_bytes, kms, KERNEL.get(alg, alg))}
     if do_cpu:
+        # the whole step's buffers (buffers round-robin over the threads, so a sample
+        # of fewer buffers than threads would leave cores idle)
+        cpu_bufs = nbuf if cpu_bufs is None else cpu_bufs
         torch.cuda.synchronize()
         gpu0 = eng.as_unsigned(outs[0])
         host = data[: cpu_bufs * L].cpu().numpy()
