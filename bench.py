@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-read-ceiling", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C3 / C5 / target-shape legs")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="one process drives --gpus devices (the engine's in-process fan-out: one HIP stream per GPU, "
+                         "batches sharded round-robin, no collective) instead of one rank per GPU")
     ap.add_argument("--only-coalesced", action="store_true",
                     help="profiling runs: every scan launch has the timed region's shape (no one-batch warm-up or timing "
                          "launches), so a kernel-trace average is the dominant kernel's duration")
@@ -255,8 +258,70 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
                       f"memory in one host job, results to host memory"}
 
 
+def main_inproc(args):
+    """In-process multi-device mode: each GPU holds its own rotating C2 batches; the steps are sharded
+    round-robin over the devices (step i -> device i % N) and each device's share is submitted as
+    coalesced launches on that device's stream, all devices at once; the timed region ends when every
+    device is done.  value = all devices' bytes / that time."""
+    import torch
+    import aws_crt_amd as eng
+
+    ndev = min(max(1, args.gpus), torch.cuda.device_count())
+    alg, count, L = args.alg, args.buffers, args.buffer_bytes
+    G = max(1, min(32, args.coalesce))
+    step_bytes, nb = count * L, max(1, args.batches)
+    per = []
+    for dv in range(ndev):
+        torch.cuda.set_device(dv)
+        eng.init()
+        g = torch.Generator(device=f"cuda:{dv}")
+        g.manual_seed(0x5EED + dv)
+        data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=f"cuda:{dv}", generator=g)
+        outs = [torch.empty(count, dtype=torch.int64 if alg in WIDE else torch.int32, device=f"cuda:{dv}") for _ in range(nb)]
+        per.append((data, outs, torch.cuda.Stream(device=f"cuda:{dv}")))
+
+    def prepare(k):
+        subs = []
+        for dv in range(ndev):
+            data, outs, st = per[dv]
+            mine = list(range(dv, k, ndev))  # round-robin steps
+            cuts = split(len(mine), G)
+            for j in range(len(cuts) - 1):
+                bs = [(data.data_ptr() + (mine[i] // ndev % nb) * step_bytes, None, outs[mine[i] // ndev % nb])
+                      for i in range(cuts[j], cuts[j + 1])]
+                subs.append((dv, eng.BatchSet(ALG[alg], bs, L, L, count), st))
+        return subs
+
+    def run(subs):
+        for dv, bs, st in subs:
+            torch.cuda.set_device(dv)
+            bs.run(st)
+        for dv in range(ndev):
+            torch.cuda.synchronize(dv)
+
+    run(prepare(max(args.warmup, ndev)))
+    subs = prepare(args.steps)
+    for dv in range(ndev):
+        torch.cuda.synchronize(dv)
+    t0 = time.perf_counter()
+    run(subs)
+    el = time.perf_counter() - t0
+    value = args.steps * step_bytes / el / 2**30
+    print(json.dumps({
+        "metric": "GiB/s CRC32C over device-resident buffers; % of HBM read peak", "value": round(value, 2),
+        "unit": "GiB/s", "n_gpus": ndev, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes on device)",
+        "config": {"workload": f"C2: {count} x {L // 1024} KiB per step, {alg.upper()}, steps round-robin over "
+                               f"{ndev} GPU(s) of one process", "launch": f"in-process fan-out, up to {G} batches per launch, "
+                               "one HIP stream per GPU", "parallelism": f"in-process, {ndev} device(s), no collective"},
+        "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / ndev / HBM_PEAK_GBS, 2)}), flush=True)
+
+
 def main():
     args = parse()
+    if args.inproc:
+        return main_inproc(args)
     import torch
     import torch.distributed as dist
     import aws_crt_amd as eng
