@@ -82,6 +82,28 @@ def cpu_tier() -> str:
     return lib().aws_crt_amd_cpu_tier().decode()
 
 
+class CpuBatch:
+    """A prepared aws_crt_amd_cpu_batch call (argument arrays built once; `run()` is the C call only)."""
+
+    def __init__(self, alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, threads: int = 1):
+        n = len(ptrs)
+        self.n, self.alg, self.threads = n, alg, threads
+        self.P = (ctypes.c_void_p * max(n, 1))(*ptrs)
+        self.S = (ctypes.c_size_t * max(n, 1))(*lens)
+        self.sd = (ctypes.c_uint64 * max(n, 1))(*seeds) if seeds is not None else None
+        self.out = (ctypes.c_uint64 * max(n * (2 if alg == XXH3_128 else 1), 1))()
+        self.fn = lib().aws_crt_amd_cpu_batch
+
+    def run(self) -> None:
+        _check(self.fn(self.alg, self.P, self.S, self.n, self.sd, self.out, self.threads))
+
+    def results(self) -> list:
+        out, n = self.out, self.n
+        if self.alg == XXH3_128:
+            return [(out[2 * i] << 64) | out[2 * i + 1] for i in range(n)]
+        return list(out[:n]) if n else []
+
+
 def cpu_batch(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, threads: int = 1) -> list:
     """The library's host path over host buffers (raw addresses), `threads` std::threads; one value
     per buffer (XXH3_128: 128-bit ints)."""
