@@ -14,7 +14,8 @@ Launches: steps are submitted through aws_crt_amd_checksum_batches, which puts u
 queued batches (same shape, separate bases / results) into ONE launch, so back-to-back batches do
 not each pay a launch's ramp and tail (DESIGN.md §3 "multi-batch launches"); the K steps are split
 into ceil(K / coalesce) near-equal launches, alternating over --branches HIP streams.  --coalesce 1 is
-one launch per batch.
+one launch per batch.  The resident pool holds at least as many distinct batches as one launch
+(32 x 64 MiB = 2 GiB at the default), so no launch reads any byte twice.
 
 Roofline (`roofline`): the dominant kernel's algorithmic bytes per launch (1 byte read per payload
 byte) / its mean dispatch duration, from HIP events stamped by the dispatch itself
@@ -171,6 +172,12 @@ def split(k, g):
     return [k * i // n for i in range(n + 1)]
 
 
+def widest(k, g):
+    """batches in the largest launch of split(k, g)"""
+    c = split(k, g)
+    return max(b - a for a, b in zip(c, c[1:]))
+
+
 KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc64nvme": "crc64_stream4_kernel",
           "xxh64": "xxh64_quad_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
 
@@ -182,6 +189,7 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
     import torch
 
     step_bytes = nbuf * L
+    nb = max(nb, widest(steps, coalesce))  # no launch reads a batch twice
     g = torch.Generator(device=dev)
     g.manual_seed(hash(name) & 0xFFFF)
     data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
@@ -343,7 +351,9 @@ def main():
     alg, count, L = args.alg, args.buffers, args.buffer_bytes
     G = max(1, min(32, args.coalesce))
     step_bytes = count * L
-    nb = max(1, args.batches)
+    # resident batches: at least --batches, and never fewer than a launch holds, so no launch reads a
+    # batch twice (aliased batches in one launch would hit in L2 / the Infinity Cache)
+    nb = max(1, args.batches, widest(max(args.steps, 1), G), widest(max(args.warmup, 1), G))
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED + rank)
     data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
@@ -400,7 +410,7 @@ def main():
 
     # dominant kernel: launches of G batches (the timed region's launch shape), then one-batch launches
     nt = max(1, args.timing_launches)
-    gsz = split(max(args.steps, 1), G)[1]  # batches per launch in the timed region
+    gsz = widest(max(args.steps, 1), G)  # batches per launch in the timed region
     kms, kmed = time_launches(eng, lambda i, st: launch_group(i * gsz, i * gsz + gsz, st), streams[0], nt)
     roof = roofline(gsz * step_bytes, kms, KERNEL.get(alg, alg))
     roof["kernel_ms_median"] = round(kmed, 5)
