@@ -1145,9 +1145,13 @@ __device__ __forceinline__ uint64_t basis64_rt(uint32_t t, uint32_t e) {  // t w
 }
 
 // COPIES = 8: the layout above (two 64 KiB regions).  COPIES = 4 (crc64_stream4_kernel): one
-// 64 KiB region, row e = the low dword's four tables in bytes [0, 128) and the high dword's in
-// [128, 256), quarter q = 4 copies x 8 bytes; a ds_read_b64 half-wave then meets 16 slots (2-way
-// bank conflicts) but two workgroups share a CU.
+// 64 KiB region in which the 256-byte row of entry e holds the table of byte t of a (T'_(7-t)) at
+// bytes [32 t, 32 t + 32), 4 copies x 8 bytes.  A ds_read_b64 half-wave is conflict-free when its 32
+// lanes use 32 distinct 8-byte columns (bank pair = column, whatever the row): lane group
+// jp = (lane >> 2) & 7 reads, in table slot k < 4, byte q = (k + jp) & 3 of one dword -- the low one
+// for jp < 4, the high one for jp >= 4 -- with copy lane & 3, so the half-wave covers 8 tables x 4
+// copies; slots 4..7 read the other dword.  (A layout with 4 tables per instruction met 16 columns:
+// 2-way conflicts.)  tests/test_braid64_model.py::test_four_copy_layout checks the schedule.
 constexpr uint32_t kB64x4T0Off = 65536;
 constexpr uint32_t kB64x4Lds = kB64x4T0Off + 2048;
 
@@ -1157,33 +1161,46 @@ struct Braid64 {
     static constexpr int W = 64;
     const char *L;
     uint32_t cst[4], csth[4], sel[4];
-    uint64_t kl;  // K_l = x^(-64 l)
+    uint32_t lowmask;  // COPIES = 4: ~0 for lanes whose slots 0..3 read the low dword
+    uint64_t kl;       // K_l = x^(-64 l)
 
     __device__ void init(const char *lds, int lane) {
         L = lds;
-        const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & (COPIES - 1u);
+        if (COPIES == 8) {
+            const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t q = (k + j) & 3u;
-            if (COPIES == 8) {
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t q = (k + j) & 3u;
                 cst[k] = (q << 6) | (cp << 3);
                 csth[k] = cst[k] | 0x10000u;
                 sel[k] = 0x0c060004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a, byte2 <- region
-            } else {
-                cst[k] = (q << 5) | (cp << 3);
-                csth[k] = cst[k] | 0x80u;         // high dword's tables: second half of the row
-                sel[k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of a
+            }
+            lowmask = ~0u;
+        } else {
+            const uint32_t jp = ((uint32_t)lane >> 2) & 7u, cp = (uint32_t)lane & 3u;
+            const bool lowfirst = jp < 4;
+            lowmask = lowfirst ? ~0u : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t q = (k + jp) & 3u;
+                const uint32_t t1 = lowfirst ? q : 4u + q, t2 = lowfirst ? 4u + q : q;  // byte t of a
+                cst[k] = (t1 << 5) | (cp << 3);
+                csth[k] = (t2 << 5) | (cp << 3);
+                sel[k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of the dword
             }
         }
     }
     // a * x^(8*512) ^ wn
     __device__ __forceinline__ uint64_t step_x(uint64_t a, uint64_t wn) const {
         const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+        // COPIES = 4: slots 0..3 read dword ma, slots 4..7 dword mb (per lane half, see the layout)
+        const uint32_t ma = COPIES == 8 ? lo : (lo & lowmask) | (hi & ~lowmask);
+        const uint32_t mb = COPIES == 8 ? hi : (hi & lowmask) | (lo & ~lowmask);
         uint64_t v[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            v[k] = lds64(L, __builtin_amdgcn_perm(cst[k], lo, sel[k]));
-            v[4 + k] = lds64(L, __builtin_amdgcn_perm(csth[k], hi, sel[k]));
+            v[k] = lds64(L, __builtin_amdgcn_perm(cst[k], ma, sel[k]));
+            v[4 + k] = lds64(L, __builtin_amdgcn_perm(csth[k], mb, sel[k]));
         }
         uint32_t rl = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]), (uint32_t)v[3], (uint32_t)v[4]);
         rl = xor3(xor3(rl, (uint32_t)v[5], (uint32_t)v[6]), (uint32_t)v[7], (uint32_t)wn);
@@ -1330,19 +1347,19 @@ __device__ __forceinline__ void b64_build_tables(char *lds) {
     if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
 }
 
-// the 4-copy layout (Braid64<POLY, 4>) from 512 threads: thread i fills table t = i >> 6 (wave-
-// uniform) for entries (i & 63) + 64 n, n < 4, two 16-byte stores (4 copies) each; then T0
+// the 4-copy layout (Braid64<POLY, 4>) from 512 threads: thread i fills the table of byte
+// t = i >> 6 of a (T'_(7-t), wave-uniform) for entries (i & 63) + 64 n, n < 4, two 16-byte stores
+// (4 copies) each; then T0
 template <uint64_t POLY>
 __device__ __forceinline__ void b64x4_build_tables(char *lds) {
     const uint32_t i = threadIdx.x;
     const uint32_t t = __builtin_amdgcn_readfirstlane(i >> 6);
-    const uint32_t reg = t >= 4 ? 0u : 1u, q = t >= 4 ? 7u - t : 3u - t;
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const uint32_t e = (i & 63u) + 64u * n;
-        const uint64_t v = basis64_rt<POLY>(t, e);
+        const uint64_t v = basis64_rt<POLY>(7u - t, e);
         const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
-        char *row = lds + (e << 8) + (reg << 7) + (q << 5);
+        char *row = lds + (e << 8) + (t << 5);
         *(v4u *)(row + (((i >> 2) & 1u) << 4)) = vv;
         *(v4u *)(row + ((((i >> 2) & 1u) ^ 1u) << 4)) = vv;
     }

@@ -180,45 +180,57 @@ def test_lds_schedule_is_conflict_free_and_complete(br):
 
 
 def test_four_copy_layout(br):
-    """crc64_stream4_kernel's 64 KiB layout (Braid64<POLY, 4>, b64x4_build_tables): row e = the low
-    dword's tables in bytes [0, 128), the high dword's in [128, 256), quarter q = 4 copies x 8 B.
-    The table build (thread i: table t = i >> 6, entries (i & 63) + 64 n, both 16-byte halves)
-    fills every address the lookups form with the right entry, the lookups reproduce the slice-by-8
-    step, and a ds_read_b64 half-wave meets each bank pair at most twice (2-way conflicts)."""
+    """crc64_stream4_kernel's 64 KiB layout (Braid64<POLY, 4>, b64x4_build_tables): row e holds the
+    table of byte t of a (T'_(7-t)) at bytes [32 t, 32 t + 32), 4 copies x 8 B.  The table build
+    (thread i: byte t = i >> 6, entries (i & 63) + 64 n, both 16-byte halves) fills every address the
+    lookups form with the right entry; the lookups (lane group jp = (lane >> 2) & 7 reads byte
+    (k + jp) & 3 of the low dword in slots 0..3 when jp < 4, of the high dword otherwise, and the
+    other dword in slots 4..7) reproduce the slice-by-8 step; and every ds_read_b64 half-wave meets
+    32 distinct bank pairs (conflict-free), whatever the entries."""
     lds = {}
     for i in range(512):
         t = i >> 6
-        reg, q = (0, 7 - t) if t >= 4 else (1, 3 - t)
         for n in range(4):
             e = (i & 63) + 64 * n
-            row = (e << 8) + (reg << 7) + (q << 5)
+            row = (e << 8) + (t << 5)
             for half in range(2):
                 for c in range(2):
-                    lds[row + (half << 4) + 8 * c] = br.Tp[t][e]
-    assert len(lds) == 256 * 2 * 4 * 4  # 64 KiB of 8-byte entries, all distinct addresses
+                    lds[row + (half << 4) + 8 * c] = br.Tp[7 - t][e]
+    assert len(lds) == 256 * 8 * 4  # 64 KiB of 8-byte entries, all distinct addresses
+
+    def slots(lane):
+        """(column offset, source dword, byte q) of the 8 table slots of a lane"""
+        jp, cp = (lane >> 2) & 7, lane & 3
+        low = jp < 4
+        out = []
+        for second in (False, True):
+            for k in range(4):
+                q = (k + jp) & 3
+                hi_src = (not low) != second  # first set: low dword iff jp < 4; second set: the other
+                t = (4 if hi_src else 0) + q
+                out.append(((t << 5) | (cp << 3), hi_src, q))
+        return out
 
     def step_lds4(a, lane):
-        j, cp = (lane >> 3) & 3, lane & 3
         v = 0
-        for k in range(4):
-            q = (k + j) & 3
-            cst = (q << 5) | (cp << 3)
-            v ^= lds[cst | (((a >> (8 * q)) & 255) << 8)]               # low dword: region 0
-            v ^= lds[(cst | 0x80) | (((a >> (32 + 8 * q)) & 255) << 8)]  # high dword: +128
+        for col, hi_src, q in slots(lane):
+            e = (a >> ((32 if hi_src else 0) + 8 * q)) & 255
+            v ^= lds[col | (e << 8)]
         return v
 
     rnd = random.Random(5)
-    for _ in range(200):
+    for _ in range(300):
         a = rnd.getrandbits(64)
         assert step_lds4(a, rnd.randrange(64)) == br.step(a)
-    for k in range(4):
-        for hi in (0, 1):
-            use = {}
-            for lane in range(32):
-                j, cp = (lane >> 3) & 3, lane & 3
-                addr = ((((k + j) & 3) << 5) | (cp << 3) | (hi << 7)) + (rnd.randrange(256) << 8)
-                use[(addr >> 3) & 31] = use.get((addr >> 3) & 31, 0) + 1
-            assert max(use.values()) <= 2
+    for lane in range(64):  # each lane reads each byte of a exactly once
+        assert sorted((4 if h else 0) + q for _, h, q in slots(lane)) == list(range(8))
+    for s_ in range(8):
+        for g in (0, 32):
+            pairs = set()
+            for lane in range(g, g + 32):
+                addr = slots(lane)[s_][0] + (rnd.randrange(256) << 8)
+                pairs.add((addr >> 3) & 31)
+            assert len(pairs) == 32
 
 
 def test_step_is_multiply_by_x4096(br):
