@@ -735,8 +735,9 @@ AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_e
 }
 
 // Measurement hook: one launch of the streaming-read ceiling kernel (crc_kernels.hip
-// read_ceiling_kernel) over [d_base, d_base + bytes), in the W=32 streaming scan's small-batch shape
-// (one 512-thread workgroup per CU).  Honours aws_crt_amd_debug_time_next_launch.
+// read_ceiling_kernel) over [d_base, d_base + bytes), in the W=32 streaming scan's launch shape
+// (512-thread workgroups, one per CU below 256 MiB, two above).  Honours
+// aws_crt_amd_debug_time_next_launch.
 AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t bytes, void *hip_stream) {
     Device *d;
     int rc = get_device(&d);
@@ -744,9 +745,11 @@ AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t by
     static DevBuf sink;  // one word per wave (practically never written)
     {
         std::lock_guard<std::mutex> g(d->mu);
-        if (!sink.p) HIP_TRY(hipMalloc(&sink.p, (size_t)d->cus * 8 * sizeof(uint32_t)));
+        if (!sink.p) HIP_TRY(hipMalloc(&sink.p, (size_t)d->cus * 2 * 8 * sizeof(uint32_t)));
     }
-    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)sink.p, d->cus, hip_stream, g_time_events);
+    // the streaming scan's geometry: one workgroup per CU below 256 MiB, two from there on
+    const int blocks = bytes >= kSmallBatchBytes ? 2 * d->cus : d->cus;
+    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)sink.p, blocks, hip_stream, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }

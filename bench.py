@@ -430,12 +430,18 @@ def main():
         except Exception:
             pass
 
-    # secondary denominator: the streaming-read ceiling of a one-batch launch
+    # secondary denominator: the streaming-read ceiling of a one-batch launch and
+    # of a launch of the timed region's size (the same bytes, read by an XOR-reduce kernel)
     if not args.no_read_ceiling and not args.only_coalesced:
         rc_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, step_bytes, stream=st,
                                                                      base_offset=(i % nb) * step_bytes), streams[0], nt)
         roof["single_batch"]["read_ceiling_kernel_ms"] = round(rc_ms, 5)
         roof["single_batch"]["read_ceiling_frac"] = roofline(step_bytes, rc_ms, "")["frac"]
+        rcg_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, gsz * step_bytes, stream=st), streams[0],
+                                  max(2, nt // 4))
+        roof["read_ceiling"] = {"kernel_ms": round(rcg_ms, 5), "frac": roofline(gsz * step_bytes, rcg_ms, "")["frac"],
+                                "scan_frac_of_ceiling": round(rcg_ms / kms, 4),
+                                "kernel": "read_ceiling_kernel: the scan's launch shape, 256-B non-temporal rows XOR-reduced"}
 
     cpu = e2e = None
     configs = {}
