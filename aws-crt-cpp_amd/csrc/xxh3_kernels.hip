@@ -305,9 +305,11 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 }
 
 // SPLIT: the full blocks' class sums were written by xxh3_blocksum_kernel (64 B per block at
-// p.d_sums + 8 (i nb + blk)); this wave only scrambles.  Lane l loads the two sums of class l & 3
-// for block g + (l >> 2): one coalesced 1 KiB load per 16 blocks, four loads in flight, and the
-// per-block values reach their class lanes by shuffles that do not depend on the accumulators.
+// p.d_sums + 8 (i nb + blk)); this wave only scrambles, one accumulator per lane: lane l owns
+// accumulator c = l & 7 and loads its sum for block g + (l >> 3) (one coalesced 512-byte load per 8
+// blocks, sixteen loads in flight); the per-block values reach the lanes of their accumulator by
+// shuffles that do not depend on the accumulators.  One scramble chain per lane per block (two in
+// the 4-class layout of the one-pass path) halves the serial instruction stream of a block.
 template <int BITS, bool ALIGNED, bool SPLIT = false>
 __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *ptr, uint64_t n, uint64_t seed, int lane) {
     const int s = lane >> 2, wp = lane & 3;
@@ -317,46 +319,45 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     uint64_t acc0 = init[2 * wp], acc1 = init[2 * wp + 1];
     const uint64_t nb = (n - 1) / 1024;
     const uint8_t *q = ptr + 16 * lane;
+    uint64_t accv = 0;  // SPLIT: accumulator l & 7
     if (SPLIT) {
         const uint64_t *S = p.d_sums + i * nb * 8;
-        constexpr int G = 16, DS = 4;
-        const uint64_t ng = (nb + G - 1) / G;
-        uint64_t x0[DS], x1[DS];
-        auto ldg = [&](uint64_t g, uint64_t &a, uint64_t &b) {
-            const uint64_t blk = g * G + (uint64_t)s;
-            if (blk < nb) {
-                const v2u64 v = *(const __attribute__((address_space(1))) v2u64 *)(S + blk * 8 + 2 * wp);
-                a = v.x;
-                b = v.y;
-            } else {
-                a = b = 0;
-            }
+        const int c8 = lane & 7, s8 = lane >> 3;
+        const uint64_t stv = sec64(128 + 8 * c8, seed);
+        accv = init[c8];
+        constexpr int G = 8, DS = 16;
+        // loads are unconditional (addresses clamped to the last block) so that the wait before a
+        // group's shuffles counts only that group's load: DS groups stay in flight
+        auto ldg = [&](uint64_t g) -> uint64_t {
+            uint64_t blk = g * G + (uint64_t)s8;
+            blk = blk < nb ? blk : nb - 1;
+            return *(const __attribute__((address_space(1))) uint64_t *)(S + blk * 8 + c8);
         };
+        auto group = [&](uint64_t xv, uint64_t cnt) {
+            uint64_t v[G];
 #pragma unroll
-        for (int d = 0; d < DS; ++d) ldg(d, x0[d], x1[d]);
-        for (uint64_t g = 0; g < ng; g += DS) {
+            for (int j = 0; j < G; ++j) v[j] = shfl64(xv, 8 * j + c8);
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if ((uint64_t)j < cnt) accv = scramble1(accv + v[j], stv);
+        };
+        uint64_t x[DS];
+#pragma unroll
+        for (int d = 0; d < DS; ++d) x[d] = ldg(d);
+        const uint64_t ng = (nb + G - 1) / G, nround = (nb / G) / DS;
+        uint64_t g = 0;
+        for (uint64_t r = 0; r < nround; ++r, g += DS) {
 #pragma unroll
             for (int d = 0; d < DS; ++d) {
-                if (g + d < ng) {
-                    const uint64_t base = (g + d) * G;
-                    const uint64_t cnt = nb - base < (uint64_t)G ? nb - base : (uint64_t)G;
-                    uint64_t v0[G], v1[G];
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        v0[j] = shfl64(x0[d], 4 * j + wp);
-                        v1[j] = shfl64(x1[d], 4 * j + wp);
-                    }
-                    ldg(g + d + DS, x0[d], x1[d]);
-#pragma unroll
-                    for (int j = 0; j < G; ++j) {
-                        if ((uint64_t)j < cnt) {
-                            acc0 = scramble1(acc0 + v0[j], st0);
-                            acc1 = scramble1(acc1 + v1[j], st1);
-                        }
-                    }
-                }
+                const uint64_t xv = x[d];
+                x[d] = ldg(g + DS + d);
+                group(xv, G);
             }
         }
+        // at most DS groups remain (the last may be partial); their sums are already in the ring
+#pragma unroll
+        for (int d = 0; d < DS; ++d)
+            if (g + d < ng) group(x[d], nb - (g + d) * G < (uint64_t)G ? nb - (g + d) * G : (uint64_t)G);
     } else {
         // D blocks per round: their lane contributions and class sums are independent of the
         // accumulators, so all D reductions issue together and only the scrambles stay serial
@@ -411,14 +412,22 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     }
     acc0 += class_sum(c0);
     acc1 += class_sum(c1);
-    // lanes 0..3 hold accumulators {0,1}, {2,3}, {4,5}, {6,7}
+    // lanes 0..3 hold accumulators {0,1}, {2,3}, {4,5}, {6,7} (the partial block's and last stripe's
+    // contributions, plus, in the one-pass layout, the full blocks'); SPLIT: lanes 0..7 hold the
+    // scrambled accumulators 0..7 of the full blocks
+    auto rl64 = [](uint64_t v, int l) -> uint64_t {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    };
     uint64_t acc[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        acc[2 * k] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(acc0 >> 32), k) << 32) |
-                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)acc0, k);
-        acc[2 * k + 1] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(acc1 >> 32), k) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)acc1, k);
+        acc[2 * k] = rl64(acc0, k);
+        acc[2 * k + 1] = rl64(acc1, k);
+        if (SPLIT) {
+            acc[2 * k] += rl64(accv, 2 * k) - init[2 * k];  // acc0 / acc1 started from init, accv too
+            acc[2 * k + 1] += rl64(accv, 2 * k + 1) - init[2 * k + 1];
+        }
     }
     if (lane != 0) return;
     auto mergeacc = [&](int off, uint64_t start) {
