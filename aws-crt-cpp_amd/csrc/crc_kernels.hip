@@ -1661,9 +1661,26 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
 // interleaving in one (the per-lane chain, not issue, then bounds a buffer: 8 B per round latency).
 // Each lane loads its words of four stripes per iteration, the next four in flight while these are
 // mixed in.  Lane 0 of the quad finishes (merge, remaining < 32 bytes, avalanche).
-__device__ __forceinline__ uint64_t ldw(const uint8_t *p, bool aligned) {
-    if (aligned) return *(const __attribute__((address_space(1))) uint64_t *)p;
-    return ld64u(p);
+// one global_load_dwordx2 whatever the alignment (the loads issue without a per-lane branch, so
+// the waits before the rounds count only the oldest slot)
+typedef uint64_t u64_any_align __attribute__((aligned(1)));
+__device__ __forceinline__ uint64_t ldw(const uint8_t *p) { return *(const __attribute__((address_space(1))) u64_any_align *)p; }
+
+// One round with the input product taken off the chain: the carried state is u = v + in * P2; the
+// round computes v' = rotl(u, 31) * P1 and returns u' = v' + y where y = next_in * P2 is computed
+// beforehand.  Dependent depth per round: two alignbits, then mad_u64_u32 (low product plus y) beside
+// two mul_lo (cross products), then one add3.
+__device__ __forceinline__ void xstep_y(uint32_t &ul, uint32_t &uh, uint64_t y) {
+    const uint32_t rl = __builtin_amdgcn_alignbit(ul, uh, 1), rh = __builtin_amdgcn_alignbit(uh, ul, 1);
+    const uint64_t m = (uint64_t)rl * (uint32_t)XP1 + y;
+    ul = (uint32_t)m;
+    uh = (uint32_t)(m >> 32) + rl * (uint32_t)(XP1 >> 32) + rh * (uint32_t)XP1;
+}
+// the same with y computed in this lane: the empty asm keeps the input product opaque, otherwise it
+// is re-associated into the chain's mad (a second dependent mad per round)
+__device__ __forceinline__ void xstep(uint32_t &ul, uint32_t &uh, uint64_t y) {
+    asm volatile("" : "+v"(y));
+    xstep_y(ul, uh, y);
 }
 
 // lane k of each quad, broadcast to the quad (DPP quad_perm [k,k,k,k])
@@ -1675,49 +1692,9 @@ __device__ __forceinline__ uint64_t quad_bcast(uint64_t v) {
     return ((uint64_t)h << 32) | l;
 }
 
-__global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
-    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
-    const int j = (int)(threadIdx.x & 3);
-    const bool valid = i < p.nbuf;
-    const uint8_t *ptr = nullptr;
-    uint64_t n = 0, seed = 0;
-    if (valid) {
-        ptr = (const uint8_t *)(p.d_ptrs ? p.d_ptrs[i] : p.base + i * p.stride);
-        n = p.d_ptrs ? p.d_lens[i] : p.len;
-        seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
-    }
-    const uint64_t ns = n >= 32 ? n / 32 : 0;
-    const bool aligned = ((uintptr_t)ptr & 7) == 0;
-    uint64_t v = seed + (j == 0 ? XP1 + XP2 : j == 1 ? XP2 : j == 2 ? 0ull : 0ull - XP1);
-    const uint8_t *q = ptr + 8 * j;
-    // kXxSlots x 4 stripes in flight per lane: an HBM load takes ~2 us, a round ~60-80 cycles of
-    // dependent 64-bit arithmetic; the kernel runs a few waves per CU, so registers are plentiful
-    constexpr int kXxSlots = 12;
-    uint64_t s = 0;
-    if (ns >= 4 * kXxSlots) {
-        uint64_t w[kXxSlots][4];
-#pragma unroll
-        for (int k = 0; k < kXxSlots; ++k)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) w[k][m] = ldw(q + 32 * (4 * k + m), aligned);
-        for (s = 4 * kXxSlots; s + 4 * kXxSlots <= ns; s += 4 * kXxSlots) {
-#pragma unroll
-            for (int k = 0; k < kXxSlots; ++k) {
-#pragma unroll
-                for (int m = 0; m < 4; ++m) v = xround(v, w[k][m]);
-#pragma unroll
-                for (int m = 0; m < 4; ++m) w[k][m] = ldw(q + 32 * (s + 4 * k + m), aligned);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kXxSlots; ++k)
-#pragma unroll
-            for (int m = 0; m < 4; ++m) v = xround(v, w[k][m]);
-    }
-    for (; s < ns; ++s) v = xround(v, ldw(q + 32 * s, aligned));
-    // lane 0 of the quad gathers v1..v4 (quad_perm DPP broadcasts of lanes 1..3)
-    const uint64_t v1 = quad_bcast<0>(v), v2 = quad_bcast<1>(v), v3 = quad_bcast<2>(v), v4 = quad_bcast<3>(v);
-    if (!valid || j != 0) return;
+// merge of the four lanes (n >= 32), the < 32-byte tail and the avalanche (XXH64 digest)
+__device__ __noinline__ uint64_t xxh64_finish(uint64_t v1, uint64_t v2, uint64_t v3, uint64_t v4, const uint8_t *ptr,
+                                              uint64_t n, uint64_t seed) {
     uint64_t h;
     if (n >= 32) {
         h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
@@ -1729,7 +1706,7 @@ __global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
         h = seed + XP5;
     }
     h += n;
-    const uint8_t *t = ptr + 32 * ns, *end = ptr + n;
+    const uint8_t *t = ptr + (n & ~31ull), *end = ptr + n;
     while (t + 8 <= end) {
         h ^= xround(0, ld64u(t));
         h = rotl64(h, 27) * XP1 + XP4;
@@ -1751,7 +1728,156 @@ __global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
     h ^= h >> 29;
     h *= XP3;
     h ^= h >> 32;
-    p.d_out[i] = h;
+    return h;
+}
+
+__global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+    const int j = (int)(threadIdx.x & 3);
+    const bool valid = i < p.nbuf;
+    const uint8_t *ptr = nullptr;
+    uint64_t n = 0, seed = 0;
+    if (valid) {
+        ptr = (const uint8_t *)(p.d_ptrs ? p.d_ptrs[i] : p.base + i * p.stride);
+        n = p.d_ptrs ? p.d_lens[i] : p.len;
+        seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
+    }
+    const uint64_t ns = n >= 32 ? n / 32 : 0;
+    uint64_t v = seed + (j == 0 ? XP1 + XP2 : j == 1 ? XP2 : j == 2 ? 0ull : 0ull - XP1);
+    const uint8_t *q = ptr + 8 * j;
+    // kXxSlots x 4 stripes in flight per lane: an HBM load takes ~2 us, a round a few dependent
+    // integer ops; the kernel runs a few waves per CU, so registers are plentiful
+    constexpr int kXxSlots = 12;
+    if (ns > 0) {
+        uint64_t u = v + ldw(q) * XP2;  // stripe 0 entered; stripes 1..ns-1 follow as y
+        uint32_t ul = (uint32_t)u, uh = (uint32_t)(u >> 32);
+        const uint8_t *q1 = q + 32;
+        const uint64_t nr = ns - 1;
+        uint64_t s = 0;
+        if (nr >= 4 * kXxSlots) {
+            uint64_t w[kXxSlots][4];
+#pragma unroll
+            for (int k = 0; k < kXxSlots; ++k)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) w[k][m] = ldw(q1 + 32 * (4 * k + m));
+            for (s = 4 * kXxSlots; s + 4 * kXxSlots <= nr; s += 4 * kXxSlots) {
+#pragma unroll
+                for (int k = 0; k < kXxSlots; ++k) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) xstep(ul, uh, w[k][m] * XP2);
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) w[k][m] = ldw(q1 + 32 * (s + 4 * k + m));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kXxSlots; ++k)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) xstep(ul, uh, w[k][m] * XP2);
+        }
+        for (; s < nr; ++s) xstep(ul, uh, ldw(q1 + 32 * s) * XP2);
+        xstep(ul, uh, 0);  // the last stripe's round
+        v = ((uint64_t)uh << 32) | ul;
+    }
+    // lane 0 of the quad gathers v1..v4 (quad_perm DPP broadcasts of lanes 1..3)
+    const uint64_t v1 = quad_bcast<0>(v), v2 = quad_bcast<1>(v), v3 = quad_bcast<2>(v), v4 = quad_bcast<3>(v);
+    if (!valid || j != 0) return;
+    p.d_out[i] = xxh64_finish(v1, v2, v3, v4, ptr, n, seed);
+}
+
+// XXH64 over strided batches (equal lengths), B buffers per wave: lane l = 4 (B t + b) + j loads
+// word j of stripe s0 + t of buffer b, so one load instruction brings T = 16 / B stripes of every
+// buffer of the wave and their input products y = w * P2 are formed lane-parallel (off the chains);
+// the chain lanes then take y of stripe s0 + t from lane l + 4 B t by ds_bpermute (LDS pipe) and
+// spend only the six-op round on the VALU.  Every t group runs the same chains redundantly.  B is
+// chosen on the host so that the launch has about one wave per SIMD (a round issues from one wave).
+constexpr uint64_t inv_odd64(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton: 6 doublings of precision)
+    uint64_t x = a;
+    for (int k = 0; k < 6; ++k) x *= 2 - a * x;
+    return x;
+}
+constexpr uint64_t kXP1Inv = inv_odd64(XP1);
+static_assert(kXP1Inv * XP1 == 1, "P1 inverse");
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, int src_lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void xxh64_wave_kernel(const XxhParams p) {
+    constexpr int T = 16 / B, DS = 12;  // stripes per load; loads in flight
+    const int lane = threadIdx.x, j = lane & 3, b = (lane >> 2) % B, t = lane / (4 * B);
+    const uint64_t i = (uint64_t)blockIdx.x * B + b;
+    const bool valid = i < p.nbuf;
+    const uint64_t ic = valid ? i : p.nbuf - 1;  // loads stay inside the batch
+    const uint8_t *ptr = (const uint8_t *)(p.base + ic * p.stride);
+    const uint64_t n = p.len, seed = p.d_seeds ? p.d_seeds[ic] : p.seed_all;
+    const uint64_t ns = n / 32, nslot = (ns + T - 1) / T;
+    uint64_t v = seed + (j == 0 ? XP1 + XP2 : j == 1 ? XP2 : j == 2 ? 0ull : 0ull - XP1);
+    const int src0 = lane & (4 * B - 1);
+    const uint8_t *q = ptr + 8 * j;
+    auto ld = [&](uint64_t slot) -> uint64_t {
+        uint64_t st = slot * T + (uint64_t)t;
+        st = st < ns ? st : ns - 1;  // the last slot's spare lanes re-read the last stripe
+        return ldw(q + 32 * st);
+    };
+    if (ns > 0) {
+        uint64_t x[DS];
+#pragma unroll
+        for (int d = 0; d < DS; ++d) x[d] = ld(d);
+        // every stripe's product is added by the round before it; the chain starts from the state
+        // whose round yields v: rotl(u0, 31) * P1 = v, so stripe 0 needs no special case
+        const uint64_t u0 = rotl64(v * kXP1Inv, 33);
+        uint32_t ul = (uint32_t)u0, uh = (uint32_t)(u0 >> 32);
+        // software pipeline: the next slot's products and bpermutes issue before this slot's T
+        // rounds (sched_barrier keeps the scheduler from sinking them to their uses; interleaving
+        // them two per round measured 11 % slower)
+        uint64_t ya[T], yb[T];
+        auto perm = [&](uint64_t xv, uint64_t (&yt)[T]) {
+            const uint64_t y = xv * XP2;
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt) yt[tt] = bperm64(y, src0 + 4 * B * tt);
+        };
+        auto rounds = [&](const uint64_t (&yt)[T], uint64_t slot, bool full) {
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt)
+                if (full || slot * T + tt < ns) xstep_y(ul, uh, yt[tt]);  // yt is a bpermute result: opaque
+        };
+        perm(x[0], ya);
+        const uint64_t nfull = ns / T;  // slots whose T stripes all exist
+        uint64_t slot = 0;
+        for (; slot + DS <= nfull; slot += DS) {
+#pragma unroll
+            for (int d = 0; d < DS; ++d) {
+                uint64_t (&cur)[T] = (d & 1) ? yb : ya;
+                uint64_t (&nxt)[T] = (d & 1) ? ya : yb;
+                perm(x[(d + 1) % DS], nxt);  // slot + d + 1 (x[0] already holds slot + DS)
+                x[d] = ld(slot + DS + d);
+                __builtin_amdgcn_sched_barrier(0);
+                rounds(cur, slot + d, true);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (DS & 1) {  // keep the next slot's products in ya
+#pragma unroll
+                for (int tt = 0; tt < T; ++tt) ya[tt] = yb[tt];
+            }
+        }
+        // at most DS slots remain (the last may be partial); their words are already in the ring
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+            if (slot + d < nslot) {
+                uint64_t (&cur)[T] = (d & 1) ? yb : ya;
+                uint64_t (&nxt)[T] = (d & 1) ? ya : yb;
+                if (d + 1 < DS && slot + d + 1 < nslot) perm(x[d + 1], nxt);
+                rounds(cur, slot + d, false);
+            }
+        }
+        xstep_y(ul, uh, 0);  // the last stripe's round
+        v = ((uint64_t)uh << 32) | ul;
+    }
+    const uint64_t v1 = quad_bcast<0>(v), v2 = quad_bcast<1>(v), v3 = quad_bcast<2>(v), v4 = quad_bcast<3>(v);
+    if (!valid || t != 0 || j != 0) return;
+    p.d_out[i] = xxh64_finish(v1, v2, v3, v4, ptr, n, seed);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2032,9 +2158,21 @@ extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *strea
 }
 
 extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream, void *const *ev) {
+    if (p->nbuf == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (!p->d_ptrs) {
+        // strided: B buffers per wave, the fewest that keep the launch near one wave per SIMD
+        constexpr uint64_t kSimds = 1024;
+        auto go = [&](auto kern, uint64_t bper) { launch(kern, (int)((p->nbuf + bper - 1) / bper), 64, s, p, ev); };
+        if (p->nbuf <= kSimds) go(xxh64_wave_kernel<1>, 1);
+        else if (p->nbuf <= 2 * kSimds) go(xxh64_wave_kernel<2>, 2);
+        else if (p->nbuf <= 4 * kSimds) go(xxh64_wave_kernel<4>, 4);
+        else if (p->nbuf <= 8 * kSimds) go(xxh64_wave_kernel<8>, 8);
+        else go(xxh64_wave_kernel<16>, 16);
+        return (int)hipGetLastError();
+    }
     const int threads = 256;
     const uint64_t blocks = (p->nbuf * 4 + threads - 1) / threads;  // a quad per buffer
-    if (blocks == 0) return 0;
-    launch(xxh64_quad_kernel, (int)blocks, threads, (hipStream_t)stream, p, ev);
+    launch(xxh64_quad_kernel, (int)blocks, threads, s, p, ev);
     return (int)hipGetLastError();
 }

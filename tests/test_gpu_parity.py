@@ -130,6 +130,30 @@ def test_strided_shapes_with_seeds(engine, alg, L, off, count):
     assert engine.as_unsigned(out) == want
 
 
+@pytest.mark.parametrize("L,off,count,stride_pad", [
+    (0, 0, 5, 0), (31, 1, 3, 1), (32, 0, 7, 0), (33, 3, 17, 5), (511, 0, 1, 0), (512, 0, 2, 0), (513, 5, 3, 3),
+    (32 * 16 * 12 * 3 + 100, 0, 4, 0), (32 * 16 * 12 + 32 * 5, 2, 3, 1), ((1 << 20) + 7, 1, 3, 9),
+    (65536, 0, 1024, 0), (1000, 0, 1500, 0), (777, 4, 3000, 3), (300, 0, 6000, 0), (200, 1, 9000, 1)])
+def test_xxh64_strided_wave_kernel(engine, L, off, count, stride_pad):
+    """Strided XXH64 (xxh64_wave_kernel): B = 1, 2, 4, 8, 16 buffers per wave (by count), lengths
+    with no full stripe, partial last slots and whole pipeline rounds, unaligned bases and strides,
+    per-buffer seeds and seed 0."""
+    import torch
+
+    stride = L + stride_pad
+    d = dev_random(stride * count + off + 16, 11 + L + count)
+    rng = random.Random(L * 7 + count)
+    seeds = [rng.getrandbits(64) for _ in range(count)]
+    out = engine.checksum_strided(ALG["xxh64"], d, stride, L, count, seeds=seeds_tensor("xxh64", seeds), base_offset=off)
+    out0 = engine.checksum_strided(ALG["xxh64"], d, stride, L, count, base_offset=off)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    ptrs = [h.ctypes.data + off + i * stride for i in range(count)]
+    assert results(engine, "xxh64", out0) == oracle.batch("xxh64", ptrs, [L] * count, 8)
+    assert results(engine, "xxh64", out) == [oracle.checksum("xxh64", h[off + i * stride: off + i * stride + L], s)
+                                             for i, s in enumerate(seeds)]
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_ragged_list_random(engine, alg):
     import torch
