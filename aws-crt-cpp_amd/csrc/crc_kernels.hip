@@ -1731,10 +1731,13 @@ __device__ __noinline__ uint64_t xxh64_finish(uint64_t v1, uint64_t v2, uint64_t
     return h;
 }
 
-__global__ __launch_bounds__(256) void xxh64_quad_kernel(const XxhParams p) {
-    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+// One wave per block, bpw buffers per wave (quads 0..bpw-1; the rest of the wave idles), bpw sized
+// on the host so that the launch spreads over the SIMDs.
+__global__ __launch_bounds__(64) void xxh64_quad_kernel(const XxhParams p, uint32_t bpw) {
+    const uint32_t quad = threadIdx.x >> 2;
+    const uint64_t i = (uint64_t)blockIdx.x * bpw + quad;
     const int j = (int)(threadIdx.x & 3);
-    const bool valid = i < p.nbuf;
+    const bool valid = quad < bpw && i < p.nbuf;
     const uint8_t *ptr = nullptr;
     uint64_t n = 0, seed = 0;
     if (valid) {
@@ -2096,12 +2099,13 @@ extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stre
 
 // Scan launch.  ev[0] / ev[1] (diagnostics, may be null): HIP events stamped with the dispatch's own
 // start / end time (hipExtLaunchKernel), i.e. the interval a kernel-trace profiler reports.
-template <typename K, typename P>
-static void launch(K kernel, int nblocks, int threads, hipStream_t s, const P *p, void *const *ev) {
+template <typename K, typename P, typename... A>
+static void launch(K kernel, int nblocks, int threads, hipStream_t s, const P *p, void *const *ev, A... extra) {
     if (ev && (ev[0] || ev[1]))
-        hipExtLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p);
+        hipExtLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, (hipEvent_t)ev[0], (hipEvent_t)ev[1], 0, *p,
+                              extra...);
     else
-        hipLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, *p);
+        hipLaunchKernelGGL(kernel, dim3(nblocks), dim3(threads), 0, s, *p, extra...);
 }
 
 extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, void *stream, void *const *ev) {
@@ -2171,8 +2175,9 @@ extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream, void *const
         else go(xxh64_wave_kernel<16>, 16);
         return (int)hipGetLastError();
     }
-    const int threads = 256;
-    const uint64_t blocks = (p->nbuf * 4 + threads - 1) / threads;  // a quad per buffer
-    launch(xxh64_quad_kernel, (int)blocks, threads, s, p, ev);
+    // lists (ragged lengths): a quad per buffer, the fewest buffers per wave that keep about one
+    // wave per SIMD
+    const uint64_t bpw = std::min<uint64_t>(16, std::max<uint64_t>(1, (p->nbuf + 1023) / 1024));
+    launch(xxh64_quad_kernel, (int)((p->nbuf + bpw - 1) / bpw), 64, s, p, ev, (uint32_t)bpw);
     return (int)hipGetLastError();
 }
