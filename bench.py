@@ -181,7 +181,7 @@ def widest(k, g):
 
 
 KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc64nvme": "crc64_stream4_kernel",
-          "xxh64": "xxh64_quad_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
+          "xxh64": "xxh64_wave_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
 
 
 def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,

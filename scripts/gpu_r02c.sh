@@ -16,5 +16,6 @@ cd /tmp &&
 step 300 $O/prof_c2.log rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 20 $PROF &&
 step 300 $O/prof_c3.log rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 $R/bench.py --steps 12 --warmup 2 --buffers 16 --buffer-bytes 268435456 --batches 2 --coalesce 1 --timing-launches 6 --branches 1 --only-coalesced --no-configs --no-cpu-baseline --e2e-batches 0 &&
 step 300 $O/prof_t16.log rocprofv3 --kernel-trace --stats -d $O/prof_t16 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --buffers 16 --buffer-bytes 67108864 --batches 2 --coalesce 1 --timing-launches 6 --branches 1 --only-coalesced --no-configs --no-cpu-baseline --e2e-batches 0 &&
+step 300 $O/prof_c5.log rocprofv3 --kernel-trace --stats -d $O/prof_c5 -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --steps 20 --warmup 2 --buffers 8 --buffer-bytes 67108864 --batches 2 --coalesce 1 --timing-launches 6 --branches 1 --only-coalesced --no-configs --no-cpu-baseline --e2e-batches 0 &&
 step 120 $O/pmc_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 20 $PROF &&
 echo "session ok"
