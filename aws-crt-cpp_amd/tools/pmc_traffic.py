@@ -4,7 +4,10 @@
     rocprofv3 --pmc FETCH_SIZE -d D -o run --output-format csv -- python3 bench.py ...
     rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum -d D2 ...
     python3 tools/pmc_traffic.py --fetch D/run_counter_collection.csv --rdreq D2/run_counter_collection.csv \
-        --workload crc32c:1024x65536 --bytes-per-launch 67108864 > profiles/pmc_traffic.json
+        --workload crc32c:1024x65536 --bytes-per-launch 67108864 --update profiles/pmc_traffic.json
+
+profiles/pmc_traffic.json holds one record per (workload, batches per launch); --update replaces the
+record of the same shape and keeps the others.
 
 Corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section): FETCH_SIZE is in KiB and on gfx950
 reports half the bytes of a wide coalesced streaming read, so bytes = 2 * 1024 * FETCH_SIZE; the
@@ -34,6 +37,7 @@ def main():
     ap.add_argument("--bytes-per-launch", type=int, required=True)
     ap.add_argument("--batches-per-launch", type=int, default=1)
     ap.add_argument("--source", default="", help="where the counter CSV came from (recorded in the output)")
+    ap.add_argument("--update", help="JSON file of records to add this record to (replacing the same shape)")
     a = ap.parse_args()
     f = per_dispatch(a.fetch, a.kernel)["FETCH_SIZE"]
     fetch_bytes = 2 * 1024 * statistics.median(f)
@@ -48,6 +52,17 @@ def main():
         req32 = statistics.median(r.get("TCC_EA0_RDREQ_32B_sum", [0.0]))
         rec["rdreq_bytes_per_launch"] = round(128 * (req - req32) + 32 * req32)
     print(json.dumps(rec, indent=1))
+    if a.update:
+        try:
+            doc = json.load(open(a.update))
+        except FileNotFoundError:
+            doc = {"records": []}
+        recs = doc["records"] if "records" in doc else [doc]
+        recs = [r for r in recs if (r.get("workload"), r.get("batches_per_launch", 1)) !=
+                (rec["workload"], rec["batches_per_launch"])] + [rec]
+        with open(a.update, "w") as fh:
+            json.dump({"records": recs}, fh, indent=1)
+            fh.write("\n")
 
 
 if __name__ == "__main__":

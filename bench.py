@@ -431,10 +431,11 @@ def main():
     pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            rec = json.load(open(pmc))
-            if rec.get("workload") == f"{alg}:{count}x{L}" and rec.get("batches_per_launch", 1) == gsz:
-                roof["traffic"] = rec.get("hbm_bytes_per_launch")
-                roof["traffic_source"] = rec.get("source", "profiles/pmc_traffic.json")
+            doc = json.load(open(pmc))
+            for rec in doc["records"] if "records" in doc else [doc]:
+                if rec.get("workload") == f"{alg}:{count}x{L}" and rec.get("batches_per_launch", 1) == gsz:
+                    roof["traffic"] = rec.get("hbm_bytes_per_launch")
+                    roof["traffic_source"] = rec.get("source", "profiles/pmc_traffic.json")
         except Exception:
             pass
 
