@@ -99,6 +99,7 @@ struct Device {
     size_t stage_bytes = 0;
     DevBuf hash_stage;        // whole-buffer device copy for GPU-dispatched host xxHash
     void *d_small = nullptr;  // results / seeds for the single path
+    void *h_res = nullptr;    // pinned, coherent host slot the single path's last launch stores into
     std::mutex single_mu;
 };
 
@@ -593,6 +594,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
 int ensure_stage(Device *d, size_t bytes) {
     if (!d->own_stream) HIP_TRY(hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking));
     if (!d->d_small) HIP_TRY(hipMalloc(&d->d_small, 64));
+    if (!d->h_res) HIP_TRY(hipHostMalloc(&d->h_res, 64, hipHostMallocCoherent));
     if (d->stage_bytes >= bytes) return 0;
     for (int i = 0; i < 2; ++i) {
         if (d->pin[i]) {
@@ -650,19 +652,19 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
             dp = d->hash_stage.p;
         }
         const uint64_t base = len ? (uint64_t)(uintptr_t)dp : 16;
-        rc = strided_impl(d, alg, base, len, len, 1, nullptr, seed, res, s);
-        uint64_t out[2] = {0, 0};
+        rc = strided_impl(d, alg, base, len, len, 1, nullptr, seed, d->h_res, s);
         if (!rc) {
-            hipError_t e = hipMemcpyAsync(out, res, osz, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            const hipError_t e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = fail(AWS_CRT_AMD_ERR_HIP, hipGetErrorString(e));
         }
-        result[0] = out[0];
-        if (osz == 16) result[1] = out[1];
+        const volatile uint64_t *h = (const volatile uint64_t *)d->h_res;
+        result[0] = rc ? 0 : h[0];
+        if (osz == 16) result[1] = rc ? 0 : h[1];
         return rc;
     }
+    // the last launch stores its result straight into pinned host memory (no device-to-host copy)
     if (is_device_ptr(input)) {
-        rc = strided_impl(d, alg, (uint64_t)(uintptr_t)input, len, len, 1, nullptr, seed, res, s);
+        rc = strided_impl(d, alg, (uint64_t)(uintptr_t)input, len, len, 1, nullptr, seed, d->h_res, s);
         if (rc) return rc;
     } else {
         const char *src = (const char *)input;
@@ -676,17 +678,17 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
             HIP_TRY(hipMemcpyAsync(d->dbuf[slot], d->pin[slot], n, hipMemcpyHostToDevice, s));
             HIP_TRY(hipEventRecord(d->pin_free[slot], s));
             const void *dseed = i == 0 ? nullptr : res + ((i - 1) & 1) * 8;
-            rc = strided_impl(d, alg, (uint64_t)(uintptr_t)d->dbuf[slot], n, n, 1, dseed, seed, res + slot * 8, s);
+            const bool last = off + n == len;
+            rc = strided_impl(d, alg, (uint64_t)(uintptr_t)d->dbuf[slot], n, n, 1, dseed, seed,
+                              last ? d->h_res : (void *)(res + slot * 8), s);
             if (rc) return rc;
             off += n;
             ++i;
         }
-        if (i > 0) res = res + ((i - 1) & 1) * 8;
     }
-    uint64_t out = 0;
-    HIP_TRY(hipMemcpyAsync(&out, res, osz, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    *result = out;
+    const volatile char *h = (const volatile char *)d->h_res;
+    *result = osz == 4 ? *(const volatile uint32_t *)h : *(const volatile uint64_t *)h;
     return 0;
 }
 
