@@ -98,6 +98,7 @@ struct Device {
     hipEvent_t pin_free[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
     DevBuf hash_stage;        // whole-buffer device copy for GPU-dispatched host xxHash
+    DevBuf ceil_sink;         // read-ceiling diagnostics: one word per wave
     void *d_small = nullptr;  // results / seeds for the single path
     void *h_res = nullptr;    // pinned, coherent host slot the single path's last launch stores into
     std::mutex single_mu;
@@ -744,14 +745,16 @@ AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t by
     Device *d;
     int rc = get_device(&d);
     if (rc) return rc;
-    static DevBuf sink;  // one word per wave (practically never written)
+    const size_t words = (size_t)d->cus * 2 * 8;  // one word per wave (practically never written)
     {
         std::lock_guard<std::mutex> g(d->mu);
-        if (!sink.p) HIP_TRY(hipMalloc(&sink.p, (size_t)d->cus * 2 * 8 * sizeof(uint32_t)));
+        if (!d->ceil_sink.p) {
+            HIP_TRY(hipMalloc(&d->ceil_sink.p, words * sizeof(uint32_t)));
+            d->ceil_sink.bytes = words * sizeof(uint32_t);
+        }
     }
-    // the streaming scan's geometry: one workgroup per CU below 256 MiB, two from there on
     const int blocks = bytes >= kSmallBatchBytes ? 2 * d->cus : d->cus;
-    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)sink.p, blocks, hip_stream, g_time_events);
+    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)d->ceil_sink.p, blocks, hip_stream, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
