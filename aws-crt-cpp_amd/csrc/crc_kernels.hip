@@ -1353,6 +1353,7 @@ __device__ __forceinline__ void b64_build_tables(char *lds) {
 template <uint64_t POLY>
 __device__ __forceinline__ void b64x4_build_tables(char *lds) {
     const uint32_t i = threadIdx.x;
+    if (i >= 512) return;  // eight waves build the eight tables
     const uint32_t t = __builtin_amdgcn_readfirstlane(i >> 6);
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
@@ -1551,10 +1552,11 @@ __device__ __forceinline__ void stream64_finish(const ScanParams &p, const Tile 
 // a launch queued on another stream co-resides with the running one.  The default W=64 streaming
 // scan: C5 pipelined 5500-5558 vs 5138-5143 GiB/s for an 8-copy kernel with one workgroup per CU, at a
 // 4 % slower isolated launch (2-way bank conflicts on the lookups).
-template <uint64_t POLY>
-__global__ __launch_bounds__(kBraidBlock, 4) void crc64_stream4_kernel(const ScanParams p) {
+template <uint64_t POLY, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParams p) {
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kB64x4Lds];
+    constexpr int kBraidWaves = BLOCK / 64;
 
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
@@ -2129,8 +2131,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (p->stream && !list)  // 4-copy tables, two workgroups per CU
-                launch(crc64_stream4_kernel<kPoly64Nvme>, nblocks, kBraidBlock, s, p, ev);
+            if (p->stream && !list)  // 4-copy tables
+                launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);
             else

@@ -313,8 +313,8 @@ struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
 ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main, bool w64_half_blocks = false) {
-    const uint64_t wpb = width_of(alg) == 32 || w64_half_blocks ? 8 : (uint64_t)kWavesPerBlock;
-    const uint64_t per_cu = w64_half_blocks ? 2 : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
+    const uint64_t wpb = width_of(alg) == 32 ? 8 : w64_half_blocks ? (uint64_t)kW64StreamBlock / kWave : (uint64_t)kWavesPerBlock;
+    const uint64_t per_cu = w64_half_blocks ? 1024 / kW64StreamBlock : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
     const uint64_t cap = (uint64_t)d->cus * per_cu;
     const uint64_t blocks = std::min<uint64_t>((ntiles + wpb - 1) / wpb, cap);
     return {blocks, wpb};
