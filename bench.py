@@ -184,8 +184,39 @@ KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc6
           "xxh64": "xxh64_wave_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
 
 
+def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
+    """One config step from pinned host memory through the host-ingest API (SURVEY.md §8(d)
+    end-to-end row): results in host memory, checked against the device-resident results; beside it
+    the H2D-only rate of the same bytes (the PCIe ceiling)."""
+    import torch
+
+    host = torch.empty(nbuf * L, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev_step[: nbuf * L])
+    ptrs = [host.data_ptr() + i * L for i in range(nbuf)]
+    job = eng.HostJob(ALG[alg], ptrs, [L] * nbuf)
+    job.run()  # warm-up (device lanes, first DMA touch of the pinned pages)
+    t0 = time.perf_counter()
+    job.run()
+    el = time.perf_counter() - t0
+    parity = job.results() == gpu_results[:nbuf]
+    slot = torch.empty(min(nbuf * L, 256 << 20), dtype=torch.uint8, device=dev_step.device)
+    cs = torch.cuda.Stream(device=dev_step.device)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    with torch.cuda.stream(cs):
+        for off in range(0, nbuf * L, slot.numel()):
+            n = min(slot.numel(), nbuf * L - off)
+            slot[:n].copy_(host[off:off + n], non_blocking=True)
+    torch.cuda.synchronize()
+    el_h2d = time.perf_counter() - t1
+    del host
+    return {"value": round(nbuf * L / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(nbuf * L / el_h2d / 2**30, 2),
+            "api": "aws_crt_amd_host_submit + aws_crt_amd_job_wait", "parity_with_device_path": parity,
+            "sample": f"one step ({nbuf} x {L} B) from pinned host memory, results to host memory"}
+
+
 def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,
-               cpu_seconds=0.5, do_cpu=True):
+               cpu_seconds=0.5, do_cpu=True, do_e2e=True):
     """One BASELINE config: `steps` steps of `nbuf` x L bytes (nb rotating batches), pipelined over
     the streams; roofline from `timing` serialised launches; CPU baseline on `cpu_bufs` buffers."""
     import torch
@@ -227,6 +258,9 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
         gpu0 = eng.as_unsigned(outs[0])
         host = data[: cpu_bufs * L].cpu().numpy()
         rec["cpu_baseline"] = cpu_baseline(eng, alg, host, cpu_bufs, L, gpu0, cpu_seconds)
+    if do_e2e and alg not in ("xxh64", "xxh3_64", "xxh3_128"):  # host-ingest hash jobs run on the host path
+        torch.cuda.synchronize()
+        rec["e2e_pinned"] = e2e_step(eng, alg, data, nbuf, L, eng.as_unsigned(outs[0]))
     del data
     torch.cuda.empty_cache()
     return rec
@@ -465,14 +499,15 @@ def main():
             del data
             torch.cuda.empty_cache()
             do_cpu = not args.no_cpu_baseline
-            configs["C3_crc32c"] = config_leg(eng, "C3", "crc32c", 16, 256 << 20, streams, dev, do_cpu=do_cpu)
-            configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, do_cpu=do_cpu)
+            legs = {"do_cpu": do_cpu, "do_e2e": args.e2e_batches > 0}
+            configs["C3_crc32c"] = config_leg(eng, "C3", "crc32c", 16, 256 << 20, streams, dev, **legs)
+            configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, **legs)
             configs["C4_shard_crc32c"] = config_leg(eng, "C4 per-GPU shard", "crc32c", 131072, 8192, streams, dev,
-                                                    steps=20, do_cpu=do_cpu)
-            configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, do_cpu=do_cpu)
-            configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, do_cpu=do_cpu)
+                                                    steps=20, **legs)
+            configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, **legs)
+            configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, **legs)
             configs["target_16x64MiB_crc32c"] = config_leg(eng, "north-star target", "crc32c", 16, 64 << 20, streams, dev,
-                                                           steps=20, do_cpu=do_cpu)
+                                                           steps=20, **legs)
             configs["target_16x64MiB_crc32c"]["target_pct"] = 80.0
 
     if rank == 0:
