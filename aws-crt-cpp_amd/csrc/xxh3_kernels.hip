@@ -281,6 +281,13 @@ __device__ __forceinline__ uint64_t class_sum(uint64_t v) {  // sum over the 16 
     return v;
 }
 __device__ __forceinline__ uint64_t mul32x32(uint64_t k) { return (k & 0xFFFFFFFFull) * (k >> 32); }
+constexpr uint64_t inv_odd64(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton)
+    uint64_t x = a;
+    for (int k = 0; k < 6; ++k) x *= 2 - a * x;
+    return x;
+}
+constexpr uint64_t kP32_1Inv = inv_odd64(P32_1);
+static_assert(kP32_1Inv * P32_1 == 1, "P32_1 inverse");
 __device__ __forceinline__ uint64_t scramble1(uint64_t a, uint64_t s) {
     a ^= a >> 47;
     a ^= s;
@@ -333,31 +340,63 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
             blk = blk < nb ? blk : nb - 1;
             return *(const __attribute__((address_space(1))) uint64_t *)(S + blk * 8 + c8);
         };
-        auto group = [&](uint64_t xv, uint64_t cnt) {
-            uint64_t v[G];
+        // the chain carries u = acc + v (the next block's sum already added): per block
+        //   a = u ^ (u >> 47) ^ key;  u' = a * P32_1 + v_next
+        // = one v_xor3 after the shift, then v_mad_u64_u32 (low half, v_next as the addend) beside
+        // v_mul_lo_u32 (high half), then one add
+        const uint32_t kl = (uint32_t)stv, kh = (uint32_t)(stv >> 32);
+        auto step = [&](uint32_t &ul, uint32_t &uh, uint64_t vnext) {
+            const uint32_t al = ul ^ (uh >> 15) ^ kl, ah = uh ^ kh;
+            uint32_t c = ah * (uint32_t)P32_1;
+            asm("" : "+v"(c));  // keep the high product off the low mad's chain
+            const uint64_t m = (uint64_t)al * (uint32_t)P32_1 + vnext;
+            ul = (uint32_t)m;
+            uh = (uint32_t)(m >> 32) + c;
+        };
+        // start from the state whose step yields accv + v0: a = accv * P^-1, u0 = xorshift^-1(a ^ key)
+        // (x ^ (x >> 47) is its own inverse on 64 bits), so every block is the same step
+        const uint64_t b0 = (accv * kP32_1Inv) ^ stv, u0 = b0 ^ (b0 >> 47);
+        uint32_t ul = (uint32_t)u0, uh = (uint32_t)(u0 >> 32);
+        uint64_t ya[G], yb[G];
+        auto perm = [&](uint64_t xv, uint64_t (&v)[G]) {
 #pragma unroll
             for (int j = 0; j < G; ++j) v[j] = shfl64(xv, 8 * j + c8);
-#pragma unroll
-            for (int j = 0; j < G; ++j)
-                if ((uint64_t)j < cnt) accv = scramble1(accv + v[j], stv);
         };
         uint64_t x[DS];
 #pragma unroll
         for (int d = 0; d < DS; ++d) x[d] = ldg(d);
         const uint64_t ng = (nb + G - 1) / G, nround = (nb / G) / DS;
         uint64_t g = 0;
+        perm(x[0], ya);
         for (uint64_t r = 0; r < nround; ++r, g += DS) {
 #pragma unroll
             for (int d = 0; d < DS; ++d) {
-                const uint64_t xv = x[d];
+                uint64_t (&cur)[G] = (d & 1) ? yb : ya;
+                uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
+                perm(x[(d + 1) % DS], nxt);  // group g + d + 1 (x[0] already holds g + DS)
                 x[d] = ldg(g + DS + d);
-                group(xv, G);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < G; ++j) step(ul, uh, cur[j]);
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // at most DS groups remain (the last may be partial); their sums are already in the ring
+        // at most DS groups remain (the last may be partial); their sums are in the ring, and the
+        // first of them already in ya (DS is even)
 #pragma unroll
-        for (int d = 0; d < DS; ++d)
-            if (g + d < ng) group(x[d], nb - (g + d) * G < (uint64_t)G ? nb - (g + d) * G : (uint64_t)G);
+        for (int d = 0; d < DS; ++d) {
+            if (g + d < ng) {
+                uint64_t (&cur)[G] = (d & 1) ? yb : ya;
+                uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
+                if (d + 1 < DS && g + d + 1 < ng) perm(x[d + 1], nxt);
+                const uint64_t cnt = nb - (g + d) * G < (uint64_t)G ? nb - (g + d) * G : (uint64_t)G;
+#pragma unroll
+                for (int j = 0; j < G; ++j)
+                    if ((uint64_t)j < cnt) step(ul, uh, cur[j]);
+            }
+        }
+        step(ul, uh, 0);  // the last block's scramble
+        accv = ((uint64_t)uh << 32) | ul;
     } else {
         // D blocks per round: their lane contributions and class sums are independent of the
         // accumulators, so all D reductions issue together and only the scrambles stay serial
