@@ -2163,6 +2163,71 @@ extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *strea
     return (int)hipGetLastError();
 }
 
+// XXH64, one buffer per wave (strided batches of at most one buffer per SIMD): row r of the wave
+// (lanes 16 r .. 16 r + 15) runs chain r (accumulator v_(r+1)), replicated over the row; lane t of the
+// row loads word r of stripe s0 + t, so one load instruction brings 16 stripes (512 contiguous
+// bytes) and their input products form lane-parallel.  Stripe t's product reaches its row by two DPP
+// row_newbcast:t moves (VALU, no LDS round trip); the round is xstep_y.
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {  // lane l's value (l wave-uniform)
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+template <int T>
+__device__ __forceinline__ uint64_t row_bcast64(uint64_t v) {
+    // bound_ctrl set and every row and bank enabled: every lane reads a live lane, no "old" operand
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, 0x150 + T, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), 0x150 + T, 0xF, 0xF, true);
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int T>
+__device__ __forceinline__ void row_rounds(uint32_t &ul, uint32_t &uh, uint64_t y, uint64_t first, uint64_t ns, bool full) {
+    if constexpr (T < 16) {
+        const uint64_t yt = row_bcast64<T>(y);
+        if (full || first + T < ns) xstep_y(ul, uh, yt);  // yt comes through DPP: opaque to re-association
+        row_rounds<T + 1>(ul, uh, y, first, ns, full);
+    }
+}
+__global__ __launch_bounds__(64) void xxh64_row_kernel(const XxhParams p) {
+    constexpr int DS = 12;  // loads in flight
+    const int lane = threadIdx.x, r = lane >> 4, t = lane & 15;
+    const uint64_t i = blockIdx.x;
+    const uint8_t *ptr = (const uint8_t *)(p.base + i * p.stride);
+    const uint64_t n = p.len, seed = p.d_seeds ? p.d_seeds[i] : p.seed_all;
+    const uint64_t ns = n / 32, nslot = (ns + 15) / 16;
+    uint64_t v = seed + (r == 0 ? XP1 + XP2 : r == 1 ? XP2 : r == 2 ? 0ull : 0ull - XP1);
+    const uint8_t *q = ptr + 8 * r;
+    auto ld = [&](uint64_t slot) -> uint64_t {
+        uint64_t st = slot * 16 + (uint64_t)t;
+        st = st < ns ? st : ns - 1;  // the last slot's spare lanes re-read the last stripe
+        return ldw(q + 32 * st);
+    };
+    if (ns > 0) {
+        uint64_t x[DS];
+#pragma unroll
+        for (int d = 0; d < DS; ++d) x[d] = ld(d);
+        const uint64_t u0 = rotl64(v * kXP1Inv, 33);  // its round yields v (stripe 0 needs no special case)
+        uint32_t ul = (uint32_t)u0, uh = (uint32_t)(u0 >> 32);
+        const uint64_t nfull = ns / 16;
+        uint64_t slot = 0;
+        for (; slot + DS <= nfull; slot += DS) {
+#pragma unroll
+            for (int d = 0; d < DS; ++d) {
+                const uint64_t y = x[d] * XP2;
+                x[d] = ld(slot + DS + d);
+                row_rounds<0>(ul, uh, y, 0, 0, true);
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < DS; ++d)
+            if (slot + d < nslot) row_rounds<0>(ul, uh, x[d] * XP2, (slot + d) * 16, ns, false);
+        xstep_y(ul, uh, 0);  // the last stripe's round
+        v = ((uint64_t)uh << 32) | ul;
+    }
+    const uint64_t v1 = rl64(v, 0), v2 = rl64(v, 16), v3 = rl64(v, 32), v4 = rl64(v, 48);
+    if (lane != 0) return;
+    p.d_out[i] = xxh64_finish(v1, v2, v3, v4, ptr, n, seed);
+}
+
 extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream, void *const *ev) {
     if (p->nbuf == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
@@ -2170,7 +2235,7 @@ extern "C" int amdcrc_launch_xxh64(const XxhParams *p, void *stream, void *const
         // strided: B buffers per wave, the fewest that keep the launch near one wave per SIMD
         constexpr uint64_t kSimds = 1024;
         auto go = [&](auto kern, uint64_t bper) { launch(kern, (int)((p->nbuf + bper - 1) / bper), 64, s, p, ev); };
-        if (p->nbuf <= kSimds) go(xxh64_wave_kernel<1>, 1);
+        if (p->nbuf <= kSimds) go(xxh64_row_kernel, 1);
         else if (p->nbuf <= 2 * kSimds) go(xxh64_wave_kernel<2>, 2);
         else if (p->nbuf <= 4 * kSimds) go(xxh64_wave_kernel<4>, 4);
         else if (p->nbuf <= 8 * kSimds) go(xxh64_wave_kernel<8>, 8);
