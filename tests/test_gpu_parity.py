@@ -154,6 +154,27 @@ def test_xxh64_strided_wave_kernel(engine, L, off, count, stride_pad):
                                              for i, s in enumerate(seeds)]
 
 
+def test_xxh64_list_many_buffers_per_wave(engine):
+    """Ragged XXH64 lists of more than 1024 buffers put several buffers in one wave
+    (xxh64_quad_kernel, bpw = ceil(n / 1024)): 5000 buffers of random length 0..3000 at random
+    alignments, with per-buffer seeds, so the last wave is partly idle."""
+    import torch
+
+    rng = random.Random(0x64_5000)
+    lens = [rng.randrange(0, 3001) for _ in range(5000)]
+    offs, pos = [], 0
+    for ln in lens:
+        pos += rng.randrange(0, 16)
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 0x5000)
+    seeds = [rng.getrandbits(64) for _ in lens]
+    out = engine.checksum_list(ALG["xxh64"], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor("xxh64", seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    assert results(engine, "xxh64", out) == [oracle.checksum("xxh64", h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_ragged_list_random(engine, alg):
     import torch
