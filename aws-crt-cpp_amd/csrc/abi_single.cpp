@@ -20,6 +20,7 @@
 #include <cstring>
 #include <new>
 
+#include "abi_guard.h"
 #include "cpu/cpu_checksums.h"
 #include "gf2.h"
 
@@ -34,7 +35,11 @@ extern "C" int amdcrc_is_device_ptr(const void *p);
 extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_t seed, uint64_t *out);
 extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n);
 
+using amdcrc::guarded;
+
 namespace {
+
+void no_sink(const char *) noexcept {}
 
 std::atomic<int> g_mode{-1};
 std::atomic<unsigned long long> g_fallbacks{0};
@@ -181,10 +186,12 @@ AWS_CRT_AMD_API unsigned long long aws_crt_amd_fallback_count(void) { return g_f
 
 AWS_CRT_AMD_API int aws_crt_amd_cpu_batch(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                           const uint64_t *seeds, uint64_t *out, int threads) {
-    if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    if (count && (!h_ptrs || !lens || !out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    cpu::batch(alg, (const uint8_t *const *)h_ptrs, lens, seeds, out, count, threads);
-    return 0;
+    return guarded(no_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        if (count && (!h_ptrs || !lens || !out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        cpu::batch(alg, (const uint8_t *const *)h_ptrs, lens, seeds, out, count, threads);
+        return 0;
+    });
 }
 
 AWS_CRT_AMD_API const char *aws_crt_amd_cpu_tier(void) {

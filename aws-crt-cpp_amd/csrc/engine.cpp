@@ -25,6 +25,7 @@
 
 #include <aws/crt/Types.h>
 
+#include "abi_guard.h"
 #include "cpu/cpu_checksums.h"
 #include "engine.h"
 #include "gf2.h"
@@ -43,6 +44,12 @@ thread_local void *g_time_events[2] = {nullptr, nullptr};
 int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
+}
+void err_sink(const char *m) noexcept {
+    try {
+        g_last_error = m;
+    } catch (...) {
+    }
 }
 
 #define HIP_TRY(expr)                                                                                      \
@@ -697,12 +704,16 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
 
 // ================================================================== internal (abi_single.cpp)
 extern "C" int amdcrc_gpu_usable(void) {
-    Device *d;
-    return get_device(&d) == 0 ? 1 : 0;
+    return guarded(err_sink, [&]() -> int {
+        Device *d;
+        return get_device(&d) == 0 ? 1 : 0;
+    });
 }
 extern "C" int amdcrc_is_device_ptr(const void *p) { return is_device_ptr(p) ? 1 : 0; }
 extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_t seed, uint64_t *out) {
-    return single_impl(alg, input, len, seed, out);
+    return guarded(err_sink, [&]() -> int {
+        return single_impl(alg, input, len, seed, out);
+    });
 }
 extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n) {
     return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
@@ -712,8 +723,10 @@ extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n) {
 extern "C" {
 
 AWS_CRT_AMD_API int aws_crt_amd_init(void) {
-    Device *d;
-    return get_device(&d);
+    return guarded(err_sink, [&]() -> int {
+        Device *d;
+        return get_device(&d);
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_device_count(void) { return device_count_noinit(); }
@@ -742,202 +755,218 @@ AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_e
 // (512-thread workgroups, one per CU below 256 MiB, two above).  Honours
 // aws_crt_amd_debug_time_next_launch.
 AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t bytes, void *hip_stream) {
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    const size_t words = (size_t)d->cus * 2 * 8;  // one word per wave (practically never written)
-    {
-        std::lock_guard<std::mutex> g(d->mu);
-        if (!d->ceil_sink.p) {
-            HIP_TRY(hipMalloc(&d->ceil_sink.p, words * sizeof(uint32_t)));
-            d->ceil_sink.bytes = words * sizeof(uint32_t);
+    return guarded(err_sink, [&]() -> int {
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        const size_t words = (size_t)d->cus * 2 * 8;  // one word per wave (practically never written)
+        {
+            std::lock_guard<std::mutex> g(d->mu);
+            if (!d->ceil_sink.p) {
+                HIP_TRY(hipMalloc(&d->ceil_sink.p, words * sizeof(uint32_t)));
+                d->ceil_sink.bytes = words * sizeof(uint32_t);
+            }
         }
-    }
-    const int blocks = bytes >= kSmallBatchBytes ? 2 * d->cus : d->cus;
-    const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)d->ceil_sink.p, blocks, hip_stream, g_time_events);
-    g_time_events[0] = g_time_events[1] = nullptr;
-    return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+        const int blocks = bytes >= kSmallBatchBytes ? 2 * d->cus : d->cus;
+        const int e = amdcrc_launch_read_ceiling(d_base, bytes, (uint32_t *)d->ceil_sink.p, blocks, hip_stream, g_time_events);
+        g_time_events[0] = g_time_events[1] = nullptr;
+        return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,
                                                  const void *d_seeds, void *d_out, void *hip_stream) {
-    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    if (count == 1) stride = len;
-    return strided_impl(d, alg, (uint64_t)(uintptr_t)d_base, stride, len, count, d_seeds, 0, d_out, (hipStream_t)hip_stream);
+    return guarded(err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        if (count == 1) stride = len;
+        return strided_impl(d, alg, (uint64_t)(uintptr_t)d_base, stride, len, count, d_seeds, 0, d_out, (hipStream_t)hip_stream);
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(int alg, const struct aws_crt_amd_batch *batches, size_t nbatches,
                                                  size_t stride, size_t len, size_t count, void *hip_stream) {
-    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
-    if (nbatches && !batches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null batches");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    hipStream_t s = (hipStream_t)hip_stream;
-    if (count == 1) stride = len;
-    for (size_t j = 0; j < nbatches; ++j)
-        if (!batches[j].d_out || (len && !batches[j].d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
-    if (count == 0 || nbatches == 0) return 0;
-    if (is_hash(alg)) {  // the hash kernels run one launch per batch
-        for (size_t j = 0; j < nbatches && !rc; ++j)
-            rc = strided_impl(d, alg, (uint64_t)(uintptr_t)batches[j].d_base, stride, len, count, batches[j].d_seeds, 0,
-                              batches[j].d_out, s);
-        return rc;
-    }
-    // one launch per run of up to kMaxBatches batches whose bases share their alignment mod 16
-    std::vector<Batch> run;
-    for (size_t j = 0; j <= nbatches && !rc; ++j) {
-        const bool flush = j == nbatches || run.size() == (size_t)kMaxBatches ||
-                           (!run.empty() && ((uint64_t)(uintptr_t)batches[j].d_base & 15) != (run[0].base & 15));
-        if (flush && !run.empty()) {
-            rc = scan_batches(d, alg, run.data(), run.size(), stride, len, count, 0, s);
-            run.clear();
+    return guarded(err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        if (nbatches && !batches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null batches");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        hipStream_t s = (hipStream_t)hip_stream;
+        if (count == 1) stride = len;
+        for (size_t j = 0; j < nbatches; ++j)
+            if (!batches[j].d_out || (len && !batches[j].d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
+        if (count == 0 || nbatches == 0) return 0;
+        if (is_hash(alg)) {  // the hash kernels run one launch per batch
+            for (size_t j = 0; j < nbatches && !rc; ++j)
+                rc = strided_impl(d, alg, (uint64_t)(uintptr_t)batches[j].d_base, stride, len, count, batches[j].d_seeds, 0,
+                                  batches[j].d_out, s);
+            return rc;
         }
-        if (j < nbatches) run.push_back({(uint64_t)(uintptr_t)batches[j].d_base, batches[j].d_seeds, batches[j].d_out});
-    }
-    return rc;
+        // one launch per run of up to kMaxBatches batches whose bases share their alignment mod 16
+        std::vector<Batch> run;
+        for (size_t j = 0; j <= nbatches && !rc; ++j) {
+            const bool flush = j == nbatches || run.size() == (size_t)kMaxBatches ||
+                               (!run.empty() && ((uint64_t)(uintptr_t)batches[j].d_base & 15) != (run[0].base & 15));
+            if (flush && !run.empty()) {
+                rc = scan_batches(d, alg, run.data(), run.size(), stride, len, count, 0, s);
+                run.clear();
+            }
+            if (j < nbatches) run.push_back({(uint64_t)(uintptr_t)batches[j].d_base, batches[j].d_seeds, batches[j].d_out});
+        }
+        return rc;
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,
                                               const void *d_seeds, void *d_out, void *hip_stream) {
-    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    return list_impl(d, alg, d_ptrs, lens, count, d_seeds, d_out, (hipStream_t)hip_stream);
+    return guarded(err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        return list_impl(d, alg, d_ptrs, lens, count, d_seeds, d_out, (hipStream_t)hip_stream);
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(const void *base, uint64_t limit, const uint64_t *d_offsets, size_t count,
                                                  uint32_t *d_prelude_crc, uint32_t *d_message_crc, uint32_t *d_status,
                                                  void *hip_stream) {
-    if (count == 0) return 0;
-    if (!base || !d_offsets || !d_prelude_crc || !d_message_crc || !d_status)
-        return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status};
-    int e = amdcrc_launch_eventstream(&ep, hip_stream, g_time_events);
-    g_time_events[0] = g_time_events[1] = nullptr;
-    return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("event-stream kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+    return guarded(err_sink, [&]() -> int {
+        if (count == 0) return 0;
+        if (!base || !d_offsets || !d_prelude_crc || !d_message_crc || !d_status)
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status};
+        int e = amdcrc_launch_eventstream(&ep, hip_stream, g_time_events);
+        g_time_events[0] = g_time_events[1] = nullptr;
+        return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("event-stream kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_checksum_host(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                               const void *h_seeds, void *h_out) {
-    if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
-    if (count && (!h_ptrs || !lens || !h_out)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
-    const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
-    const bool gpu = aws_crt_amd_get_dispatch() == AWS_CRT_AMD_DISPATCH_GPU;
-    for (size_t i = 0; i < count; ++i) {
-        uint64_t seed = 0;
-        if (h_seeds) seed = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
-        uint64_t r[2] = {0, 0};
-        if (!gpu || single_impl(alg, h_ptrs[i], lens[i], seed, r) != 0) {
-            const uint8_t *p = (const uint8_t *)h_ptrs[i];
-            (void)aws_crt_amd_cpu_batch(alg, (const void *const *)&p, &lens[i], 1, &seed, r, 1);
+    return guarded(err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        if (count && (!h_ptrs || !lens || !h_out)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
+        const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
+        const bool gpu = aws_crt_amd_get_dispatch() == AWS_CRT_AMD_DISPATCH_GPU;
+        for (size_t i = 0; i < count; ++i) {
+            uint64_t seed = 0;
+            if (h_seeds) seed = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+            uint64_t r[2] = {0, 0};
+            if (!gpu || single_impl(alg, h_ptrs[i], lens[i], seed, r) != 0) {
+                const uint8_t *p = (const uint8_t *)h_ptrs[i];
+                (void)aws_crt_amd_cpu_batch(alg, (const void *const *)&p, &lens[i], 1, &seed, r, 1);
+            }
+            if (alg == AWS_CRT_AMD_XXH3_128) {
+                ((uint64_t *)h_out)[2 * i] = r[0];
+                ((uint64_t *)h_out)[2 * i + 1] = r[1];
+            } else if (seed64) {
+                ((uint64_t *)h_out)[i] = r[0];
+            } else {
+                ((uint32_t *)h_out)[i] = (uint32_t)r[0];
+            }
         }
-        if (alg == AWS_CRT_AMD_XXH3_128) {
-            ((uint64_t *)h_out)[2 * i] = r[0];
-            ((uint64_t *)h_out)[2 * i + 1] = r[1];
-        } else if (seed64) {
-            ((uint64_t *)h_out)[i] = r[0];
-        } else {
-            ((uint32_t *)h_out)[i] = (uint32_t)r[0];
-        }
-    }
-    return 0;
+        return 0;
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(int alg, const void *d_crc1, const void *d_crc2, const uint64_t *len2,
                                                   size_t count, void *d_out, void *hip_stream) {
-    if (alg < 0 || alg > 2) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "combine needs a CRC algorithm");
-    if (count == 0) return 0;
-    if (!d_crc1 || !d_crc2 || !len2 || !d_out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    hipStream_t s = (hipStream_t)hip_stream;
-    std::lock_guard<std::mutex> g(d->mu);
-    // staging: [x^(8*2^i), i < 64][len2[count]]
-    uint64_t *h;
-    const size_t words = 64 + count;
-    if ((rc = stage_begin(d, s, words * 8, (void **)&h))) return rc;
-    const uint64_t poly = alg_poly(alg);
-    const int w = width_of(alg);
-    uint64_t sq = (1ull << (w - 1)) >> 8;
-    for (int i = 0; i < 64; ++i) {
-        h[i] = sq;
-        sq = gf2_mulmod(sq, sq, poly, w);
-    }
-    std::memcpy(h + 64, len2, count * 8);
-    const uint64_t *dd;
-    if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;
-    CombineParams cp{d_crc1, d_crc2, dd + 64, count, d_out, dd};
-    int e = amdcrc_launch_combine(alg, &cp, s);
-    return e ? fail(AWS_CRT_AMD_ERR_HIP, "combine launch failed") : 0;
+    return guarded(err_sink, [&]() -> int {
+        if (alg < 0 || alg > 2) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "combine needs a CRC algorithm");
+        if (count == 0) return 0;
+        if (!d_crc1 || !d_crc2 || !len2 || !d_out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        hipStream_t s = (hipStream_t)hip_stream;
+        std::lock_guard<std::mutex> g(d->mu);
+        // staging: [x^(8*2^i), i < 64][len2[count]]
+        uint64_t *h;
+        const size_t words = 64 + count;
+        if ((rc = stage_begin(d, s, words * 8, (void **)&h))) return rc;
+        const uint64_t poly = alg_poly(alg);
+        const int w = width_of(alg);
+        uint64_t sq = (1ull << (w - 1)) >> 8;
+        for (int i = 0; i < 64; ++i) {
+            h[i] = sq;
+            sq = gf2_mulmod(sq, sq, poly, w);
+        }
+        std::memcpy(h + 64, len2, count * 8);
+        const uint64_t *dd;
+        if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;
+        CombineParams cp{d_crc1, d_crc2, dd + 64, count, d_out, dd};
+        int e = amdcrc_launch_combine(alg, &cp, s);
+        return e ? fail(AWS_CRT_AMD_ERR_HIP, "combine launch failed") : 0;
+    });
 }
 
 // S3 multipart composition (checksums_batch.h): one batched scan over the parts, then the
 // Combine fold of the part values (4/8-byte scalars, no payload) into the full-object checksum.
 AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_parts, const size_t *lens, size_t count,
                                               void *h_part_out, void *h_object_out, char *b64_out, void *hip_stream) {
-    if (alg < AWS_CRT_AMD_CRC32 || alg > AWS_CRT_AMD_CRC64NVME || !h_object_out || (count && (!d_parts || !lens)))
-        return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "multipart: CRC32/CRC32C/CRC64NVME, parts and an object result");
-    Device *d;
-    int rc = get_device(&d);
-    if (rc) return rc;
-    const int w = width_of(alg);
-    const uint64_t poly = alg_poly(alg);
-    std::vector<uint64_t> part(count, 0);
-    if (count) {
-        const size_t osz = w / 8;
-        hipStream_t s = (hipStream_t)hip_stream;
-        void *d_out;
-        {
-            std::lock_guard<std::mutex> g(d->mu);
-            DevBuf &ob = d->mp_out[s];
-            if (ob.bytes < count * osz) {
-                if (ob.p) d->retired.push_back(ob);
-                ob = DevBuf{};
-                HIP_TRY(hipMalloc(&ob.p, count * osz));
-                ob.bytes = count * osz;
-            }
-            d_out = ob.p;
-        }
-        rc = list_impl(d, alg, d_parts, lens, count, nullptr, d_out, s);
-        std::vector<uint8_t> h(count * osz);
-        if (!rc && hipMemcpyAsync(h.data(), d_out, h.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess) {
-            for (size_t i = 0; i < count; ++i)
-                part[i] = w == 64 ? ((const uint64_t *)h.data())[i] : ((const uint32_t *)h.data())[i];
-        } else if (!rc) {
-            rc = fail(AWS_CRT_AMD_ERR_HIP, "multipart: result copy failed");
-        }
+    return guarded(err_sink, [&]() -> int {
+        if (alg < AWS_CRT_AMD_CRC32 || alg > AWS_CRT_AMD_CRC64NVME || !h_object_out || (count && (!d_parts || !lens)))
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "multipart: CRC32/CRC32C/CRC64NVME, parts and an object result");
+        Device *d;
+        int rc = get_device(&d);
         if (rc) return rc;
-    }
-    uint64_t obj = 0;  // CRC of zero bytes
-    for (size_t i = 0; i < count; ++i)
-        obj = gf2_mulmod(obj, gf2_xpow8n(lens[i], poly, w), poly, w) ^ part[i];
-    for (size_t i = 0; h_part_out && i < count; ++i) {
+        const int w = width_of(alg);
+        const uint64_t poly = alg_poly(alg);
+        std::vector<uint64_t> part(count, 0);
+        if (count) {
+            const size_t osz = w / 8;
+            hipStream_t s = (hipStream_t)hip_stream;
+            void *d_out;
+            {
+                std::lock_guard<std::mutex> g(d->mu);
+                DevBuf &ob = d->mp_out[s];
+                if (ob.bytes < count * osz) {
+                    if (ob.p) d->retired.push_back(ob);
+                    ob = DevBuf{};
+                    HIP_TRY(hipMalloc(&ob.p, count * osz));
+                    ob.bytes = count * osz;
+                }
+                d_out = ob.p;
+            }
+            rc = list_impl(d, alg, d_parts, lens, count, nullptr, d_out, s);
+            std::vector<uint8_t> h(count * osz);
+            if (!rc && hipMemcpyAsync(h.data(), d_out, h.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                hipStreamSynchronize(s) == hipSuccess) {
+                for (size_t i = 0; i < count; ++i)
+                    part[i] = w == 64 ? ((const uint64_t *)h.data())[i] : ((const uint32_t *)h.data())[i];
+            } else if (!rc) {
+                rc = fail(AWS_CRT_AMD_ERR_HIP, "multipart: result copy failed");
+            }
+            if (rc) return rc;
+        }
+        uint64_t obj = 0;  // CRC of zero bytes
+        for (size_t i = 0; i < count; ++i)
+            obj = gf2_mulmod(obj, gf2_xpow8n(lens[i], poly, w), poly, w) ^ part[i];
+        for (size_t i = 0; h_part_out && i < count; ++i) {
+            if (w == 64)
+                ((uint64_t *)h_part_out)[i] = part[i];
+            else
+                ((uint32_t *)h_part_out)[i] = (uint32_t)part[i];
+        }
         if (w == 64)
-            ((uint64_t *)h_part_out)[i] = part[i];
+            *(uint64_t *)h_object_out = obj;
         else
-            ((uint32_t *)h_part_out)[i] = (uint32_t)part[i];
-    }
-    if (w == 64)
-        *(uint64_t *)h_object_out = obj;
-    else
-        *(uint32_t *)h_object_out = (uint32_t)obj;
-    if (b64_out) {
-        uint8_t be[8];
-        for (int i = 0; i < w / 8; ++i) be[i] = (uint8_t)(obj >> (w - 8 * (i + 1)));
-        const Aws::Crt::String b64 = Aws::Crt::Base64Encode(aws_byte_cursor_from_array(be, (size_t)(w / 8)));
-        std::memcpy(b64_out, b64.c_str(), b64.size() + 1);
-    }
-    return 0;
+            *(uint32_t *)h_object_out = (uint32_t)obj;
+        if (b64_out) {
+            uint8_t be[8];
+            for (int i = 0; i < w / 8; ++i) be[i] = (uint8_t)(obj >> (w - 8 * (i + 1)));
+            const Aws::Crt::String b64 = Aws::Crt::Base64Encode(aws_byte_cursor_from_array(be, (size_t)(w / 8)));
+            std::memcpy(b64_out, b64.c_str(), b64.size() + 1);
+        }
+        return 0;
+    });
 }
 
 }  // extern "C"

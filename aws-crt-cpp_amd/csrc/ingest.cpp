@@ -30,6 +30,7 @@
 #include <thread>
 #include <vector>
 
+#include "abi_guard.h"
 #include "cpu/cpu_checksums.h"
 #include "gf2.h"
 
@@ -41,6 +42,12 @@ using namespace amdcrc;
 namespace {
 
 thread_local std::string t_err;
+void job_err_sink(const char *m) noexcept {
+    try {
+        t_err = m;
+    } catch (...) {
+    }
+}
 
 constexpr size_t kSlotBytes = 32u << 20;  // device slot / pinned mirror per pipeline stage
 constexpr int kSlots = 3;
@@ -89,11 +96,26 @@ struct JobImpl {
     std::atomic<int> rc{0};
     std::string err;
     std::mutex err_mu;
-    void set_error(int code, const std::string &m) {
+    void set_error(int code, const char *m) noexcept {
         std::lock_guard<std::mutex> g(err_mu);
         if (rc.load() == 0) {
             rc.store(code);
-            err = m;
+            try {
+                err = m;
+            } catch (...) {
+            }
+        }
+    }
+    void set_error(int code, const std::string &m) noexcept { set_error(code, m.c_str()); }
+    // start a worker; on failure join the ones already started (the job must not be freed under them)
+    template <class... A>
+    void spawn(A &&...a) {
+        try {
+            workers.emplace_back(std::forward<A>(a)...);
+        } catch (...) {
+            for (auto &t : workers) t.join();
+            workers.clear();
+            throw;
         }
     }
 };
@@ -152,7 +174,17 @@ void lane_free(Lane &L) {
 }
 
 // Worker for one device: pieces `mine` (indices into job->pieces, in order) through the 3-slot ring
-void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) {
+void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine);
+void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) noexcept {
+    try {
+        device_worker_body(job, dev, mine);
+    } catch (const std::bad_alloc &) {
+        job->set_error(AWS_CRT_AMD_ERR_OOM, "out of host memory");
+    } catch (...) {
+        job->set_error(AWS_CRT_AMD_ERR_HIP, "internal error in a device worker");
+    }
+}
+void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine) {
     Lane *lp = lane_take(dev);
     Lane &L = *lp;
     struct Guard {
@@ -333,76 +365,80 @@ AWS_CRT_AMD_API int aws_crt_amd_unregister_host(void *p) {
 
 AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                             const void *h_seeds, void *h_out, int ndevices, struct aws_crt_amd_job **job_out) {
-    if (!job_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    *job_out = nullptr;
-    if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    if (count && (!h_ptrs || !lens || !h_out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    for (size_t i = 0; i < count; ++i)
-        if (lens[i] && !h_ptrs[i]) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    std::unique_ptr<aws_crt_amd_job> job(new (std::nothrow) aws_crt_amd_job);
-    if (!job) return AWS_CRT_AMD_ERR_OOM;
-    JobImpl &J = job->impl;
-    J.alg = alg;
-    J.ptrs = h_ptrs;
-    J.lens = lens;
-    J.count = count;
-    J.h_out = h_out;
-    const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
-    J.seeds.assign(count, 0);
-    for (size_t i = 0; h_seeds && i < count; ++i)
-        J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
-    const int vis = visible_devices();
-    int G = ndevices <= 0 ? vis : std::min(ndevices, vis);
-    if (!is_crc(alg) || G <= 0) {
-        // xxHash (or no device): the host path, one thread per device the job would have used
-        const size_t threads = (size_t)std::max(1, std::min(G > 0 ? G : 1, 16));
-        for (size_t t = 0; t < threads; ++t) J.workers.emplace_back(host_worker, &J, t, threads);
+    return guarded(job_err_sink, [&]() -> int {
+        if (!job_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        *job_out = nullptr;
+        if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        if (count && (!h_ptrs || !lens || !h_out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        for (size_t i = 0; i < count; ++i)
+            if (lens[i] && !h_ptrs[i]) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        std::unique_ptr<aws_crt_amd_job> job(new (std::nothrow) aws_crt_amd_job);
+        if (!job) return AWS_CRT_AMD_ERR_OOM;
+        JobImpl &J = job->impl;
+        J.alg = alg;
+        J.ptrs = h_ptrs;
+        J.lens = lens;
+        J.count = count;
+        J.h_out = h_out;
+        const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
+        J.seeds.assign(count, 0);
+        for (size_t i = 0; h_seeds && i < count; ++i)
+            J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+        const int vis = visible_devices();
+        int G = ndevices <= 0 ? vis : std::min(ndevices, vis);
+        if (!is_crc(alg) || G <= 0) {
+            // xxHash (or no device): the host path, one thread per device the job would have used
+            const size_t threads = (size_t)std::max(1, std::min(G > 0 ? G : 1, 16));
+            for (size_t t = 0; t < threads; ++t) J.spawn(host_worker, &J, t, threads);
+            *job_out = job.release();
+            return 0;
+        }
+        // pieces, buffer by buffer; buffer i goes to device i % G
+        std::vector<std::vector<size_t>> per_dev((size_t)G);
+        for (size_t i = 0; i < count; ++i) {
+            size_t off = 0;
+            do {
+                const size_t n = std::min(kSlotBytes, lens[i] - off);
+                per_dev[i % (size_t)G].push_back(J.pieces.size());
+                J.pieces.push_back({i, off, n, off == 0 ? J.seeds[i] : 0});
+                off += n;
+            } while (off < lens[i]);
+        }
+        J.piece_val.assign(J.pieces.size(), 0);
+        for (int g = 0; g < G; ++g)
+            if (!per_dev[(size_t)g].empty()) J.spawn(device_worker, &J, g, std::move(per_dev[(size_t)g]));
         *job_out = job.release();
         return 0;
-    }
-    // pieces, buffer by buffer; buffer i goes to device i % G
-    std::vector<std::vector<size_t>> per_dev((size_t)G);
-    for (size_t i = 0; i < count; ++i) {
-        size_t off = 0;
-        do {
-            const size_t n = std::min(kSlotBytes, lens[i] - off);
-            per_dev[i % (size_t)G].push_back(J.pieces.size());
-            J.pieces.push_back({i, off, n, off == 0 ? J.seeds[i] : 0});
-            off += n;
-        } while (off < lens[i]);
-    }
-    J.piece_val.assign(J.pieces.size(), 0);
-    for (int g = 0; g < G; ++g)
-        if (!per_dev[(size_t)g].empty()) J.workers.emplace_back(device_worker, &J, g, std::move(per_dev[(size_t)g]));
-    *job_out = job.release();
-    return 0;
+    });
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
-    if (!job) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    JobImpl &J = job->impl;
-    for (auto &t : J.workers) t.join();
-    int rc = J.rc.load();
-    if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
-        // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
-        const uint64_t poly = alg_poly(J.alg);
-        const int w = alg_width(J.alg);
-        size_t p = 0;
-        for (size_t i = 0; i < J.count; ++i) {
-            uint64_t acc = J.piece_val[p++];
-            while (p < J.pieces.size() && J.pieces[p].buf == i) {
-                acc = gf2_mulmod(acc, gf2_xpow8n(J.pieces[p].len, poly, w), poly, w) ^ J.piece_val[p];
-                ++p;
+    return guarded(job_err_sink, [&]() -> int {
+        if (!job) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        JobImpl &J = job->impl;
+        for (auto &t : J.workers) t.join();
+        int rc = J.rc.load();
+        if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
+            // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
+            const uint64_t poly = alg_poly(J.alg);
+            const int w = alg_width(J.alg);
+            size_t p = 0;
+            for (size_t i = 0; i < J.count; ++i) {
+                uint64_t acc = J.piece_val[p++];
+                while (p < J.pieces.size() && J.pieces[p].buf == i) {
+                    acc = gf2_mulmod(acc, gf2_xpow8n(J.pieces[p].len, poly, w), poly, w) ^ J.piece_val[p];
+                    ++p;
+                }
+                if (w == 64)
+                    ((uint64_t *)J.h_out)[i] = acc;
+                else
+                    ((uint32_t *)J.h_out)[i] = (uint32_t)acc;
             }
-            if (w == 64)
-                ((uint64_t *)J.h_out)[i] = acc;
-            else
-                ((uint32_t *)J.h_out)[i] = (uint32_t)acc;
         }
-    }
-    if (rc) t_err = J.err;
-    delete job;
-    return rc;
+        if (rc) t_err = J.err;
+        delete job;
+        return rc;
+    });
 }
 
 AWS_CRT_AMD_API const char *aws_crt_amd_job_last_error(void) { return t_err.c_str(); }
@@ -412,110 +448,128 @@ AWS_CRT_AMD_API const char *aws_crt_amd_job_last_error(void) { return t_err.c_st
 // results are scattered in caller order into h_out.  Synchronous.
 AWS_CRT_AMD_API int aws_crt_amd_checksum_list_devices(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,
                                                       const void *h_seeds, void *h_out) {
-    if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    if (!count) return 0;
-    if (!d_ptrs || !lens || !h_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    const int vis = visible_devices();
-    if (vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
-    std::vector<std::vector<size_t>> by_dev((size_t)vis);
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
-    for (size_t i = 0; i < count; ++i) {
-        int dev = cur;  // zero-length entries may carry any pointer
-        if (lens[i]) {
-            hipPointerAttribute_t a;
-            if (!d_ptrs[i] || hipPointerGetAttributes(&a, d_ptrs[i]) != hipSuccess || a.type != hipMemoryTypeDevice) {
-                (void)hipGetLastError();
-                t_err = "aws_crt_amd_checksum_list_devices: buffer " + std::to_string(i) + " is not device memory";
-                return AWS_CRT_AMD_ERR_INVALID_ARG;
+    return guarded(job_err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        if (!count) return 0;
+        if (!d_ptrs || !lens || !h_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        const int vis = visible_devices();
+        if (vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
+        std::vector<std::vector<size_t>> by_dev((size_t)vis);
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
+        for (size_t i = 0; i < count; ++i) {
+            int dev = cur;  // zero-length entries may carry any pointer
+            if (lens[i]) {
+                hipPointerAttribute_t a;
+                if (!d_ptrs[i] || hipPointerGetAttributes(&a, d_ptrs[i]) != hipSuccess || a.type != hipMemoryTypeDevice) {
+                    (void)hipGetLastError();
+                    t_err = "aws_crt_amd_checksum_list_devices: buffer " + std::to_string(i) + " is not device memory";
+                    return AWS_CRT_AMD_ERR_INVALID_ARG;
+                }
+                dev = a.device;
             }
-            dev = a.device;
+            by_dev[(size_t)dev].push_back(i);
         }
-        by_dev[(size_t)dev].push_back(i);
-    }
-    const int per = out_words(alg);
-    const size_t osz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8 * (size_t)per;
-    const size_t ssz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8;
-    std::atomic<int> rc{0};
-    std::vector<std::thread> pool;
-    for (int g = 0; g < vis; ++g) {
-        if (by_dev[(size_t)g].empty()) continue;
-        pool.emplace_back([&, g] {
-            const std::vector<size_t> &ix = by_dev[(size_t)g];
-            const size_t n = ix.size();
-            std::vector<const void *> ptrs(n);
-            std::vector<size_t> ls(n);
-            std::vector<uint8_t> seeds(n * ssz), res(n * osz);
-            for (size_t j = 0; j < n; ++j) {
-                ptrs[j] = d_ptrs[ix[j]];
-                ls[j] = lens[ix[j]];
-                if (h_seeds) std::memcpy(seeds.data() + j * ssz, (const uint8_t *)h_seeds + ix[j] * ssz, ssz);
+        const int per = out_words(alg);
+        const size_t osz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8 * (size_t)per;
+        const size_t ssz = alg == AWS_CRT_AMD_CRC32 || alg == AWS_CRT_AMD_CRC32C ? 4 : 8;
+        std::atomic<int> rc{0};
+        std::vector<std::thread> pool;
+        for (int g = 0; g < vis; ++g) {
+            if (by_dev[(size_t)g].empty()) continue;
+            auto body = [&, g] {
+                const std::vector<size_t> &ix = by_dev[(size_t)g];
+                const size_t n = ix.size();
+                std::vector<const void *> ptrs(n);
+                std::vector<size_t> ls(n);
+                std::vector<uint8_t> seeds(n * ssz), res(n * osz);
+                for (size_t j = 0; j < n; ++j) {
+                    ptrs[j] = d_ptrs[ix[j]];
+                    ls[j] = lens[ix[j]];
+                    if (h_seeds) std::memcpy(seeds.data() + j * ssz, (const uint8_t *)h_seeds + ix[j] * ssz, ssz);
+                }
+                hipStream_t st = nullptr;
+                void *dbuf = nullptr;
+                int e = hipSetDevice(g) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+                                hipMalloc(&dbuf, n * (osz + ssz)) == hipSuccess
+                            ? 0
+                            : AWS_CRT_AMD_ERR_HIP;
+                void *dseed = dbuf ? (uint8_t *)dbuf + n * osz : nullptr;
+                if (!e && h_seeds && hipMemcpyAsync(dseed, seeds.data(), n * ssz, hipMemcpyHostToDevice, st) != hipSuccess)
+                    e = AWS_CRT_AMD_ERR_HIP;
+                if (!e) e = aws_crt_amd_checksum_list(alg, ptrs.data(), ls.data(), n, h_seeds ? dseed : nullptr, dbuf, st);
+                if (!e && (hipMemcpyAsync(res.data(), dbuf, n * osz, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                           hipStreamSynchronize(st) != hipSuccess))
+                    e = AWS_CRT_AMD_ERR_HIP;
+                if (!e)
+                    for (size_t j = 0; j < n; ++j) std::memcpy((uint8_t *)h_out + ix[j] * osz, res.data() + j * osz, osz);
+                if (dbuf) (void)hipFree(dbuf);
+                if (st) (void)hipStreamDestroy(st);
+                if (e) {
+                    int z = 0;
+                    rc.compare_exchange_strong(z, e);
+                }
+            };
+            auto worker = [&rc, body] {
+                try {
+                    body();
+                } catch (...) {  // host allocation inside the worker
+                    int z = 0;
+                    rc.compare_exchange_strong(z, (int)AWS_CRT_AMD_ERR_OOM);
+                }
+            };
+            try {
+                pool.emplace_back(worker);
+            } catch (...) {
+                for (auto &t : pool) t.join();
+                throw;
             }
-            hipStream_t st = nullptr;
-            void *dbuf = nullptr;
-            int e = hipSetDevice(g) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
-                            hipMalloc(&dbuf, n * (osz + ssz)) == hipSuccess
-                        ? 0
-                        : AWS_CRT_AMD_ERR_HIP;
-            void *dseed = dbuf ? (uint8_t *)dbuf + n * osz : nullptr;
-            if (!e && h_seeds && hipMemcpyAsync(dseed, seeds.data(), n * ssz, hipMemcpyHostToDevice, st) != hipSuccess)
-                e = AWS_CRT_AMD_ERR_HIP;
-            if (!e) e = aws_crt_amd_checksum_list(alg, ptrs.data(), ls.data(), n, h_seeds ? dseed : nullptr, dbuf, st);
-            if (!e && (hipMemcpyAsync(res.data(), dbuf, n * osz, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                       hipStreamSynchronize(st) != hipSuccess))
-                e = AWS_CRT_AMD_ERR_HIP;
-            if (!e)
-                for (size_t j = 0; j < n; ++j) std::memcpy((uint8_t *)h_out + ix[j] * osz, res.data() + j * osz, osz);
-            if (dbuf) (void)hipFree(dbuf);
-            if (st) (void)hipStreamDestroy(st);
-            if (e) {
-                int z = 0;
-                rc.compare_exchange_strong(z, e);
-            }
-        });
-    }
-    for (auto &t : pool) t.join();
-    (void)hipSetDevice(cur);
-    return rc.load();
+        }
+        for (auto &t : pool) t.join();
+        (void)hipSetDevice(cur);
+        return rc.load();
+    });
 }
 
 // Per-device uniform batches, all devices at once: each entry is launched on its device (one stream
 // per device: the entry's, or one the call creates), then every device is awaited.  Synchronous.
 AWS_CRT_AMD_API int aws_crt_amd_checksum_devices(int alg, const struct aws_crt_amd_device_batch *b, size_t n) {
-    if (alg < 0 || alg > 5 || (n && !b)) return AWS_CRT_AMD_ERR_INVALID_ARG;
-    const int vis = visible_devices();
-    if (n && vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
-    std::vector<hipStream_t> own(n, nullptr);
-    int rc = 0;
-    for (size_t i = 0; i < n && !rc; ++i) {
-        if (b[i].device < 0 || b[i].device >= vis) {
-            rc = AWS_CRT_AMD_ERR_INVALID_ARG;
-            break;
-        }
-        if (hipSetDevice(b[i].device) != hipSuccess) {
-            rc = AWS_CRT_AMD_ERR_HIP;
-            break;
-        }
-        hipStream_t st = (hipStream_t)b[i].hip_stream;
-        if (!st) {
-            if (hipStreamCreateWithFlags(&own[i], hipStreamNonBlocking) != hipSuccess) {
+    return guarded(job_err_sink, [&]() -> int {
+        if (alg < 0 || alg > 5 || (n && !b)) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        const int vis = visible_devices();
+        if (n && vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
+        std::vector<hipStream_t> own(n, nullptr);
+        int rc = 0;
+        for (size_t i = 0; i < n && !rc; ++i) {
+            if (b[i].device < 0 || b[i].device >= vis) {
+                rc = AWS_CRT_AMD_ERR_INVALID_ARG;
+                break;
+            }
+            if (hipSetDevice(b[i].device) != hipSuccess) {
                 rc = AWS_CRT_AMD_ERR_HIP;
                 break;
             }
-            st = own[i];
+            hipStream_t st = (hipStream_t)b[i].hip_stream;
+            if (!st) {
+                if (hipStreamCreateWithFlags(&own[i], hipStreamNonBlocking) != hipSuccess) {
+                    rc = AWS_CRT_AMD_ERR_HIP;
+                    break;
+                }
+                st = own[i];
+            }
+            rc = aws_crt_amd_checksum_strided(alg, b[i].d_base, b[i].stride, b[i].len, b[i].count, b[i].d_seeds, b[i].d_out, st);
         }
-        rc = aws_crt_amd_checksum_strided(alg, b[i].d_base, b[i].stride, b[i].len, b[i].count, b[i].d_seeds, b[i].d_out, st);
-    }
-    for (size_t i = 0; i < n; ++i) {  // await every device (also after a failure: nothing stays queued)
-        if (hipSetDevice(b[i].device) != hipSuccess) continue;
-        hipStream_t st = own[i] ? own[i] : (hipStream_t)b[i].hip_stream;
-        if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = AWS_CRT_AMD_ERR_HIP;
-        if (own[i]) (void)hipStreamDestroy(own[i]);
-    }
-    (void)hipSetDevice(cur);
-    return rc;
+        for (size_t i = 0; i < n; ++i) {  // await every device (also after a failure: nothing stays queued)
+            if (hipSetDevice(b[i].device) != hipSuccess) continue;
+            hipStream_t st = own[i] ? own[i] : (hipStream_t)b[i].hip_stream;
+            if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = AWS_CRT_AMD_ERR_HIP;
+            if (own[i]) (void)hipStreamDestroy(own[i]);
+        }
+        (void)hipSetDevice(cur);
+        return rc;
+    });
 }
 
 }  // extern "C"
