@@ -135,12 +135,51 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
     ov = None
     if alg in oracle.ALG_INDEX:
         ov = rate(oracle.prepared_batch(alg, ptrs, lens, threads), count * L)
+    third = third_party_rates(alg, host, count, L, threads, gpu_results, rate)
     return {"value": round(v, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
             "impl": f"engine host path ({eng.cpu_tier()} tier)",
             "sample": f"{count} x {L >> 10} KiB ({count * L >> 20} MiB) copied to host, median of {reps} reps "
                       f"of >= {rep_seconds:g} s, {threads} std::threads round-robin",
             "single_thread_gibs": round(v1, 2), "cpu_model": model, "logical_cpus_visible": aff,
-            "oracle_hw_tier_gibs": round(ov, 2) if ov is not None else None, "parity_with_gpu": parity}
+            "oracle_hw_tier_gibs": round(ov, 2) if ov is not None else None, "parity_with_gpu": parity,
+            "third_party": third}
+
+
+def third_party_rates(alg, host, count, L, threads, gpu_results, rate):
+    """SURVEY.md §8(d) extra CPU data points: zlib crc32 for CRC32, libxxhash XXH64 for XXH64 (the
+    system libraries; their calls release the GIL, so Python threads run them in parallel), 1 thread
+    and `threads` threads over the same buffers, checked against the GPU results."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+
+    mv = memoryview(host)
+    bufs = [mv[i * L:(i + 1) * L] for i in range(count)]
+    if alg == "crc32":
+        import zlib
+
+        fn, name = zlib.crc32, f"zlib {zlib.ZLIB_RUNTIME_VERSION} crc32"
+    elif alg == "xxh64":
+        try:
+            lib = ctypes.CDLL("libxxhash.so.0")
+        except OSError:
+            return None
+        lib.XXH64.restype = ctypes.c_uint64
+        lib.XXH64.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+        base = host.ctypes.data
+        addrs = [base + i * L for i in range(count)]
+        fn, name = (lambda a: lib.XXH64(a, L, 0)), "libxxhash XXH64 (system libxxhash.so.0)"
+        bufs = addrs
+    else:
+        return None
+    if [fn(b) for b in bufs] != list(gpu_results[:count]):
+        return {"impl": name, "parity_with_gpu": False}
+    pool = ThreadPoolExecutor(max_workers=threads)
+    try:
+        v1 = rate(lambda: [fn(b) for b in bufs[: max(1, min(count, (64 << 20) // L))]], max(1, min(count, (64 << 20) // L)) * L)
+        vn = rate(lambda: list(pool.map(fn, bufs)), count * L)
+    finally:
+        pool.shutdown()
+    return {"impl": name, "gibs": round(vn, 2), "threads": threads, "single_thread_gibs": round(v1, 2), "parity_with_gpu": True}
 
 
 def time_launches(eng, launch, st, nt):
