@@ -1985,10 +1985,28 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
     lane_tables<T, POLY>(tab);
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.nbuf) return;
+    const uint8_t *ptr;
+    uint64_t n, ix = b;
+    const void *seeds = p.d_seeds;
+    void *out = p.d_out;
+    if (p.d_ptrs) {
+        ptr = (const uint8_t *)p.d_ptrs[b];
+        n = p.d_lens[b];
+    } else {  // strided batches
+        // the batch index differs between lanes: read the descriptors through the kernarg segment
+        // (an indexed read of the by-value parameter would copy the whole block to scratch)
+        const LaneParams *kp = (const LaneParams *)__builtin_amdgcn_kernarg_segment_ptr();
+        const uint64_t j = b / p.bcount;
+        ix = b - j * p.bcount;
+        ptr = (const uint8_t *)(kp->bbase[j] + ix * p.stride);
+        n = p.len;
+        seeds = (const void *)kp->bseed[j];
+        out = (void *)kp->bout[j];
+    }
     uint64_t seed = p.seed_all;
-    if (p.d_seeds) seed = sizeof(T) == 4 ? (uint64_t)((const uint32_t *)p.d_seeds)[b] : ((const uint64_t *)p.d_seeds)[b];
-    const T s = lane_scan<T>((T)~seed, (const uint8_t *)p.d_ptrs[b], p.d_lens[b], tab);
-    ((T *)p.d_out)[b] = (T)~s;
+    if (seeds) seed = sizeof(T) == 4 ? (uint64_t)((const uint32_t *)seeds)[ix] : ((const uint64_t *)seeds)[ix];
+    const T s = lane_scan<T>((T)~seed, ptr, n, tab);
+    ((T *)out)[ix] = (T)~s;
 }
 
 // Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads

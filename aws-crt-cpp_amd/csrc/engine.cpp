@@ -314,6 +314,12 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 constexpr uint64_t kLaneMaxBytes = 4096;
+// Strided CRC64NVME launches of short buffers take the lane-per-buffer scan once they hold enough
+// buffers for a wave per SIMD: 1 GiB steps measured 3735 vs 1636 GiB/s (4 KiB buffers) and 3668 vs
+// 2693 (8 KiB, the C4 shard) for lanes vs the braided stream, and 3051 vs 3922 at 16 KiB
+// (profiles/r02/lane64/).  The W=32 scans stay braided (4 KiB CRC32C: 5561 braided vs 4029 lanes).
+constexpr uint64_t kLaneStrided64Max = 8192;
+constexpr uint64_t kLaneStrided64MinBuffers = 65536;
 // Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
 constexpr uint64_t kXxh3SplitBlocks = 4096;
 struct ScanGeometry {
@@ -434,6 +440,20 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
         p.bseed[j] = (uint64_t)(uintptr_t)bs[j].seeds;
     }
     count *= nb;  // buffers of the launch
+    if (alg == AWS_CRT_AMD_CRC64NVME && len <= kLaneStrided64Max && count >= kLaneStrided64MinBuffers) {
+        // short CRC64NVME buffers: one lane per buffer (crc_lanes_kernel) -- the W=64 braided scan's
+        // per-tile lane combine (a 64-step GF(2) multiply per lane) costs more than such a tile's scan
+        LaneParams lp{};
+        lp.nbuf = count;
+        lp.seed_all = seed_all;
+        lp.stride = stride;
+        lp.len = len;
+        lp.bcount = p.bcount;
+        for (size_t j = 0; j < nb; ++j) lp.bbase[j] = p.bbase[j], lp.bout[j] = p.bout[j], lp.bseed[j] = p.bseed[j];
+        int e = amdcrc_launch_lanes(alg, &lp, s, g_time_events);
+        g_time_events[0] = g_time_events[1] = nullptr;
+        return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+    }
     // Batches whose main regions are whole tiles take the streaming scans (crc32_stream_kernel,
     // crc64_stream4_kernel), tiles sized for one per wave slot of the launch: 1024 x 64 KiB CRC32C
     // measured 5250-5315 GiB/s with one 32 KiB tile per wave against 5000-5030 with two of 16 KiB.
@@ -533,7 +553,8 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         }
         const uint64_t *dl;
         if ((rc1 = stage_end(d, s, count * 16, (const void **)&dl))) return rc1;
-        LaneParams lp{dl, dl + count, count, d_seeds, 0, d_out};
+        LaneParams lp{};
+        lp.d_ptrs = dl, lp.d_lens = dl + count, lp.nbuf = count, lp.d_seeds = d_seeds, lp.d_out = d_out;
         int e = amdcrc_launch_lanes(alg, &lp, s, g_time_events);
         g_time_events[0] = g_time_events[1] = nullptr;
         return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;

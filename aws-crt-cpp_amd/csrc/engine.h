@@ -98,14 +98,18 @@ struct CombineParams {
     const uint64_t *d_xpow2;  // x^(8 * 2^i) mod P, i < 64
 };
 
-// Lane-per-buffer scan of a ragged list of short buffers (crc_lanes_kernel)
+// Lane-per-buffer scan (crc_lanes_kernel): a ragged list of short buffers, or (d_ptrs == null) up to
+// kMaxBatches strided batches of short uniform buffers -- buffer b of the launch is buffer b % bcount
+// of batch b / bcount, at bbase[j] + i * stride, seeds / results per batch as in ScanParams
 struct LaneParams {
-    const uint64_t *d_ptrs;  // device addresses
+    const uint64_t *d_ptrs;  // device addresses (list form)
     const uint64_t *d_lens;
     uint64_t nbuf;
     const void *d_seeds;  // u32/u64 per buffer, or null -> seed_all
     uint64_t seed_all;
     void *d_out;  // u32/u64 per buffer
+    uint64_t stride, len, bcount;  // strided form
+    uint64_t bbase[kMaxBatches], bout[kMaxBatches], bseed[kMaxBatches];
 };
 
 // Event-stream framing check (eventstream_kernel)

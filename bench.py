@@ -430,7 +430,9 @@ def main():
     eng.init()
 
     alg, count, L = args.alg, args.buffers, args.buffer_bytes
-    G = max(1, min(32, args.coalesce))
+    # hash batches run one launch per batch (aws_crt_amd_checksum_batches coalesces CRC scans only),
+    # so their launch shape is one batch
+    G = 1 if alg in ("xxh64", "xxh3_64", "xxh3_128") else max(1, min(32, args.coalesce))
     step_bytes = count * L
     # resident batches: at least --batches, and never fewer than a launch holds, so no launch reads a
     # batch twice (aliased batches in one launch would hit in L2 / the Infinity Cache)

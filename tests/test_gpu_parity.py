@@ -154,6 +154,33 @@ def test_xxh64_strided_wave_kernel(engine, L, off, count, stride_pad):
                                              for i, s in enumerate(seeds)]
 
 
+def test_crc64_short_strided_batches_lane_path(engine):
+    """Strided CRC64NVME launches of >= 65536 buffers of <= 8 KiB take the lane-per-buffer scan with
+    per-batch bases, seeds and results: three queued batches of 30000 x 3000 B (stride 3008), seeds
+    on two of them."""
+    import torch
+
+    L, stride, count, nb = 3000, 3008, 30000, 3
+    d = dev_random(nb * stride * count + 64, 0x640)
+    rng = random.Random(0x64)
+    seeds = [[rng.getrandbits(64) for _ in range(count)] if j != 1 else None for j in range(nb)]
+    outs = [torch.empty(count, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    batches = [(d.data_ptr() + j * stride * count, seeds_tensor("crc64nvme", seeds[j]) if seeds[j] else None, outs[j])
+               for j in range(nb)]
+    engine.checksum_batches(ALG["crc64nvme"], batches, stride, L, count)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    for j in range(nb):
+        base = j * stride * count
+        ptrs = [h.ctypes.data + base + i * stride for i in range(count)]
+        if seeds[j] is None:
+            assert engine.as_unsigned(outs[j]) == oracle.batch("crc64nvme", ptrs, [L] * count, 8), j
+        else:
+            got = engine.as_unsigned(outs[j])
+            for i in range(0, count, 997):
+                assert got[i] == oracle.crc("crc64nvme", h[base + i * stride: base + i * stride + L], seeds[j][i]), (j, i)
+
+
 def test_xxh64_list_many_buffers_per_wave(engine):
     """Ragged XXH64 lists of more than 1024 buffers put several buffers in one wave
     (xxh64_quad_kernel, bpw = ceil(n / 1024)): 5000 buffers of random length 0..3000 at random
