@@ -1958,10 +1958,17 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
         n -= hb;
     }
     uint64_t k = n >> 3;
+    // 16 bytes per lane per load instruction: the lanes of a wave read 64 different buffers, so the
+    // instruction count per byte (one cache-line request per lane), not bandwidth, bounds this loop
     for (; k >= 8; k -= 8, w += 8) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
         uint64_t v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = w[j];
+        for (int j = 0; j < 4; ++j) {
+            const u64x2 x = *(const __attribute__((address_space(1))) u64x2 *)(w + 2 * j);
+            v[2 * j] = x.x;
+            v[2 * j + 1] = x.y;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
     }
