@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--messages", type=int, default=131072)
     ap.add_argument("--min-bytes", type=int, default=16)
     ap.add_argument("--max-bytes", type=int, default=1024)
-    ap.add_argument("--batches", type=int, default=3)
+    ap.add_argument("--batches", type=int, default=6, help="rotating copies (6 x 65 MiB exceeds the 256 MiB Infinity Cache)")
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--timing-launches", type=int, default=8)
@@ -50,9 +50,12 @@ def main():
         import numpy as np
         import ctypes
 
+        # prelude: total_length (big-endian) and headers_length = 0, so every frame is well formed and
+        # is CRC'd (a random headers_length > total - 16 would be flagged malformed and skipped)
         hdr = np.zeros(pos, dtype=np.uint8)
-        be = np.array(lens, dtype=">u4").view(np.uint8).reshape(-1, 4)
-        idx = np.array(offs, dtype=np.int64)[:, None] + np.arange(4)[None, :]
+        be = np.concatenate([np.array(lens, dtype=">u4").view(np.uint8).reshape(-1, 4),
+                             np.zeros((len(lens), 4), dtype=np.uint8)], axis=1)
+        idx = np.array(offs, dtype=np.int64)[:, None] + np.arange(8)[None, :]
         hdr[idx.ravel()] = be.ravel()
         hd = torch.from_numpy(hdr).cuda()
         mask = torch.zeros(pos, dtype=torch.bool, device="cuda")
