@@ -1214,14 +1214,36 @@ struct Braid64 {
     __device__ __forceinline__ uint64_t byte(uint64_t s, uint32_t b) const {
         return (s >> 8) ^ lds64(L, (COPIES == 8 ? kB64T0Off : kB64x4T0Off) + 8 * (((uint32_t)s ^ b) & 0xffu));
     }
-    // r * K_l, bit-serial (once per tile)
+    // r * K_l (once per tile), Horner over the bytes of r: bit 63-j of r pairs with K_l * x^j, so
+    // with B_m = sum_i bit(63-8m-i) * K_l x^i (byte 7-m of r against the eight columns K_l x^i),
+    // r * K_l = sum_m B_m x^(8m) = (((B_7 x^8 ^ B_6) x^8 ^ ...) ^ B_0, and a * x^8 is one plain
+    // byte step, (a >> 8) ^ T0[a & 0xff].  About 230 VALU and 7 LDS reads instead of a 64-step
+    // bit-serial product (~950 VALU).  tests/test_braid64_model.py::test_mulk_byte_horner models it.
     __device__ __forceinline__ uint64_t mulK(uint64_t r) const {
-        uint64_t b = kl, acc = 0;
-#pragma unroll 8
-        for (int j = 0; j < 64; ++j) {
-            acc ^= b & (uint64_t)((int64_t)(r << j) >> 63);
+        uint32_t cl[8], ch[8];
+        uint64_t b = kl;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            cl[i] = (uint32_t)b, ch[i] = (uint32_t)(b >> 32);
             b = gf2_mulx(b, POLY);
         }
+        const uint32_t rl = (uint32_t)r, rh = (uint32_t)(r >> 32);
+        auto bm = [&](int m) -> uint64_t {
+            const uint32_t word = m < 4 ? rh : rl;
+            const int sh = 8 * ((7 - m) & 3);
+            uint32_t al = 0, ah = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t mask = (uint32_t)((int32_t)(word << (31 - (sh + 7 - i))) >> 31);
+                al = xor_and(al, cl[i], mask);
+                ah = xor_and(ah, ch[i], mask);
+            }
+            return ((uint64_t)ah << 32) | al;
+        };
+        constexpr uint32_t t0 = COPIES == 8 ? kB64T0Off : kB64x4T0Off;
+        uint64_t acc = bm(7);
+#pragma unroll
+        for (int m = 6; m >= 0; --m) acc = (acc >> 8) ^ lds64(L, t0 + 8u * ((uint32_t)acc & 0xffu)) ^ bm(m);
         return acc;
     }
 };

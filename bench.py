@@ -481,10 +481,12 @@ def main():
     for bs, st in subs:
         bs.run(st)
     torch.cuda.synchronize()
+    # each rank's clock stops when its own GPU is done; the closing barrier follows, and the slowest
+    # rank's time (max over ranks) is the job's, so the barrier's own latency is not counted as work
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+        torch.cuda.synchronize()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -102,6 +102,28 @@ class Braid64:
             s = (s >> 8) ^ self.T0[(s ^ b) & 255]
         return s
 
+    def mulK(self, r, lane):
+        """the kernel's Braid64::mulK: Horner over the bytes of r, columns K_l x^i (i < 8), a * x^8
+        as one plain byte step through T0"""
+        c, b = [], self.K[lane]
+        for _ in range(8):
+            c.append(b)
+            b = mulx(b)
+
+        def bm(m):
+            word = r >> 32 if m < 4 else r & 0xFFFFFFFF
+            sh = 8 * ((7 - m) & 3)
+            a = 0
+            for i in range(8):
+                if (word >> (sh + 7 - i)) & 1:
+                    a ^= c[i]
+            return a
+
+        acc = bm(7)
+        for m in range(6, -1, -1):
+            acc = (acc >> 8) ^ self.T0[acc & 0xFF] ^ bm(m)
+        return acc
+
 
 @pytest.fixture(scope="module")
 def br():
@@ -135,7 +157,7 @@ def braid64_model(br, data, addr, seed, rows):
                     if k == 0 and pad and vo == pad:
                         w ^= s_h
                     u = br.step(u ^ w)
-                r ^= mulmod(u, br.K[lane])
+                r ^= br.mulK(u, lane)
         if T == 1:
             fin = r if mainlen else s_h
             break
@@ -154,6 +176,13 @@ def braid64_model(br, data, addr, seed, rows):
                     fin = buf_val
     fin = br.bytes_(fin, data[tail - ptr:])
     return ~fin & M64
+
+
+def test_mulk_byte_horner(br):
+    rng = random.Random(7)
+    for lane in range(64):
+        for r in (0, 1, 1 << 63, M64, rng.getrandbits(64), rng.getrandbits(64)):
+            assert br.mulK(r, lane) == mulmod(r, br.K[lane])
 
 
 def test_inverse_x(br):
