@@ -315,10 +315,15 @@ constexpr uint64_t kSmallBatchBytes = 256ull << 20;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 constexpr uint64_t kLaneMaxBytes = 4096;
 // Strided CRC64NVME launches of short buffers take the lane-per-buffer scan once they hold enough
-// buffers for a wave per SIMD: 1 GiB steps measured 3735 vs 1636 GiB/s (4 KiB buffers) and 3668 vs
-// 2693 (8 KiB, the C4 shard) for lanes vs the braided stream, and 3051 vs 3922 at 16 KiB
-// (profiles/r02/lane64/).  The W=32 scans stay braided (4 KiB CRC32C: 5561 braided vs 4029 lanes).
-constexpr uint64_t kLaneStrided64Max = 8192;
+// buffers for a wave per SIMD.  1 GiB steps, lanes vs the streaming scan with the byte-Horner tile
+// finish (profiles/r02/lane64_r2/): 3749 vs 1262 GiB/s at 2 KiB, 3754 vs 2933 at 4 KiB, 3738 vs 4259
+// at 8 KiB (the C4 shard), so buffers up to 4 KiB.  (Round-2 before the finish rewrite, lanes won at
+// 8 KiB too: 3668 vs 2693, profiles/r02/lane64/.)  The W=32 scans stay braided (4 KiB CRC32C: 5561
+// braided vs 4029 lanes).
+#ifndef AMDCRC_LANE64_MAX  // compile-time only (launch-shape sweeps build a variant; no run-time switch)
+#define AMDCRC_LANE64_MAX 4096
+#endif
+constexpr uint64_t kLaneStrided64Max = AMDCRC_LANE64_MAX;
 constexpr uint64_t kLaneStrided64MinBuffers = 65536;
 // Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
 constexpr uint64_t kXxh3SplitBlocks = 4096;

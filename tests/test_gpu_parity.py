@@ -155,7 +155,7 @@ def test_xxh64_strided_wave_kernel(engine, L, off, count, stride_pad):
 
 
 def test_crc64_short_strided_batches_lane_path(engine):
-    """Strided CRC64NVME launches of >= 65536 buffers of <= 8 KiB take the lane-per-buffer scan with
+    """Strided CRC64NVME launches of >= 65536 buffers of <= 4 KiB take the lane-per-buffer scan with
     per-batch bases, seeds and results: three queued batches of 30000 x 3000 B (stride 3008), seeds
     on two of them."""
     import torch
