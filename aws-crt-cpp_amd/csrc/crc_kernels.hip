@@ -349,6 +349,24 @@ struct Braid32 {
     }
     // a * x^(8*256) ^ wn  (two 3-input XORs)
     __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
+#ifdef AMDCRC_XP_NOLOOKUP  // experiment builds only: the row step without its table lookups
+        return xor3(a * 0x9E3779B1u, wn, a >> 7);
+#endif
+#ifdef AMDCRC_XP_HALFLOOKUP  // experiment builds only: two of the four lookups
+        {
+            const uint32_t h3 = lds32(L, __builtin_amdgcn_perm(cst[0], a, sel[0]));
+            const uint32_t h2 = lds32(L, __builtin_amdgcn_perm(cst[1], a, sel[1]));
+            const uint32_t p1 = __builtin_amdgcn_perm(cst[2], a, sel[2]), p0 = __builtin_amdgcn_perm(cst[3], a, sel[3]);
+            return xor3(xor3(h3, h2, wn), p1 * 0x9E3779B1u, p0);
+        }
+#endif
+#ifdef AMDCRC_XP_PERMONLY  // experiment builds only: the lookups' address perms, no LDS reads
+        {
+            const uint32_t p3 = __builtin_amdgcn_perm(cst[0], a, sel[0]), p2 = __builtin_amdgcn_perm(cst[1], a, sel[1]);
+            const uint32_t p1 = __builtin_amdgcn_perm(cst[2], a, sel[2]), p0 = __builtin_amdgcn_perm(cst[3], a, sel[3]);
+            return xor3(xor3(p3, p2, wn), p1 * 0x9E3779B1u, p0);
+        }
+#endif
         uint32_t l3, l2, l1, l0;
         look(a, l3, l2, l1, l0);
         return xor3(xor3(l3, l2, wn), l1, l0);
@@ -895,6 +913,12 @@ struct LocalBufs {
 template <class B>
 __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc,
                                               const LocalBufs &lb) {
+#ifdef AMDCRC_XP_NOFINISH  // experiment builds only: tiles end without their finish
+    if (d.T == 1) {
+        if (lane == 0) finalize<false>(p, d.b, u, eng);
+        return;
+    }
+#endif
     const uint32_t r = wave_xor_s(eng.mulK(u, lane));
     if (!AMDCRC_GUARD_OK(d.b < p.nbuf && d.k < d.T, 2, d.b)) return;
     if (d.T == 1) {
@@ -994,6 +1018,9 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
     }
     BGroup ra, rb, rc;
+#ifdef AMDCRC_XP_RING4  // experiment builds only: four ring slots (three groups in flight)
+    BGroup rd;
+#endif
     if (work) {
         stream_issue<0>(ra, voff, f_addr());
         f_next();
@@ -1022,6 +1049,10 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     if (work) {
         stream_issue<0>(rb, voff, f_addr());
         f_next();
+#ifdef AMDCRC_XP_RING4
+        stream_issue<0>(rc, voff, f_addr());
+        f_next();
+#endif
     }
     bool consts_ready = false;
     // every wave publishes its share of the K image and P columns once and counts itself in LDS; a
@@ -1074,6 +1105,20 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     };
     // the first step is peeled (it publishes the constants, whose loads are then out of the loop),
     // so the loop header sees the same two ring slots in flight from the prologue and the back edge
+#ifdef AMDCRC_XP_RING4
+    step(ra, rd, true);
+    while (q < nq) {
+        step(rb, ra, false);
+        if (q >= nq) break;
+        step(rc, rb, false);
+        if (q >= nq) break;
+        step(rd, rc, false);
+        if (q >= nq) break;
+        step(ra, rd, false);
+    }
+    ring_drain(ra, rb, rc);
+    asm volatile("" : AMDCRC_R16(rd));
+#else
     step(ra, rc, true);
     while (q < nq) {
         step(rb, ra, false);
@@ -1083,6 +1128,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         step(ra, rc, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
+#endif
     stream_publish(p, acc, eng, lane);
 }
 

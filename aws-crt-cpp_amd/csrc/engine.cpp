@@ -311,7 +311,10 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 // another's streaming (4950 vs 4290 GiB/s with 3 streams).  Large batches are long
 // enough to amortise their own ramp and use both slots.  The W=64 streaming scan runs 512-thread
 // workgroups two per CU (66 KiB of LDS); the W=64 braided scan one 1024-thread workgroup per CU.
-constexpr uint64_t kSmallBatchBytes = 256ull << 20;
+#ifndef AMDCRC_SMALL_BATCH  // compile-time only (geometry experiments build a variant)
+#define AMDCRC_SMALL_BATCH (256ull << 20)
+#endif
+constexpr uint64_t kSmallBatchBytes = AMDCRC_SMALL_BATCH;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 constexpr uint64_t kLaneMaxBytes = 4096;
 // Strided CRC64NVME launches of short buffers take the lane-per-buffer scan once they hold enough

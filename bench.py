@@ -25,7 +25,7 @@ for one-batch launches.  `traffic` is HBM bytes per launch from the committed ro
 named in `traffic_source` (not measured in this run).
 
 Config legs (rank 0, N = 1; `configs`): C3 (16 x 256 MiB, CRC32 and CRC32C), C4's per-GPU shard
-(131072 x 8 KiB, 1/8 of 1M x 8 KiB), C5 (8 x 64 MiB, CRC64NVME and XXH64) and the north-star target
+(131072 x 8 KiB, 1/8 of 1M x 8 KiB; CRC32C and CRC64NVME), C5 (8 x 64 MiB, CRC64NVME and XXH64) and the north-star target
 shape (16 x 64 MiB CRC32C), each with value, kernel duration, roofline and cpu_baseline.  Never
 `value`.
 
@@ -547,6 +547,8 @@ def main():
             configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, **legs)
             configs["C4_shard_crc32c"] = config_leg(eng, "C4 per-GPU shard", "crc32c", 131072, 8192, streams, dev,
                                                     steps=20, **legs)
+            configs["C4_shard_crc64nvme"] = config_leg(eng, "C4 per-GPU shard", "crc64nvme", 131072, 8192, streams, dev,
+                                                       steps=20, **legs)
             configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, **legs)
             configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, **legs)
             configs["target_16x64MiB_crc32c"] = config_leg(eng, "north-star target", "crc32c", 16, 64 << 20, streams, dev,
