@@ -1018,9 +1018,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
     }
     BGroup ra, rb, rc;
-#ifdef AMDCRC_XP_RING4  // experiment builds only: four ring slots (three groups in flight)
-    BGroup rd;
-#endif
     if (work) {
         stream_issue<0>(ra, voff, f_addr());
         f_next();
@@ -1049,10 +1046,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     if (work) {
         stream_issue<0>(rb, voff, f_addr());
         f_next();
-#ifdef AMDCRC_XP_RING4
-        stream_issue<0>(rc, voff, f_addr());
-        f_next();
-#endif
     }
     bool consts_ready = false;
     // every wave publishes its share of the K image and P columns once and counts itself in LDS; a
@@ -1105,20 +1098,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     };
     // the first step is peeled (it publishes the constants, whose loads are then out of the loop),
     // so the loop header sees the same two ring slots in flight from the prologue and the back edge
-#ifdef AMDCRC_XP_RING4
-    step(ra, rd, true);
-    while (q < nq) {
-        step(rb, ra, false);
-        if (q >= nq) break;
-        step(rc, rb, false);
-        if (q >= nq) break;
-        step(rd, rc, false);
-        if (q >= nq) break;
-        step(ra, rd, false);
-    }
-    ring_drain(ra, rb, rc);
-    asm volatile("" : AMDCRC_R16(rd));
-#else
     step(ra, rc, true);
     while (q < nq) {
         step(rb, ra, false);
@@ -1128,7 +1107,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         step(ra, rc, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
-#endif
     stream_publish(p, acc, eng, lane);
 }
 
