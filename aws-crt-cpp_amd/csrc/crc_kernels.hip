@@ -18,6 +18,12 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
+#ifndef AMDCRC_STREAM_W8  // compile-time only: the W=32 streaming scan on 8-byte words (1) or 4-byte words (0)
+#define AMDCRC_STREAM_W8 1
+#endif
+
 #include "engine.h"
 #include "gf2.h"
 
@@ -394,6 +400,83 @@ struct Braid32 {
 
 struct BGroup {
     uint32_t w[kBraidRowsPerGroup];
+};
+
+// ---- the W=32 streaming scan on 8-byte words (crc32_stream_kernel<POLY, true>).  A row is 512
+// bytes, lane l owning the 8-byte word at 8l (one global_load_dwordx2 per lane: half the load
+// instructions of 4-byte words for the same bytes).  The row step is slice-by-8 for the 32-bit
+// register: a = (u ^ lo(w), hi(w)), u' = XOR_t T'_t[byte (7-t) of a] with
+// T'_t[e] = e * x^(8(t+1)) * x^(8*504), so the four lookups of hi(w) do not depend on u and only
+// half of a row's lookups sit on the braid's dependency chain.  Lane l's share is u * x^(-64 l).
+// LDS: the eight tables in 8 copies, one 256-byte row per entry e (table t at 32 t, copy c at 4 c:
+// the row is fully used, the constants region at kBKOff is unchanged).  In slot k < 4 a lane reads
+// byte q = (k + j) & 3 of lo (table 7 - q), in slot 4 + k the same byte of hi (table 3 - q), with
+// j = (lane >> 3) & 3 and copy lane & 7: a ds_read_b32 half-wave meets 32 distinct dword columns.
+constexpr uint32_t kW8Row = 512;
+constexpr int kW8RowsPerGroup = 8;  // 4 KiB per wave per ring slot, as the 4-byte rows
+static_assert(kW8Row * kW8RowsPerGroup == kBraidRow * kBraidRowsPerGroup, "ring slot size");
+
+template <uint32_t POLY>
+struct BraidW8Basis {
+    uint32_t b[9][8];  // b[t][i] = T'_t[1 << i] (t < 8); b[8][i] = T_0[1 << i]
+    constexpr BraidW8Basis() : b() {
+        const uint64_t skip = gf2_xpow8n(kW8Row - 8, POLY, 32);
+        for (int i = 0; i < 8; ++i) {
+            for (int t = 0; t < 8; ++t) b[t][i] = (uint32_t)gf2_mulmod(gf2_table_entry(1u << i, t, POLY), skip, POLY, 32);
+            b[8][i] = (uint32_t)gf2_table_entry(1u << i, 0, POLY);
+        }
+    }
+};
+template <uint32_t POLY, int K>
+__device__ __forceinline__ uint32_t basis_w8(uint32_t e) {
+    constexpr BraidW8Basis<POLY> B{};
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0u;
+    return v;
+}
+template <uint32_t POLY>
+__device__ __forceinline__ uint32_t basis_w8_rt(uint32_t t, uint32_t e) {  // t wave-uniform
+    switch (t) {
+        case 0: return basis_w8<POLY, 0>(e);
+        case 1: return basis_w8<POLY, 1>(e);
+        case 2: return basis_w8<POLY, 2>(e);
+        case 3: return basis_w8<POLY, 3>(e);
+        case 4: return basis_w8<POLY, 4>(e);
+        case 5: return basis_w8<POLY, 5>(e);
+        case 6: return basis_w8<POLY, 6>(e);
+        default: return basis_w8<POLY, 7>(e);
+    }
+}
+
+template <uint32_t POLY>
+struct Braid32W8 : Braid32<POLY> {
+    uint32_t cst8[8], sel8[8];
+    __device__ void init(const char *lds, int lane) {
+        this->L = lds;
+        const uint32_t j = ((uint32_t)lane >> 3) & 3u, c = (uint32_t)lane & 7u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = (k + j) & 3u;
+            cst8[k] = ((7u - q) << 5) | (c << 2);
+            cst8[4 + k] = ((3u - q) << 5) | (c << 2);
+            sel8[k] = sel8[4 + k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of the dword
+        }
+    }
+    // u' for a = (lo, hi): eight lookups, XORed with wn (the next row's lo word, or 0)
+    __device__ __forceinline__ uint32_t step_w8(uint32_t lo, uint32_t hi, uint32_t wn) const {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = lds32(this->L, __builtin_amdgcn_perm(cst8[k], lo, sel8[k]));
+            v[4 + k] = lds32(this->L, __builtin_amdgcn_perm(cst8[4 + k], hi, sel8[4 + k]));
+        }
+        return xor3(xor3(xor3(xor3(v[4], v[5], v[6]), v[7], v[0]), v[1], v[2]), v[3], wn);
+    }
+};
+
+struct W8Group {
+    uint64_t w[kW8RowsPerGroup];
 };
 
 // one payload word; NT: non-temporal (streamed once, not kept in the caches)
@@ -814,6 +897,43 @@ __device__ __forceinline__ uint32_t stream_rows(uint32_t x, BGroup &cur, BGroup 
     }
 }
 
+template <int R>
+__device__ __forceinline__ uint64_t gld_w8(uint32_t voff, uint64_t sbase) {
+    return __builtin_nontemporal_load((gu64 *)(sbase + voff + R * kW8Row));
+}
+
+// 8-byte rows: x = u ^ lo(w_r) is the chained value; row r's hi word enters its step directly
+template <int R, class B>
+__device__ __forceinline__ uint32_t stream_rows(uint32_t x, W8Group &cur, W8Group &nxt, uint32_t voff, uint64_t snext, const B &eng) {
+    if constexpr (R < kW8RowsPerGroup) {
+        nxt.w[R] = gld_w8<R>(voff, snext);
+        if constexpr (R == 0)
+            x ^= (uint32_t)cur.w[0];
+        else
+            x = eng.step_w8(x, (uint32_t)(cur.w[R - 1] >> 32), (uint32_t)cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return stream_rows<R + 1, B>(x, cur, nxt, voff, snext, eng);
+    } else {
+        return eng.step_w8(x, (uint32_t)(cur.w[kW8RowsPerGroup - 1] >> 32), 0u);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void stream_issue(W8Group &g, uint32_t voff, uint64_t s) {
+    if constexpr (R < kW8RowsPerGroup) {
+        g.w[R] = gld_w8<R>(voff, s);
+        stream_issue<R + 1>(g, voff, s);
+    }
+}
+
+#define AMDCRC_R8W(g) "+v"(g.w[0]), "+v"(g.w[1]), "+v"(g.w[2]), "+v"(g.w[3]), "+v"(g.w[4]), "+v"(g.w[5]), "+v"(g.w[6]), \
+    "+v"(g.w[7])
+__device__ __forceinline__ void ring_drain(W8Group &a, W8Group &b, W8Group &c) {
+    asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R8W(a)::"memory");
+    asm volatile("" : AMDCRC_R8W(b));
+    asm volatile("" : AMDCRC_R8W(c));
+}
+
 // Keep a ring slot's registers live up to this point.  A row load whose value is never read (the
 // placeholder rows past a wave's last group) would otherwise leave its destination registers "free"
 // to the compiler while the load is still in flight, and the returning data would overwrite whatever
@@ -954,9 +1074,10 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
 }
 
 // Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
-template <uint32_t POLY>
+template <uint32_t POLY, bool W8>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const ScanParams p) {
-    using B = Braid32<POLY>;
+    using B = typename std::conditional<W8, Braid32W8<POLY>, Braid32<POLY>>::type;
+    using Grp = typename std::conditional<W8, W8Group, BGroup>::type;
     __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
 
     const int lane = threadIdx.x & 63;
@@ -969,7 +1090,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     const uint32_t G = p.seg / kGroupBytes;
     const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = 4u * (uint32_t)lane;
+    const uint32_t voff = (W8 ? 8u : 4u) * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
     const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
     const uint32_t gsh = __builtin_ctz(G);
@@ -1009,7 +1130,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     // loads: issued before the first group, so the compiler's wait for them in the peeled first step
     // is the exact count of the row loads issued after them)
     const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + 4 * threadIdx.x);
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + (W8 ? kBraidK64Word : 0) + 4 * threadIdx.x);
     const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
     // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
     LocalBufs lb{0, 0};
@@ -1017,12 +1138,24 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
         if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
     }
-    BGroup ra, rb, rc;
+    Grp ra, rb, rc;
     if (work) {
         stream_issue<0>(ra, voff, f_addr());
         f_next();
     }
-    {
+    if constexpr (W8) {
+        // wave t builds table T'_t (t wave-uniform): entries lane + 64 n, 8 copies (two 16-byte stores)
+        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint32_t e = (uint32_t)lane + 64u * n;
+            const uint32_t te = basis_w8_rt<POLY>(t, e);
+            char *row = lds + (e << 8) + (t << 5);
+            *(uint4 *)row = make_uint4(te, te, te, te);
+            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
+        }
+        if (threadIdx.x < 256) *(uint32_t *)(lds + kT0Off + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
+    } else {
         const uint32_t i = threadIdx.x;
         const uint32_t q = (i >> 1) & 3u, h = i & 1u;
         uint32_t bq[8];
@@ -1082,7 +1215,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     uint32_t q = 0;  // groups scanned
     BGroupAcc acc{};
     acc.slot = ~0ull;
-    auto step = [&](BGroup &cur, BGroup &nxt, bool first) {
+    auto step = [&](Grp &cur, Grp &nxt, bool first) {
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
         const uint64_t sn = f_addr();
         f_next();
@@ -2187,7 +2320,7 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     switch (alg) {
         case ALG_CRC32:
             if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev);
+                launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
@@ -2195,7 +2328,7 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             break;
         case ALG_CRC32C:
             if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
+                launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
             else

@@ -190,6 +190,15 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
         for (int i = 0; i < 1024; ++i)
             c[2048 + i] = (uint32_t)gf2_mulmod(gf2_table_entry(i & 255, i >> 8, poly), skip, poly, 32);
         for (int e = 0; e < 256; ++e) c[3072 + e] = (uint32_t)gf2_table_entry(e, 0, poly);
+        kl = 0x80000000u;  // the streaming scan's lanes own 8-byte words: K_l = x^(-64 l)
+        for (int l = 0; l < 64; ++l) {
+            uint32_t col = kl;
+            for (int j = 0; j < 32; ++j) {
+                c[kBraidK64Word + ((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
+                col = (uint32_t)gf2_mulx(col, poly);
+            }
+            for (int i = 0; i < 64; ++i) kl = inv_mulx32(kl, poly);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;

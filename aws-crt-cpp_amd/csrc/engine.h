@@ -73,10 +73,12 @@ struct ScanParams {
 //   [2048, 3072)  T'_k[e] = e * x^(8(k+1) + 8*252): slice-by-4 step that also skips the other
 //                 63 lanes' words of a 256-byte row
 //   [3072, 3328)  T_0[e] = e * x^8: plain byte step for head / tail bytes
+//   [3328, 5376)  K-matrix image of x^(-64 l) (the streaming scan's 8-byte words), same layout
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 3328;
+constexpr int kBraidConstWords = 5376;
+constexpr int kBraidK64Word = 3328;  // first word of the x^(-64 l) K image
 
 struct XxhParams {
     const uint64_t *d_ptrs;  // device addresses (list) or null (strided)
