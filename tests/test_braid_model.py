@@ -175,3 +175,82 @@ def test_braid_model_vs_oracle(braid, rows):
             want = oracle.crc(alg, data, seed)
             got = braid_model(br, data, 0x1000 + misalign, seed, rows)
             assert got == want, (alg, rows, n, misalign, hex(seed))
+
+
+# ---- the streaming scan on 8-byte words (crc32_stream_kernel<POLY, true>)
+ROW8 = 512
+
+
+class BraidW8:
+    """512-byte rows, lane l owning the 8-byte word at 8l; the row step is slice-by-8 on
+    a = (u ^ lo(w), hi(w)) with T'_t[e] = e * x^(8(t+1)) * x^(8*504); K_l = x^(-64 l)."""
+
+    def __init__(self, alg):
+        P = self.P = POLY[alg]
+        skip = xpow8n(ROW8 - 8, P)
+        self.Tp = [[mulmod(table_entry(e, t, P), skip, P) for e in range(256)] for t in range(8)]
+        self.K = []
+        kl = 0x80000000
+        for _ in range(64):
+            self.K.append(kl)
+            for _ in range(64):
+                kl = inv_mulx(kl, P)
+
+    def step(self, lo, hi):
+        v = 0
+        for i in range(4):
+            v ^= self.Tp[7 - i][(lo >> (8 * i)) & 255] ^ self.Tp[3 - i][(hi >> (8 * i)) & 255]
+        return v
+
+
+def lds_w8_schedule(lane):
+    """(slot -> (which dword, byte q, table t, column)) of the kernel's Braid32W8::init"""
+    j, c = (lane >> 3) & 3, lane & 7
+    out = []
+    for k in range(8):
+        q = ((k & 3) + j) & 3
+        hi = k >= 4
+        t = (3 - q) if hi else (7 - q)
+        out.append((hi, q, t, t * 8 + c))
+    return out
+
+
+def test_w8_lds_schedule_conflict_free_and_complete():
+    for half in (range(32), range(32, 64)):
+        for k in range(8):
+            cols = [lds_w8_schedule(l)[k][3] for l in half]
+            assert len(set(cols)) == 32, k  # one dword column (bank) per lane: conflict-free
+    for lane in range(64):
+        seen = {(hi, q) for hi, q, _, _ in lds_w8_schedule(lane)}
+        assert seen == {(h, q) for h in (False, True) for q in range(4)}  # all 8 bytes, once each
+        for hi, q, t, _ in lds_w8_schedule(lane):
+            assert t == 7 - (4 * hi + q)  # byte i of the 8-byte a indexes T'_(7-i)
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
+@pytest.mark.parametrize("rows", [1, 8, 24])
+def test_braid_w8_model_vs_oracle(alg, rows):
+    """whole-tile buffers (the streaming scan's case): lanes run the fused chain of the kernel's
+    stream_rows (x = u ^ lo(w_r); hi(w_r) enters its own step), shares combine with K_l, tiles
+    with x^(8*TILE*(T-1-k))"""
+    br = BraidW8(alg)
+    P = br.P
+    rnd = random.Random(hash((alg, rows, "w8")) & 0xFFFF)
+    tile = ROW8 * rows
+    for ntiles in (1, 2, 3):
+        data = bytes(rnd.getrandbits(8) for _ in range(tile * ntiles))
+        seed = rnd.choice([0, rnd.getrandbits(32)])
+        fin = 0
+        for k in range(ntiles):
+            r = 0
+            for lane in range(64):
+                u = (~seed & M32) if (k == 0 and lane == 0) else 0
+                words = [int.from_bytes(data[k * tile + ROW8 * c + 8 * lane: k * tile + ROW8 * c + 8 * lane + 8], "little")
+                         for c in range(rows)]
+                x = u ^ (words[0] & M32)
+                for c in range(1, rows):
+                    x = br.step(x, words[c - 1] >> 32) ^ (words[c] & M32)
+                u = br.step(x, words[-1] >> 32)
+                r ^= mulmod(u, br.K[lane], P)
+            fin ^= mulmod(r, xpow8n(tile * (ntiles - 1 - k), P), P)
+        assert (~fin & M32) == oracle.crc(alg, data, seed), (alg, rows, ntiles)
