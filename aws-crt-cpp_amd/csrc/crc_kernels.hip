@@ -1310,7 +1310,12 @@ __device__ __forceinline__ uint64_t basis64_rt(uint32_t t, uint32_t e) {  // t w
 // copies; slots 4..7 read the other dword.  (A layout with 4 tables per instruction met 16 columns:
 // 2-way conflicts.)  tests/test_braid64_model.py::test_four_copy_layout checks the schedule.
 constexpr uint32_t kB64x4T0Off = 65536;
-constexpr uint32_t kB64x4Lds = kB64x4T0Off + 2048;
+// the tile finish's per-lane nibble multiples NT_l[v] = sum_(i<4) bit(3-i) of v * K_l x^i (64 lanes x
+// 16 x u64) and R4[u] = u * x^4 (16 x u64): see Braid64::mulK
+constexpr uint32_t kB64x4NibOff = kB64x4T0Off + 2048;
+constexpr uint32_t kB64x4R4Off = kB64x4NibOff + 64 * 16 * 8;
+constexpr uint32_t kB64x4Lds = kB64x4R4Off + 16 * 8;
+static_assert(2 * kB64x4Lds <= 160 * 1024, "two crc64_stream4_kernel workgroups per CU");
 
 template <uint64_t POLY, int COPIES = 8>
 struct Braid64 {
@@ -1320,9 +1325,11 @@ struct Braid64 {
     uint32_t cst[4], csth[4], sel[4];
     uint32_t lowmask;  // COPIES = 4: ~0 for lanes whose slots 0..3 read the low dword
     uint64_t kl;       // K_l = x^(-64 l)
+    const char *nib;   // COPIES = 4: this lane's nibble multiples NT_l
 
     __device__ void init(const char *lds, int lane) {
         L = lds;
+        nib = lds + kB64x4NibOff + 128u * (uint32_t)lane;
         if (COPIES == 8) {
             const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
 #pragma unroll
@@ -1371,12 +1378,30 @@ struct Braid64 {
     __device__ __forceinline__ uint64_t byte(uint64_t s, uint32_t b) const {
         return (s >> 8) ^ lds64(L, (COPIES == 8 ? kB64T0Off : kB64x4T0Off) + 8 * (((uint32_t)s ^ b) & 0xffu));
     }
+    // r * K_l with the nibble multiples in LDS (COPIES = 4): the byte-Horner form below with each
+    // B_m = NT_l[high nibble] ^ NT_l[low nibble] * x^4, and a * x^4 = (a >> 4) ^ R4[a & 15].  24 LDS
+    // reads and ~60 VALU for the bytes of r instead of ~190 VALU of masked column XORs.
+    // tests/test_braid64_model.py::test_mulk_nibble_tables models it.
+    __device__ __forceinline__ uint64_t mulK_nib(uint64_t r) const {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int m = 7; m >= 0; --m) {
+            const uint32_t word = (7 - m) < 4 ? (uint32_t)r : (uint32_t)(r >> 32);
+            const int sh = 8 * ((7 - m) & 3);
+            const uint64_t nh = lds64(nib, 8u * ((word >> (sh + 4)) & 15u));
+            const uint64_t nl = lds64(nib, 8u * ((word >> sh) & 15u));
+            const uint64_t b = nh ^ (nl >> 4) ^ lds64(L, kB64x4R4Off + 8u * ((uint32_t)nl & 15u));
+            acc = m == 7 ? b : (acc >> 8) ^ lds64(L, kB64x4T0Off + 8u * ((uint32_t)acc & 0xffu)) ^ b;
+        }
+        return acc;
+    }
     // r * K_l (once per tile), Horner over the bytes of r: bit 63-j of r pairs with K_l * x^j, so
     // with B_m = sum_i bit(63-8m-i) * K_l x^i (byte 7-m of r against the eight columns K_l x^i),
     // r * K_l = sum_m B_m x^(8m) = (((B_7 x^8 ^ B_6) x^8 ^ ...) ^ B_0, and a * x^8 is one plain
     // byte step, (a >> 8) ^ T0[a & 0xff].  About 230 VALU and 7 LDS reads instead of a 64-step
     // bit-serial product (~950 VALU).  tests/test_braid64_model.py::test_mulk_byte_horner models it.
     __device__ __forceinline__ uint64_t mulK(uint64_t r) const {
+        if constexpr (COPIES == 4) return mulK_nib(r);
         uint32_t cl[8], ch[8];
         uint64_t b = kl;
 #pragma unroll
@@ -1544,6 +1569,32 @@ __device__ __forceinline__ void b64x4_build_tables(char *lds) {
         *(v4u *)(row + ((((i >> 2) & 1u) ^ 1u) << 4)) = vv;
     }
     if (i < 256) *(uint64_t *)(lds + kB64x4T0Off + 8 * i) = basis64<POLY, 8>(i);
+}
+
+// the tile finish's nibble tables (Braid64<POLY, 4>::mulK_nib): thread i fills NT_l[v] of lane
+// l = i & 63 (its own K_l) for v = i >> 6 and v + 8; threads below 16 fill R4
+template <uint64_t POLY>
+__device__ __forceinline__ void b64x4_build_nib(char *lds, uint64_t kl) {
+    const uint32_t i = threadIdx.x;
+    if (i >= 512) return;
+    uint64_t c[4];
+    c[0] = kl;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) c[k] = gf2_mulx(c[k - 1], POLY);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t v = (i >> 6) + 8u * h;
+        uint64_t a = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a ^= ((v >> (3 - k)) & 1u) ? c[k] : 0ull;
+        *(uint64_t *)(lds + kB64x4NibOff + 128u * (i & 63u) + 8u * v) = a;
+    }
+    if (i < 16) {
+        uint64_t u = i;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u = gf2_mulx(u, POLY);
+        *(uint64_t *)(lds + kB64x4R4Off + 8u * i) = u;
+    }
 }
 
 template <uint64_t POLY, bool LIST, bool NT = true>
@@ -1780,6 +1831,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
         f_next();
     }
     b64x4_build_tables<POLY>(lds);
+    b64x4_build_nib<POLY>(lds, kl);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);

@@ -178,6 +178,36 @@ def braid64_model(br, data, addr, seed, rows):
     return ~fin & M64
 
 
+def test_mulk_nibble_tables(br):
+    """Braid64<POLY, 4>::mulK_nib: per-lane nibble multiples NT_l[v] = sum_(i<4) bit(3-i) of v *
+    K_l x^i, B_m = NT_l[hi nibble] ^ NT_l[lo nibble] * x^4 with a * x^4 = (a >> 4) ^ R4[a & 15],
+    then the byte-Horner chain through T0"""
+    R4 = []
+    for u in range(16):
+        a = u
+        for _ in range(4):
+            a = mulx(a)
+        R4.append(a)
+    rng = random.Random(11)
+    for lane in range(64):
+        c = [br.K[lane]]
+        for _ in range(3):
+            c.append(mulx(c[-1]))
+        NT = [0] * 16
+        for v in range(16):
+            for i in range(4):
+                if (v >> (3 - i)) & 1:
+                    NT[v] ^= c[i]
+        for r in (0, 1, 1 << 63, M64, rng.getrandbits(64), rng.getrandbits(64)):
+            acc = None
+            for m in range(7, -1, -1):
+                byte = (r >> (8 * (7 - m))) & 0xFF
+                nl = NT[byte & 15]
+                b = NT[byte >> 4] ^ (nl >> 4) ^ R4[nl & 15]
+                acc = b if acc is None else (acc >> 8) ^ br.T0[acc & 0xFF] ^ b
+            assert acc == mulmod(r, br.K[lane]), (lane, hex(r))
+
+
 def test_mulk_byte_horner(br):
     rng = random.Random(7)
     for lane in range(64):
