@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Ragged-list scans (crc32_braid_kernel<LIST>) against the strided streaming scan on the same bytes:
+dispatch-stamped kernel time (median of `reps`) for a few list shapes."""
+import json
+import os
+import random
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import torch  # noqa: E402
+
+import aws_crt_amd as eng  # noqa: E402
+
+
+def timed(fn, reps=12):
+    out = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e1.record()
+        eng.time_next_launch(e0, e1)
+        fn()
+        torch.cuda.synchronize()
+        out.append(eng.event_ms(e0, e1) * 1e3)
+    return statistics.median(out)
+
+
+def main():
+    eng.init()
+    alg = eng.CRC32C
+    total = 256 << 20
+    data = torch.randint(0, 256, (2 * total + 4096,), dtype=torch.uint8, device="cuda")
+    base = data.data_ptr()
+    rnd = random.Random(1)
+    res = {}
+    L = 65536
+    n = total // L
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    res["strided_4096x64KiB"] = timed(lambda: eng.checksum_strided(alg, data, L, L, n, out=out))
+    ptrs, lens = [base + i * L for i in range(n)], [L] * n
+    res["list_4096x64KiB_aligned"] = timed(lambda: eng.checksum_list(alg, ptrs, lens, out=out))
+    lens2 = [rnd.randrange(32 << 10, 96 << 10) for _ in range(n)]
+    ptrs2, a = [], base + 5
+    for ln in lens2:
+        ptrs2.append(a)
+        a += ln + rnd.randrange(0, 64)
+    res["list_4096_ragged_32-96KiB_unaligned"] = timed(lambda: eng.checksum_list(alg, ptrs2, lens2, out=out))
+    res["list_ragged_bytes"] = sum(lens2)
+    for k in list(res):
+        if k.startswith(("strided", "list_4096x")):
+            res[k + "_gibs"] = round(total / (res[k] * 1e-6) / 2**30, 1)
+    res["list_4096_ragged_32-96KiB_unaligned_gibs"] = round(sum(lens2) / (res["list_4096_ragged_32-96KiB_unaligned"] * 1e-6) / 2**30, 1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
