@@ -164,6 +164,14 @@ __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walke
     return d;
 }
 
+// Front pad of a buffer's first tile: the braids stay zero through the virtual zero rows (u starts
+// at 0 and T'(0) = 0), so the scans start at the group holding the pad's end, and a group is
+// "clean" (no zeroed rows, no head-state injection: the fused load-and-scan path) once it starts
+// past the pad.  A wave group is 4 KiB for both widths (16 rows of 256 B, 8 of 512 B).
+constexpr uint32_t kWaveGroupBytes = 4096;
+__device__ __forceinline__ uint32_t first_group(uint32_t pad) { return pad / kWaveGroupBytes; }
+__device__ __forceinline__ bool group_clean(uint32_t pad, uint32_t g) { return pad == 0 || pad < g * kWaveGroupBytes; }
+
 // bytes [a, end) folded into state s (a < end, both inside 16-aligned blocks read by SMEM)
 template <class E>
 __device__ __forceinline__ typename E::T fold_bytes(typename E::T s, uint64_t a, uint64_t end, const E &eng) {
@@ -512,7 +520,7 @@ __device__ __forceinline__ void braid_load(BGroup &g, uint64_t vbase, uint32_t p
 template <class B>
 __device__ __forceinline__ uint32_t braid_proc(uint32_t u, const BGroup &g, const B &eng, const Tile &d, uint32_t gi,
                                                int lane, uint32_t s_h) {
-    if (d.pad == 0) {
+    if (group_clean(d.pad, gi)) {
         uint32_t a = u ^ g.w[0];
 #pragma unroll
         for (int r = 0; r + 1 < kBraidRowsPerGroup; ++r) a = eng.step_x(a, g.w[r + 1]);
@@ -685,6 +693,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
         const Tile d = make_tile<LIST>(p, tf, wf);
         if (d.ngroups) {
             fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
+            gf = first_group(d.pad);
             any = true;
             break;
         }
@@ -703,7 +712,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
                 fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
                 wf = w2;
                 tf = t;
-                gf = 0;
+                gf = first_group(d.pad);
                 return;
             }
         }
@@ -716,7 +725,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
                 const Tile d = make_tile<LIST>(p, t, w2);
                 fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
                 tf = t;
-                gf = 0;
+                gf = first_group(d.pad);
                 if (fifo_n == 0) fifo0 = t; else fifo1 = t;
                 ++fifo_n;
                 return;
@@ -796,6 +805,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     uint64_t tp = t0;
     uint32_t gp = 0;
     Tile dp = make_tile<LIST>(p, tp, wp);
+    gp = first_group(dp.pad);
     uint32_t s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0u;
     uint32_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
     BPending pd{};
@@ -825,7 +835,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
             await_consts();
             braid_finish<LIST>(p, dp, u, s_h, eng, lane, acc, pd);
             if (!next_scan()) return false;
-            gp = 0;
+            gp = first_group(dp.pad);
             s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0u;
             u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0u;
         }
@@ -838,7 +848,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     auto ring_step = [&](const BGroup &cur, BGroup &dst) {
         if (pf_done) {
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
-        } else if (dp.pad == 0 && fpad == 0) {
+        } else if (group_clean(dp.pad, gp) && group_clean(fpad, gf)) {
             u = braid_fused<1, NT>(u, cur, dst, fvb + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
         } else {
             braid_load<NT>(dst, fvb, fpad, gf, lane);
@@ -1475,7 +1485,7 @@ __device__ __forceinline__ void b64_load(B64Group &g, uint64_t vbase, uint32_t p
 template <class B>
 __device__ __forceinline__ uint64_t b64_proc(uint64_t u, const B64Group &g, const B &eng, const Tile &d, uint32_t gi,
                                              int lane, uint64_t s_h) {
-    if (d.pad == 0) {
+    if (group_clean(d.pad, gi)) {
         uint64_t a = u ^ g.w[0];
 #pragma unroll
         for (int r = 0; r + 1 < kB64RowsPerGroup; ++r) a = eng.step_x(a, g.w[r + 1]);
@@ -1643,6 +1653,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
         const Tile d = make_tile<LIST>(p, tf, wf);
         if (d.ngroups) {
             fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
+            gf = first_group(d.pad);
             any = true;
             break;
         }
@@ -1661,7 +1672,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
                 fvb = d.vbase, fpad = d.pad, fng = d.ngroups;
                 wf = w2;
                 tf = t;
-                gf = 0;
+                gf = first_group(d.pad);
                 return;
             }
         }
@@ -1684,6 +1695,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     uint64_t tp = t0;
     uint32_t gp = 0;
     Tile dp = make_tile<LIST>(p, tp, wp);
+    gp = first_group(dp.pad);
     uint64_t s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0ull;
     uint64_t u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
 
@@ -1692,7 +1704,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
             b64_finish<LIST>(p, dp, u, s_h, eng, lane);
             if (++tp >= t1) return false;
             dp = make_tile<LIST>(p, tp, wp);
-            gp = 0;
+            gp = first_group(dp.pad);
             s_h = dp.k == 0 ? head_state<LIST>(p, dp.b, eng) : 0ull;
             u = (dp.k == 0 && dp.pad == 0 && lane == 0) ? s_h : 0ull;
         }
@@ -1701,7 +1713,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     auto ring_step = [&](const B64Group &cur, B64Group &dst) {
         if (pf_done) {
             u = b64_proc(u, cur, eng, dp, gp, lane, s_h);
-        } else if (dp.pad == 0 && fpad == 0) {
+        } else if (group_clean(dp.pad, gp) && group_clean(fpad, gf)) {
             u = b64_fused<NT>(u, cur, dst, fvb + gf * (kB64Row * kB64RowsPerGroup) + 8u * lane, eng);
         } else {
             b64_load<NT>(dst, fvb, fpad, gf, lane);

@@ -49,9 +49,20 @@ def main():
         a += ln + rnd.randrange(0, 64)
     res["list_4096_ragged_32-96KiB_unaligned"] = timed(lambda: eng.checksum_list(alg, ptrs2, lens2, out=out))
     res["list_ragged_bytes"] = sum(lens2)
-    for k in list(res):
-        if k.startswith(("strided", "list_4096x")):
-            res[k + "_gibs"] = round(total / (res[k] * 1e-6) / 2**30, 1)
+    # which of the two costs: raggedness (aligned starts, lengths a multiple of 16) or misalignment
+    # (uniform 64 KiB buffers starting 5 bytes past 16-byte alignment)
+    lens3 = [16 * rnd.randrange(2 << 10, 6 << 10) for _ in range(n)]
+    ptrs3, a = [], base
+    for ln in lens3:
+        ptrs3.append(a)
+        a += ln
+    res["list_4096_ragged_aligned"] = timed(lambda: eng.checksum_list(alg, ptrs3, lens3, out=out))
+    res["list_4096_ragged_aligned_gibs"] = round(sum(lens3) / (res["list_4096_ragged_aligned"] * 1e-6) / 2**30, 1)
+    ptrs4 = [base + 5 + i * L for i in range(n)]
+    res["list_4096x64KiB_unaligned"] = timed(lambda: eng.checksum_list(alg, ptrs4, lens, out=out))
+    res["list_4096x64KiB_unaligned_gibs"] = round(total / (res["list_4096x64KiB_unaligned"] * 1e-6) / 2**30, 1)
+    for k in ("strided_4096x64KiB", "list_4096x64KiB_aligned"):
+        res[k + "_gibs"] = round(total / (res[k] * 1e-6) / 2**30, 1)
     res["list_4096_ragged_32-96KiB_unaligned_gibs"] = round(sum(lens2) / (res["list_4096_ragged_32-96KiB_unaligned"] * 1e-6) / 2**30, 1)
     print(json.dumps(res))
 
