@@ -363,24 +363,6 @@ struct Braid32 {
     }
     // a * x^(8*256) ^ wn  (two 3-input XORs)
     __device__ __forceinline__ uint32_t step_x(uint32_t a, uint32_t wn) const {
-#ifdef AMDCRC_XP_NOLOOKUP  // experiment builds only: the row step without its table lookups
-        return xor3(a * 0x9E3779B1u, wn, a >> 7);
-#endif
-#ifdef AMDCRC_XP_HALFLOOKUP  // experiment builds only: two of the four lookups
-        {
-            const uint32_t h3 = lds32(L, __builtin_amdgcn_perm(cst[0], a, sel[0]));
-            const uint32_t h2 = lds32(L, __builtin_amdgcn_perm(cst[1], a, sel[1]));
-            const uint32_t p1 = __builtin_amdgcn_perm(cst[2], a, sel[2]), p0 = __builtin_amdgcn_perm(cst[3], a, sel[3]);
-            return xor3(xor3(h3, h2, wn), p1 * 0x9E3779B1u, p0);
-        }
-#endif
-#ifdef AMDCRC_XP_PERMONLY  // experiment builds only: the lookups' address perms, no LDS reads
-        {
-            const uint32_t p3 = __builtin_amdgcn_perm(cst[0], a, sel[0]), p2 = __builtin_amdgcn_perm(cst[1], a, sel[1]);
-            const uint32_t p1 = __builtin_amdgcn_perm(cst[2], a, sel[2]), p0 = __builtin_amdgcn_perm(cst[3], a, sel[3]);
-            return xor3(xor3(p3, p2, wn), p1 * 0x9E3779B1u, p0);
-        }
-#endif
         uint32_t l3, l2, l1, l0;
         look(a, l3, l2, l1, l0);
         return xor3(xor3(l3, l2, wn), l1, l0);
@@ -1062,12 +1044,6 @@ struct LocalBufs {
 template <class B>
 __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc,
                                               const LocalBufs &lb) {
-#ifdef AMDCRC_XP_NOFINISH  // experiment builds only: tiles end without their finish
-    if (d.T == 1) {
-        if (lane == 0) finalize<false>(p, d.b, u, eng);
-        return;
-    }
-#endif
     const uint32_t r = wave_xor_s(eng.mulK(u, lane));
     if (!AMDCRC_GUARD_OK(d.b < p.nbuf && d.k < d.T, 2, d.b)) return;
     if (d.T == 1) {
