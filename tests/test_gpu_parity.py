@@ -245,6 +245,33 @@ def test_fuzz_lengths_alignments_seeds(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("alg", ["crc32c", "crc64nvme"])
+def test_list_front_pads_at_group_boundaries(engine, alg):
+    """Braided list scans start a buffer's first tile at the 4 KiB group holding its front pad's end
+    (DESIGN.md §3.3).  A 64 MiB list of 16 KiB buffers sets 16 KiB tiles (four groups); buffers of
+    T tiles minus pads of 4096 k + {0, 16, 4080} bytes (k < 4) put the pad's end on, just past and
+    just before every group boundary, at aligned and unaligned starts, with seeds."""
+    import torch
+
+    rng = random.Random(0x9AD + ALG[alg])
+    special = [16384 * T - (4096 * k + dl) for T in (1, 2, 3) for k in range(4) for dl in (0, 16, 4080)
+               if 16384 * T - (4096 * k + dl) > 0]
+    lens = [16384] * 4000 + special * 4
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for ln in lens:
+        pos = (pos + 15) // 16 * 16 + rng.choice([0, 0, 3, 9])
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 0x9AD)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
 def test_checksum_batches(engine, alg):
     """aws_crt_amd_checksum_batches: 37 batches of one shape (more than one launch holds), each with its
