@@ -541,6 +541,62 @@ __device__ __forceinline__ uint32_t braid_fused(uint32_t u, const BGroup &g, BGr
     return x;
 }
 
+// The same three steps on 8-byte words (crc32_braid_kernel<POLY, LIST, NT, true>): group gi is rows
+// [8 gi, 8 gi + 8) of 512 bytes, this lane's word at virtual offset gi*4096 + 512 r + 8 lane; the row
+// step splits into the lo word's lookups (the chain) and the hi word's, looked up one row ahead.
+template <bool NT>
+__device__ __forceinline__ uint64_t ldpay8(uint64_t a) {
+    if (NT) return __builtin_nontemporal_load((gu64 *)a);
+    return *(gu64 *)a;
+}
+template <bool NT>
+__device__ __forceinline__ void braid_load(W8Group &g, uint64_t vbase, uint32_t pad, uint32_t gi, int lane) {
+    const uint32_t vo0 = gi * (kW8Row * kW8RowsPerGroup) + 8u * lane;
+#pragma unroll
+    for (int r = 0; r < kW8RowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kW8Row * r;
+        g.w[r] = ldpay8<NT>(vbase + (vo >= pad ? vo : pad));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+template <class B>
+__device__ __forceinline__ uint32_t braid_proc(uint32_t u, const W8Group &g, const B &eng, const Tile &d, uint32_t gi,
+                                               int lane, uint32_t s_h) {
+    if (group_clean(d.pad, gi)) {
+        uint32_t x = u ^ (uint32_t)g.w[0];
+        typename B::Hi h = eng.look_hi((uint32_t)(g.w[0] >> 32));
+#pragma unroll
+        for (int r = 1; r < kW8RowsPerGroup; ++r) {
+            x = eng.look_lo(x, h, (uint32_t)g.w[r]);
+            h = eng.look_hi((uint32_t)(g.w[r] >> 32));
+        }
+        return eng.look_lo(x, h, 0u);
+    }
+    const uint32_t vo0 = gi * (kW8Row * kW8RowsPerGroup) + 8u * lane;
+#pragma unroll
+    for (int r = 0; r < kW8RowsPerGroup; ++r) {
+        const uint32_t vo = vo0 + kW8Row * r;
+        uint64_t w = vo >= d.pad ? g.w[r] : 0ull;
+        if (vo == d.pad) w ^= s_h;  // this braid is still zero here: the head state enters with the word
+        u = eng.look_lo(u ^ (uint32_t)w, eng.look_hi((uint32_t)(w >> 32)), 0u);
+    }
+    return u;
+}
+template <int RATE, bool NT, class B>
+__device__ __forceinline__ uint32_t braid_fused(uint32_t u, const W8Group &g, W8Group &dst, uint64_t a, const B &eng) {
+    static_assert(RATE == 1, "one load per row step");
+    uint32_t x = u ^ (uint32_t)g.w[0];
+    typename B::Hi h{};
+#pragma unroll
+    for (int r = 0; r < kW8RowsPerGroup; ++r) {
+        dst.w[r] = ldpay8<NT>(a + kW8Row * r);
+        if (r > 0) x = eng.look_lo(x, h, (uint32_t)g.w[r]);
+        h = eng.look_hi((uint32_t)(g.w[r] >> 32));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return eng.look_lo(x, h, 0u);
+}
+
 // Cross-tile combine.  Tiles form groups of 32; tile k's register is moved to its group's end
 // (r * x^(8*TILE*m), m < 32: columns in LDS, one per lane).  A wave merges the shares of its own
 // tiles of one group in registers {arrival bits | XOR} and publishes them with one 64-bit atomic XOR
@@ -628,9 +684,10 @@ __device__ __forceinline__ void braid_finish(const ScanParams &p, const Tile &d,
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
-template <uint32_t POLY, bool LIST, bool NT = true>
+template <uint32_t POLY, bool LIST, bool NT = true, bool W8 = AMDCRC_STREAM_W8>
 __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanParams p) {
-    using B = Braid32<POLY>;
+    using B = typename std::conditional<W8, Braid32W8<POLY>, Braid32<POLY>>::type;
+    using Grp = typename std::conditional<W8, W8Group, BGroup>::type;
     __shared__ __attribute__((aligned(16))) char lds[kBraidLds];
 
     const int lane = threadIdx.x & 63;
@@ -717,7 +774,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     };
     // K-image word and P column of this thread: needed only when a tile finishes, so they are
     // published to LDS after the first group is scanned (see publish_consts), not before the scan
-    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + 4 * threadIdx.x);  // 16 B of the 8 KiB image
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + (W8 ? kBraidK64Word : 0) + 4 * threadIdx.x);  // 16 B of the 8 KiB image
     const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
     const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
     // prime the first group unconditionally (a wave without payload reads the 13 KiB constant block).
@@ -725,10 +782,24 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // memory system is saturated (every CU primes at once), so priming two groups kept the first scan
     // waiting for 8 KiB per wave to be accepted.  The ring scans group 0 while group 1's loads go out
     // between its table steps.
-    BGroup r0, r1;
+    Grp r0, r1;
     braid_load<NT>(r0, any ? fvb : (uint64_t)p.d_kvals, any ? fpad : 0u, any ? gf : 0u, lane);
     if (any && !dyn) pf_advance();  // pool mode: after the barrier, where the pool counter is set up
-    {
+    if constexpr (W8) {
+        // the eight slice-by-8 tables, 8 copies (as crc32_stream_kernel<POLY, true>)
+        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint32_t e = (uint32_t)lane + 64u * n;
+            const uint32_t te = basis_w8_rt<POLY>(t, e);
+            char *row = lds + (e << 8) + (t << 5);
+            *(uint4 *)row = make_uint4(te, te, te, te);
+            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
+        }
+        if (threadIdx.x < 256) *(uint32_t *)(lds + kT0Off + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
+        if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
+        if (threadIdx.x == 0) *(uint32_t *)(lds + kPoolOff) = 0u;
+    } else {
         // T' (4 tables x 256 entries, 8 copies each) and T0 from the compile-time bases.  One 16-byte
         // store = 4 copies of one (table, entry); the 8 lanes of a ds_write_b128 group take the 8
         // (quarter, half) slots of a row, so each group fills 128 distinct bytes (no bank conflict).
@@ -827,11 +898,11 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // one ring step: scan `cur` (group gp of tile dp) and load `dst` with the prefetch cursor's group
     // (once the prefetch cursor is parked on the wave's last group that group is already in flight:
     // a second load of it would be pure extra traffic -- non-temporal loads do not leave it in L2)
-    auto ring_step = [&](const BGroup &cur, BGroup &dst) {
+    auto ring_step = [&](const Grp &cur, Grp &dst) {
         if (pf_done) {
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
         } else if (group_clean(dp.pad, gp) && group_clean(fpad, gf)) {
-            u = braid_fused<1, NT>(u, cur, dst, fvb + gf * (kBraidRow * kBraidRowsPerGroup) + 4u * lane, eng);
+            u = braid_fused<1, NT>(u, cur, dst, fvb + gf * (kBraidRow * kBraidRowsPerGroup) + (W8 ? 8u : 4u) * lane, eng);
         } else {
             braid_load<NT>(dst, fvb, fpad, gf, lane);
             u = braid_proc(u, cur, eng, dp, gp, lane, s_h);
