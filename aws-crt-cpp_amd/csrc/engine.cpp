@@ -325,7 +325,10 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 #endif
 constexpr uint64_t kSmallBatchBytes = AMDCRC_SMALL_BATCH;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
-constexpr uint64_t kLaneMaxBytes = 4096;
+#ifndef AMDCRC_LANE_LIST_MAX  // compile-time only (launch-shape sweeps build a variant; no run-time switch)
+#define AMDCRC_LANE_LIST_MAX 4096
+#endif
+constexpr uint64_t kLaneMaxBytes = AMDCRC_LANE_LIST_MAX;
 // Strided CRC64NVME launches of short buffers take the lane-per-buffer scan once they hold enough
 // buffers for a wave per SIMD.  1 GiB steps, lanes vs the streaming scan with the byte-Horner tile
 // finish (profiles/r02/lane64_r2/): 3749 vs 1262 GiB/s at 2 KiB, 3754 vs 2933 at 4 KiB, 3738 vs 4259

@@ -64,6 +64,16 @@ def main():
     for k in ("strided_4096x64KiB", "list_4096x64KiB_aligned"):
         res[k + "_gibs"] = round(total / (res[k] * 1e-6) / 2**30, 1)
     res["list_4096_ragged_32-96KiB_unaligned_gibs"] = round(sum(lens2) / (res["list_4096_ragged_32-96KiB_unaligned"] * 1e-6) / 2**30, 1)
+    # short ragged lists (the lane-per-buffer scan's domain): 65536 buffers of 1..4 KiB and of 256 B..1 KiB
+    for name, lo, hi in (("short_1-4KiB", 1024, 4096), ("short_256B-1KiB", 256, 1024)):
+        ls = [rnd.randrange(lo, hi + 1) for _ in range(65536)]
+        ps, a = [], base
+        for ln in ls:
+            ps.append(a)
+            a += ln
+        o2 = torch.empty(len(ls), dtype=torch.int32, device="cuda")
+        res[name] = timed(lambda: eng.checksum_list(alg, ps, ls, out=o2))
+        res[name + "_gibs"] = round(sum(ls) / (res[name] * 1e-6) / 2**30, 1)
     print(json.dumps(res))
 
 
