@@ -1,5 +1,7 @@
-"""CPU: a Python model of the W=32 braided scan (crc_kernels.hip crc32_braid_kernel), checked
-against the oracle.  It restates the kernel's algebra independently of the C++ host code:
+"""CPU: Python models of the W=32 braided scans (crc_kernels.hip crc32_braid_kernel /
+crc32_stream_kernel), checked against the oracle.  The first model is the 4-byte-word form
+(AMDCRC_STREAM_W8=0 builds); BraidW8 below models the default 8-byte-word form, whole tiles and
+front-padded ones.  They restate the kernels' algebra independently of the C++ host code:
 
   * rows of 256 bytes; lane l owns the 4-byte word at 4l of every row;
   * braid step u <- T'(u ^ w) with T'_k[e] = e * x^(8(k+1)) * x^(8*252) (slice-by-4 plus the skip
@@ -254,3 +256,81 @@ def test_braid_w8_model_vs_oracle(alg, rows):
                 r ^= mulmod(u, br.K[lane], P)
             fin ^= mulmod(r, xpow8n(tile * (ntiles - 1 - k), P), P)
         assert (~fin & M32) == oracle.crc(alg, data, seed), (alg, rows, ntiles)
+
+
+def braid_w8_model(br: BraidW8, data: bytes, addr: int, seed: int, rows: int) -> int:
+    """crc32_braid_kernel<POLY, LIST, NT, true> on one buffer: head bytes folded bytewise, the
+    16-aligned main region front-padded to tiles of `rows` 512-byte rows, words in the pad zero, the
+    head state XORed into the low half of the word at the pad's end, groups of 8 rows before the
+    pad's end skipped (the braids are zero there), tiles combined as the W=32 model does."""
+    P = br.P
+    T0 = [table_entry(e, 0, P) for e in range(256)]
+
+    def bytes_(s, bs):
+        for b in bs:
+            s = (s >> 8) ^ T0[(s ^ b) & 255]
+        return s
+
+    n = len(data)
+    ptr, end = addr, addr + n
+    H, Ea = (ptr + 15) & ~15, end & ~15
+    if Ea > H:
+        mainlen, headend, tail = Ea - H, H, Ea
+    else:
+        mainlen, headend, tail = 0, end, end
+    tile = ROW8 * rows
+    T = -(-mainlen // tile) if mainlen else 1
+    pad = T * tile - mainlen
+    s_h = bytes_(~seed & M32, data[: headend - ptr])
+    groups = {}
+    fin = None
+    for k in range(T):
+        r = 0
+        if mainlen:
+            vbase = (H - ptr) - pad + k * tile
+            first_row = (pad // 4096) * 8 if k == 0 else 0  # the kernel's first_group, in rows
+            for lane in range(64):
+                u = s_h if (k == 0 and pad == 0 and lane == 0) else 0
+                for c in range(first_row, rows):
+                    vo = ROW8 * c + 8 * lane
+                    if k == 0 and pad and vo < pad:
+                        w = 0
+                    else:
+                        w = int.from_bytes(data[vbase + vo: vbase + vo + 8], "little")
+                    if k == 0 and pad and vo == pad:
+                        w ^= s_h
+                    u = br.step(u ^ (w & M32), w >> 32)
+                r ^= mulmod(u, br.K[lane], P)
+        if T == 1:
+            fin = r if mainlen else s_h
+        else:
+            g0 = k & ~31
+            gend = min(g0 + 32, T)
+            groups[g0] = groups.get(g0, 0) ^ mulmod(r, xpow8n(tile * (gend - 1 - k), P), P)
+    if T > 1:
+        fin = 0
+        for g0, v in groups.items():
+            gend = min(g0 + 32, T)
+            fin ^= mulmod(v, xpow8n(tile * (T - gend), P), P)
+    fin = bytes_(fin, data[tail - ptr:])
+    return ~fin & M32
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
+@pytest.mark.parametrize("rows", [8, 16])
+def test_braid_w8_padded_model_vs_oracle(alg, rows):
+    """front pads ending before, on and after 4 KiB group boundaries (rows = 16: two groups per tile),
+    unaligned heads and tails, seeds, multi-tile buffers"""
+    br = BraidW8(alg)
+    rnd = random.Random(hash((alg, rows, "w8pad")) & 0xFFFF)
+    tile = ROW8 * rows
+    sizes = [0, 5, 16, 17, 512, tile - 16, tile, tile + 16, tile - 4096, tile - 4096 - 16, tile - 4096 + 16,
+             2 * tile - 4096, 3 * tile + 7]
+    for n in sizes:
+        if n < 0:
+            continue
+        for misalign in (0, 3, 9):
+            data = bytes(rnd.getrandbits(8) for _ in range(n))
+            seed = rnd.choice([0, rnd.getrandbits(32)])
+            assert braid_w8_model(br, data, 0x1000 + misalign, seed, rows) == oracle.crc(alg, data, seed), \
+                (alg, rows, n, misalign)
