@@ -28,9 +28,10 @@ def timed(fn, reps=12):
     return statistics.median(out)
 
 
-def main():
+def main(alg_name="crc32c"):
     eng.init()
-    alg = eng.CRC32C
+    alg = {"crc32": eng.CRC32, "crc32c": eng.CRC32C, "crc64nvme": eng.CRC64NVME}[alg_name]
+    odt = torch.int64 if alg_name == "crc64nvme" else torch.int32
     total = 256 << 20
     data = torch.randint(0, 256, (2 * total + 4096,), dtype=torch.uint8, device="cuda")
     base = data.data_ptr()
@@ -38,7 +39,7 @@ def main():
     res = {}
     L = 65536
     n = total // L
-    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n, dtype=odt, device="cuda")
     res["strided_4096x64KiB"] = timed(lambda: eng.checksum_strided(alg, data, L, L, n, out=out))
     ptrs, lens = [base + i * L for i in range(n)], [L] * n
     res["list_4096x64KiB_aligned"] = timed(lambda: eng.checksum_list(alg, ptrs, lens, out=out))
@@ -71,11 +72,11 @@ def main():
         for ln in ls:
             ps.append(a)
             a += ln
-        o2 = torch.empty(len(ls), dtype=torch.int32, device="cuda")
+        o2 = torch.empty(len(ls), dtype=odt, device="cuda")
         res[name] = timed(lambda: eng.checksum_list(alg, ps, ls, out=o2))
         res[name + "_gibs"] = round(sum(ls) / (res[name] * 1e-6) / 2**30, 1)
     print(json.dumps(res))
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:])

@@ -9,8 +9,11 @@ tail -1 $O/pytest.log && grep -q " passed" $O/pytest.log && ! grep -q "failed" $
 for r in 1 2; do
   for v in A B; do
     cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so || exit 1
-    bash scripts/gpu_step.sh 120 $O/${v}_$r.log python -u aws-crt-cpp_amd/tools/list_probe.py || exit 1
+    bash scripts/gpu_step.sh 120 $O/${v}_$r.log python -u aws-crt-cpp_amd/tools/list_probe.py ${PROBE_ARGS:-} || exit 1
     echo "$v $r $(grep '^{' $O/${v}_$r.log)"
   done
 done
 cp ab/libB.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so
+if [ -n "${BENCH_AB:-}" ]; then
+  TAG=${TAG:-lists}/bench REPS=2 bash scripts/ab_lib.sh python -u bench.py $BENCH_AB
+fi
