@@ -5,11 +5,14 @@
 // buffers.  Design notes: DESIGN.md "Kernels".  In short:
 //
 //  * Braided scans.  A buffer's 16-aligned main region is cut into tiles; a wavefront scans a tile
-//    row by row, lane l owning word l of every row (one fully coalesced wave load per row).  Each
-//    lane's state is one "braid" of the CRC: u <- (u ^ w) * x^(8*row), one slice-by-4 (W=32) or
-//    slice-by-8 (W=64) step whose byte tables fold in the skip over the other 63 lanes' words.
-//  * Byte tables live in LDS in 8 copies, quarter-rotated so that every ds_read of a half-wave
-//    touches distinct banks whatever bytes it indexes (76 KiB for W=32, 130 KiB for W=64).
+//    row by row, lane l owning the 8-byte word l of every 512-byte row (one fully coalesced
+//    global_load_dwordx2 per row).  Each lane's state is one "braid" of the CRC:
+//    u <- (u ^ w) * x^(8*512), one slice-by-8 step whose byte tables fold in the skip over the other
+//    63 lanes' words (for W=32 the word's high half does not meet u: its lookups run a row ahead).
+//    4-byte words / 256-byte rows remain as the AMDCRC_STREAM_W8=0 build.
+//  * Byte tables live in LDS in several copies laid out so that every ds_read of a half-wave
+//    touches distinct banks whatever bytes it indexes (W=32: 8 copies, 64 KiB + constants; W=64
+//    streaming scan: 4 copies, 64 KiB + nibble tables; W=64 braided scan: 8 copies, 128 KiB).
 //  * A lane's state times x^(-w*l) is its share of the tile register (K_l); the wave XOR-reduces
 //    the shares, moves the tile register to its 32-tile group's end and then to the buffer end with
 //    column tables, and device-scope atomics combine the tiles of a buffer; the last arrival
