@@ -250,7 +250,8 @@ def test_list_front_pads_at_group_boundaries(engine, alg):
     """Braided list scans start a buffer's first tile at the 4 KiB group holding its front pad's end
     (DESIGN.md §3.3).  A 64 MiB list of 16 KiB buffers sets 16 KiB tiles (four groups); buffers of
     T tiles minus pads of 4096 k + {0, 16, 4080} bytes (k < 4) put the pad's end on, just past and
-    just before every group boundary, at aligned and unaligned starts, with seeds."""
+    just before every group boundary, at aligned and unaligned starts, with seeds.  Starts 9..15
+    bytes past 16-byte alignment put the head's last bytes next to a group boundary."""
     import torch
 
     rng = random.Random(0x9AD + ALG[alg])
@@ -260,7 +261,7 @@ def test_list_front_pads_at_group_boundaries(engine, alg):
     rng.shuffle(lens)
     offs, pos = [], 0
     for ln in lens:
-        pos = (pos + 15) // 16 * 16 + rng.choice([0, 0, 3, 9])
+        pos = (pos + 15) // 16 * 16 + rng.choice([0, 0, 3, 9, 13, 15])
         offs.append(pos)
         pos += ln
     d = dev_random(pos + 64, 0x9AD)
