@@ -65,3 +65,8 @@ def _no_silent_cpu_fallback(request):
     before = aws_crt_amd.fallback_count()
     yield
     assert aws_crt_amd.fallback_count() == before, "a GPU call fell back to the host path"
+
+
+def pytest_collection_modifyitems(config, items):
+    """The bench-contract test (a subprocess run of bench.py) goes last, after every parity test."""
+    items.sort(key=lambda it: it.nodeid.startswith("tests/test_bench_contract.py"))
