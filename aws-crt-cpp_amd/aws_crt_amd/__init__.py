@@ -198,6 +198,10 @@ class BatchSet:
 
     def __init__(self, alg: int, batches, stride: int, length: int, count: int):
         self.n = len(batches)
+        # the tensors behind the raw addresses stay referenced as long as the prepared submission: a
+        # temporary freed (and reused by the caching allocator) under a queued launch would be read or
+        # written by it
+        self._keep = [t for b in batches for t in b if hasattr(t, "data_ptr")]
         self.arr = (_Batch * max(self.n, 1))()
         for i, (base, seeds, out) in enumerate(batches):
             self.arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
@@ -213,6 +217,12 @@ class BatchSet:
         rc = self.fn(*self.args, _stream_handle(stream))
         if rc != 0:
             _check(rc)
+        if stream is not None and hasattr(stream, "cuda_stream"):
+            # a launch on a side stream: the caching allocator must not hand these blocks out again
+            # before that stream has finished with them
+            for t in self._keep:
+                if getattr(t, "is_cuda", False):
+                    t.record_stream(stream)
 
 
 def checksum_batches(alg: int, batches, stride: int, length: int, count: int, stream=None) -> None:

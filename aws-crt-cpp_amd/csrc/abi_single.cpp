@@ -134,9 +134,13 @@ bool checksum_one(int alg, const void *input, size_t len, uint64_t seed, uint64_
 uint64_t crc_value(int alg, const uint8_t *input, size_t len, uint64_t previous) {
     if (!len) return previous;
     uint64_t r[2];
-    // device memory the GPU cannot read back either: no error channel (CRC.h:20-36 is value-only);
-    // the diagnostic above is the report and the seed is returned unchanged
-    return checksum_one(alg, input, len, previous, r) ? r[0] : previous;
+    if (checksum_one(alg, input, len, previous, r)) return r[0];
+    // Device memory that neither the GPU nor a read-back can reach.  CRC.h:20-36 is value-only, so
+    // the failure goes to the thread's aws error (Aws::Crt::LastError(), ref source/Api.cpp:469-472):
+    // a caller that resets the error before the call and checks it after can tell this value apart
+    // from a real CRC.  The value returned is the seed, unchanged.
+    aws_raise_error(AWS_ERROR_UNSUPPORTED_OPERATION);
+    return previous;
 }
 
 // ---- xxhash ABI
@@ -183,6 +187,8 @@ AWS_CRT_AMD_API int aws_crt_amd_set_dispatch(int m) {
 }
 AWS_CRT_AMD_API int aws_crt_amd_get_dispatch(void) { return mode(); }
 AWS_CRT_AMD_API unsigned long long aws_crt_amd_fallback_count(void) { return g_fallbacks.load(); }
+// internal (ingest.cpp): a host job whose devices failed was served by the host path
+void amdcrc_note_fallback(void) { g_fallbacks.fetch_add(1, std::memory_order_relaxed); }
 
 AWS_CRT_AMD_API int aws_crt_amd_cpu_batch(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
                                           const uint64_t *seeds, uint64_t *out, int threads) {

@@ -339,10 +339,12 @@ struct Braid32 {
     using T = uint32_t;
     static constexpr int W = 32;
     const char *L;
+    const char *C;  // the constants region (K image, P columns, byte table, flags, local slots)
     uint32_t cst[4], sel[4];  // per lane and table slot k: quarter<<5 | copy<<2, and the v_perm selector
 
     __device__ void init(const char *lds, int lane) {
         L = lds;
+        C = lds + kBKOff;
         const uint32_t j = ((uint32_t)lane >> 3) & 3u, cp = (uint32_t)lane & 7u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -372,16 +374,16 @@ struct Braid32 {
     }
     // plain byte step for head / tail bytes (s is wave-uniform: broadcast reads)
     __device__ __forceinline__ uint32_t byte(uint32_t s, uint32_t b) const {
-        return (s >> 8) ^ lds32(L, kT0Off + 4 * ((s ^ b) & 0xffu));
+        return (s >> 8) ^ lds32(C, (kT0Off - kBKOff) + 4 * ((s ^ b) & 0xffu));
     }
-    // the constants region (K image, P columns, byte table, flags, local slots) at kBKOff
-    __device__ __forceinline__ const char *cbase() const { return L + kBKOff; }
+    // the constants region: after the tables (kBKOff for the 4- and 8-byte-word tables)
+    __device__ __forceinline__ const char *cbase() const { return C; }
     // r * K_lane : 32 LDS matrix columns
     __device__ __forceinline__ uint32_t mulK(uint32_t r, int lane) const {
         uint32_t acc = 0;
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint4 c = *(const uint4 *)(L + kBKOff + (g * 64 + lane) * 16);
+            const uint4 c = *(const uint4 *)(C + (g * 64 + lane) * 16);
             acc = xor_and(acc, c.x, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 0), 1));
             acc = xor_and(acc, c.y, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 1), 1));
             acc = xor_and(acc, c.z, (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - (4 * g + 2), 1));
@@ -447,6 +449,7 @@ struct Braid32W8 : Braid32<POLY> {
     uint32_t cst8[8], sel8[8];
     __device__ void init(const char *lds, int lane) {
         this->L = lds;
+        this->C = lds + kBKOff;
         const uint32_t j = ((uint32_t)lane >> 3) & 3u, c = (uint32_t)lane & 7u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -477,6 +480,104 @@ struct Braid32W8 : Braid32<POLY> {
 
 struct W8Group {
     uint64_t w[kW8RowsPerGroup];
+};
+
+// ---- the W=32 streaming scan on 16-byte words (crc32_stream_kernel<POLY, 16>, large launches).  A row
+// is 1024 bytes, lane l owning the 16-byte word at 16l (one global_load_dwordx4 per lane per row: half
+// the load instructions and half the row steps of 8-byte words for the same bytes).  The row step is
+// slice-by-16 on a = (u ^ d0, d1, d2, d3): u' = XOR_i T'_(15-i)[byte i of a] with
+// T'_t[e] = e * x^(8(t+1)) * x^(8*1008), so only d0's four lookups sit on the braid's dependency
+// chain; d1..d3's twelve are looked up one row ahead.  Lane l's share is u * x^(-128 l).
+// LDS: two regions shaped like the 8-byte-word tables, A = T'_15..T'_8 (bytes 0..7) at 0 and
+// B = T'_7..T'_0 (bytes 8..15) at 64 KiB; table t at (t & 7) * 32 of entry e's 256-byte row, 8 copies
+// of 4 bytes.  In slot k a lane reads byte q = (k + j) & 3 of dword d (table 15 - 4d - q), copy
+// lane & 7, j = (lane >> 3) & 3: bank 8 (3 - q) + copy, so every ds_read_b32 half-wave meets 32
+// distinct banks (tests/test_braid_model.py::test_w16_lds_schedule_conflict_free_and_complete).  The
+// 128 KiB of tables take one 1024-thread workgroup (16 waves) per CU.
+constexpr uint32_t kW16Row = 1024;
+constexpr int kW16RowsPerGroup = 4;  // 4 KiB per wave per ring slot, as the other widths
+constexpr uint32_t kW16TabBytes = 131072;
+constexpr int kW16Block = 1024;
+static_assert(kW16Row * kW16RowsPerGroup == kBraidRow * kBraidRowsPerGroup, "ring slot size");
+
+template <uint32_t POLY>
+struct BraidW16Basis {
+    uint32_t b[17][8];  // b[t][i] = T'_t[1 << i] (t < 16); b[16][i] = T_0[1 << i]
+    constexpr BraidW16Basis() : b() {
+        const uint64_t skip = gf2_xpow8n(kW16Row - 16, POLY, 32);
+        for (int i = 0; i < 8; ++i) {
+            for (int t = 0; t < 16; ++t) b[t][i] = (uint32_t)gf2_mulmod(gf2_table_entry(1u << i, t, POLY), skip, POLY, 32);
+            b[16][i] = (uint32_t)gf2_table_entry(1u << i, 0, POLY);
+        }
+    }
+};
+template <uint32_t POLY, int K>
+__device__ __forceinline__ uint32_t basis_w16(uint32_t e) {
+    constexpr BraidW16Basis<POLY> B{};
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0u;
+    return v;
+}
+template <uint32_t POLY, int K = 0>
+__device__ __forceinline__ uint32_t basis_w16_rt(uint32_t t, uint32_t e) {  // t wave-uniform
+    if constexpr (K < 15) {
+        if (t == K) return basis_w16<POLY, K>(e);
+        return basis_w16_rt<POLY, K + 1>(t, e);
+    } else {
+        return basis_w16<POLY, 15>(e);
+    }
+}
+
+template <uint32_t POLY>
+struct Braid32W16 : Braid32<POLY> {
+    uint32_t cst16[4][4];  // [dword d][slot k]: region B << 16 | (t & 7) << 5 | copy << 2, t = 15 - 4d - q
+    uint32_t sel16[4];     // [slot k]: byte0 <- cst, byte1 <- byte q of the dword, byte2 <- cst (region)
+    __device__ void init(const char *lds, int lane) {
+        this->L = lds;
+        this->C = lds + kW16TabBytes;
+        const uint32_t j = ((uint32_t)lane >> 3) & 3u, c = (uint32_t)lane & 7u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = (k + j) & 3u;
+            sel16[k] = 0x0c060004u | (q << 8);
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t t = 15u - 4u * d - q;
+                cst16[d][k] = (t < 8 ? 0x10000u : 0u) | ((t & 7u) << 5) | (c << 2);
+            }
+        }
+    }
+    __device__ __forceinline__ uint32_t look(int d, int k, uint32_t v) const {
+        return lds32(this->L, __builtin_amdgcn_perm(cst16[d][k], v, sel16[k]));
+    }
+    // d1..d3's twelve lookups of a row (independent of u), XORed in at the next row's chain step
+    struct Hi {
+        uint32_t v[12];
+    };
+    __device__ __forceinline__ Hi look_hi(const v4u &w) const {
+        Hi h;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            h.v[k] = look(1, k, w.y);
+            h.v[4 + k] = look(2, k, w.z);
+            h.v[8 + k] = look(3, k, w.w);
+        }
+        return h;
+    }
+    // the chain step: x = u ^ d0 of a row whose other lookups are h; returns the row's u' ^ wn
+    __device__ __forceinline__ uint32_t look_lo(uint32_t x, const Hi &h, uint32_t wn) const {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = look(0, k, x);
+        const uint32_t o = xor3(xor3(xor3(h.v[0], h.v[1], h.v[2]), xor3(h.v[3], h.v[4], h.v[5]), xor3(h.v[6], h.v[7], h.v[8])),
+                                xor3(h.v[9], h.v[10], h.v[11]), wn);
+        return xor3(xor3(o, v[0], v[1]), v[2], v[3]);
+    }
+};
+
+struct W16Group {
+    v4u w[kW16RowsPerGroup];
 };
 
 // one payload word; NT: non-temporal (streamed once, not kept in the caches)
@@ -1003,6 +1104,48 @@ __device__ __forceinline__ uint32_t stream_rows(uint32_t x, W8Group &cur, W8Grou
     return stream_rows_w8<0, B>(x, typename B::Hi{}, cur, nxt, voff, snext, eng);
 }
 
+// 16-byte rows: the same walk as stream_rows_w8 (x = u ^ d0(w_r); d1..d3 of row r looked up with
+// row r - 1's chain step)
+template <int R>
+__device__ __forceinline__ v4u gld_w16(uint32_t voff, uint64_t sbase) {
+    return __builtin_nontemporal_load((gv4u *)(sbase + voff + R * kW16Row));
+}
+template <int R, class B>
+__device__ __forceinline__ uint32_t stream_rows_w16(uint32_t x, const typename B::Hi &h, W16Group &cur, W16Group &nxt,
+                                                    uint32_t voff, uint64_t snext, const B &eng) {
+    if constexpr (R < kW16RowsPerGroup) {
+        nxt.w[R] = gld_w16<R>(voff, snext);
+        if constexpr (R == 0)
+            x ^= cur.w[0].x;
+        else
+            x = eng.look_lo(x, h, cur.w[R].x);
+        const typename B::Hi hn = eng.look_hi(cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return stream_rows_w16<R + 1, B>(x, hn, cur, nxt, voff, snext, eng);
+    } else {
+        return eng.look_lo(x, h, 0u);
+    }
+}
+template <int R, class B>
+__device__ __forceinline__ uint32_t stream_rows(uint32_t x, W16Group &cur, W16Group &nxt, uint32_t voff, uint64_t snext,
+                                                const B &eng) {
+    static_assert(R == 0, "the 16-byte row walk starts at row 0");
+    return stream_rows_w16<0, B>(x, typename B::Hi{}, cur, nxt, voff, snext, eng);
+}
+template <int R>
+__device__ __forceinline__ void stream_issue(W16Group &g, uint32_t voff, uint64_t s) {
+    if constexpr (R < kW16RowsPerGroup) {
+        g.w[R] = gld_w16<R>(voff, s);
+        stream_issue<R + 1>(g, voff, s);
+    }
+}
+#define AMDCRC_R4V(g) "+v"(g.w[0]), "+v"(g.w[1]), "+v"(g.w[2]), "+v"(g.w[3])
+__device__ __forceinline__ void ring_drain(W16Group &a, W16Group &b, W16Group &c) {
+    asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R4V(a)::"memory");
+    asm volatile("" : AMDCRC_R4V(b));
+    asm volatile("" : AMDCRC_R4V(c));
+}
+
 template <int R>
 __device__ __forceinline__ void stream_issue(W8Group &g, uint32_t voff, uint64_t s) {
     if constexpr (R < kW8RowsPerGroup) {
@@ -1026,7 +1169,7 @@ __device__ __forceinline__ void ring_drain(W8Group &a, W8Group &b, W8Group &c) {
 #define AMDCRC_R16(g) "+v"(g.w[0]), "+v"(g.w[1]), "+v"(g.w[2]), "+v"(g.w[3]), "+v"(g.w[4]), "+v"(g.w[5]), "+v"(g.w[6]), \
     "+v"(g.w[7]), "+v"(g.w[8]), "+v"(g.w[9]), "+v"(g.w[10]), "+v"(g.w[11]), "+v"(g.w[12]), "+v"(g.w[13]),          \
     "+v"(g.w[14]), "+v"(g.w[15])
-__device__ __forceinline__ void ring_drain(BGroup &a, BGroup &b, BGroup &c) {
+[[maybe_unused]] __device__ __forceinline__ void ring_drain(BGroup &a, BGroup &b, BGroup &c) {
     asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R16(a)::"memory");
     asm volatile("" : AMDCRC_R16(b));
     asm volatile("" : AMDCRC_R16(c));
@@ -1153,23 +1296,38 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
 }
 
 // Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
-template <uint32_t POLY, bool W8>
-__global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const ScanParams p) {
-    using B = typename std::conditional<W8, Braid32W8<POLY>, Braid32<POLY>>::type;
-    using Grp = typename std::conditional<W8, W8Group, BGroup>::type;
-    __shared__ __attribute__((aligned(16))) char lds[kStreamLds];
+// WB = bytes per lane word: 8 (512-thread workgroups, 64 KiB of tables, two per CU) or 16 (one
+// 1024-thread workgroup per CU, 128 KiB of tables); 4 remains as the AMDCRC_STREAM_W8=0 build.
+template <int WB>
+struct StreamShape {
+    static constexpr int kBlock = WB == 16 ? kW16Block : kBraidBlock;
+    static constexpr int kWaves = kBlock / kWave;
+    static constexpr uint32_t kTab = WB == 16 ? kW16TabBytes : kBTabBytes;  // the constants region follows
+    static constexpr uint32_t kLds = kTab + (kStreamLds - kBKOff);
+    static constexpr int kKWord = WB == 16 ? kBraidK128Word : WB == 8 ? kBraidK64Word : 0;
+};
+
+template <uint32_t POLY, int WB>
+__global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kernel(const ScanParams p) {
+    using SS = StreamShape<WB>;
+    using B = typename std::conditional<WB == 16, Braid32W16<POLY>,
+                                        typename std::conditional<WB == 8, Braid32W8<POLY>, Braid32<POLY>>::type>::type;
+    using Grp = typename std::conditional<WB == 16, W16Group, typename std::conditional<WB == 8, W8Group, BGroup>::type>::type;
+    constexpr int WAVES = SS::kWaves;
+    __shared__ __attribute__((aligned(16))) char lds[SS::kLds];
+    char *const cb = lds + SS::kTab;  // constants region (K image, P columns, byte table, flag, local slots)
 
     const int lane = threadIdx.x & 63;
     const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
-    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + wv);
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + wv);
     const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
     const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
     // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
     const uint32_t G = p.seg / kGroupBytes;
     const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
-    const uint32_t voff = (W8 ? 8u : 4u) * (uint32_t)lane;
+    const uint32_t voff = (uint32_t)WB * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
     const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
     const uint32_t gsh = __builtin_ctz(G);
@@ -1205,12 +1363,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
             }
         }
     };
-    // K-image word and P columns of this thread, published to LDS after the first scan step (ordinary
+    // K-image words and P columns of this thread, published to LDS after the first scan step (ordinary
     // loads: issued before the first group, so the compiler's wait for them in the peeled first step
-    // is the exact count of the row loads issued after them)
+    // is the exact count of the row loads issued after them).  The K image is 8 KiB (512 x 16 B) and
+    // the P columns 4 KiB (1024 words) whatever the workgroup size.
     const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + (W8 ? kBraidK64Word : 0) + 4 * threadIdx.x);
-    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + kBraidBlock);
+    const uint32_t kti = (uint32_t)threadIdx.x & 511u;
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + SS::kKWord + 4 * kti);
+    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x);
+    const uint32_t pce1 = SS::kBlock < 1024 ? *(gu32 *)(pcs + threadIdx.x + SS::kBlock) : 0u;
     // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
     LocalBufs lb{0, 0};
     if (T > 1 && T <= 32) {
@@ -1222,7 +1383,20 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
         stream_issue<0>(ra, voff, f_addr());
         f_next();
     }
-    if constexpr (W8) {
+    if constexpr (WB == 16) {
+        // wave t builds table T'_t (t wave-uniform): entries lane + 64 n, 8 copies (two 16-byte stores)
+        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        char *region = lds + (t < 8 ? 65536u : 0u) + ((t & 7u) << 5);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint32_t e = (uint32_t)lane + 64u * n;
+            const uint32_t te = basis_w16_rt<POLY>(t, e);
+            char *row = region + (e << 8);
+            *(uint4 *)row = make_uint4(te, te, te, te);
+            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
+        }
+        if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w16<POLY, 16>(threadIdx.x);
+    } else if constexpr (WB == 8) {
         // wave t builds table T'_t (t wave-uniform): entries lane + 64 n, 8 copies (two 16-byte stores)
         const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
@@ -1233,7 +1407,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
             *(uint4 *)row = make_uint4(te, te, te, te);
             *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
         }
-        if (threadIdx.x < 256) *(uint32_t *)(lds + kT0Off + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
+        if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
     } else {
         const uint32_t i = threadIdx.x;
         const uint32_t q = (i >> 1) & 3u, h = i & 1u;
@@ -1248,10 +1422,10 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
             for (int b = 0; b < 8; ++b) te ^= ((e >> b) & 1u) ? bq[b] : 0u;
             *(uint4 *)(lds + (e << 8) + (q << 5) + (h << 4)) = make_uint4(te, te, te, te);
         }
-        if (i < 256) *(uint32_t *)(lds + kT0Off + 4 * i) = basis_entry<POLY, 4>(i);
+        if (i < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * i) = basis_entry<POLY, 4>(i);
     }
-    if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
-    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(lds + kLocalOff))[threadIdx.x] = 0ull;
+    if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
+    if (threadIdx.x < kLocalSlots) ((unsigned long long *)(cb + (kLocalOff - kBKOff)))[threadIdx.x] = 0ull;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
@@ -1263,16 +1437,16 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_stream_kernel(const Scan
     // every wave publishes its share of the K image and P columns once and counts itself in LDS; a
     // wave spins on the count only before its first tile finish
     auto publish_consts = [&]() {
-        *(v4u *)(lds + kBKOff + 16 * threadIdx.x) = kq;
-        *(uint32_t *)(lds + kPcolOff + 4 * threadIdx.x) = pce0;
-        *(uint32_t *)(lds + kPcolOff + 4 * (threadIdx.x + kBraidBlock)) = pce1;
+        if (threadIdx.x < 512) *(v4u *)(cb + 16 * threadIdx.x) = kq;
+        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * threadIdx.x) = pce0;
+        if (SS::kBlock < 1024) *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * (threadIdx.x + SS::kBlock)) = pce1;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(lds + kConstFlagOff), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(cb + (kConstFlagOff - kBKOff)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     auto await_consts = [&]() {
         if (consts_ready) return;
-        while (__hip_atomic_load((uint32_t *)(lds + kConstFlagOff), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-               (uint32_t)kBraidWaves)
+        while (__hip_atomic_load((uint32_t *)(cb + (kConstFlagOff - kBKOff)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+               (uint32_t)WAVES)
             __builtin_amdgcn_s_sleep(1);
         consts_ready = true;
     };
@@ -2452,16 +2626,20 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     const bool list = p->list_mode != 0;
     switch (alg) {
         case ALG_CRC32:
-            if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8>, nblocks, kBraidBlock, s, p, ev);
+            if (p->stream == 2 && !list)
+                launch(crc32_stream_kernel<kPoly32, 16>, nblocks, kW16Block, s, p, ev);
+            else if (p->stream && !list)
+                launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
-            if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8>, nblocks, kBraidBlock, s, p, ev);
+            if (p->stream == 2 && !list)
+                launch(crc32_stream_kernel<kPoly32C, 16>, nblocks, kW16Block, s, p, ev);
+            else if (p->stream && !list)
+                launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
             else

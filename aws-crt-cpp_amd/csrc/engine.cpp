@@ -98,6 +98,9 @@ struct Device {
     std::map<hipStream_t, DevBuf> xsums;  // split XXH3 long path: per-block accumulator sums
     std::map<hipStream_t, Stage> stage;
     std::map<hipStream_t, DevBuf> mp_out;  // multipart part results
+    // held by a multipart call on that stream from its list launch until its results are on the host:
+    // two calls on one stream would otherwise queue launch A, launch B, then A's copy of B's results
+    std::map<hipStream_t, std::unique_ptr<std::mutex>> mp_mu;
     // single path (GPU-dispatched host buffers, device buffers through the aws-checksums ABI)
     hipStream_t own_stream = nullptr;
     void *pin[2] = {nullptr, nullptr};
@@ -190,14 +193,18 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
         for (int i = 0; i < 1024; ++i)
             c[2048 + i] = (uint32_t)gf2_mulmod(gf2_table_entry(i & 255, i >> 8, poly), skip, poly, 32);
         for (int e = 0; e < 256; ++e) c[3072 + e] = (uint32_t)gf2_table_entry(e, 0, poly);
-        kl = 0x80000000u;  // the streaming scan's lanes own 8-byte words: K_l = x^(-64 l)
-        for (int l = 0; l < 64; ++l) {
-            uint32_t col = kl;
-            for (int j = 0; j < 32; ++j) {
-                c[kBraidK64Word + ((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
-                col = (uint32_t)gf2_mulx(col, poly);
+        // the streaming scan's lanes own 8-byte words (K_l = x^(-64 l)) or 16-byte words (x^(-128 l))
+        for (const int wbits : {64, 128}) {
+            const int base = wbits == 64 ? kBraidK64Word : kBraidK128Word;
+            kl = 0x80000000u;
+            for (int l = 0; l < 64; ++l) {
+                uint32_t col = kl;
+                for (int j = 0; j < 32; ++j) {
+                    c[base + ((j >> 2) * 64 + l) * 4 + (j & 3)] = col;
+                    col = (uint32_t)gf2_mulx(col, poly);
+                }
+                for (int i = 0; i < wbits; ++i) kl = inv_mulx32(kl, poly);
             }
-            for (int i = 0; i < 64; ++i) kl = inv_mulx32(kl, poly);
         }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
@@ -324,6 +331,12 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 #define AMDCRC_SMALL_BATCH (256ull << 20)
 #endif
 constexpr uint64_t kSmallBatchBytes = AMDCRC_SMALL_BATCH;
+// W=32 streaming scans of at least kSmallBatchBytes: the 16-byte-word kernel (crc_kernels.hip
+// Braid32W16); 0 keeps the 8-byte-word kernel there too
+#ifndef AMDCRC_STREAM_W16  // compile-time only (A/B builds)
+#define AMDCRC_STREAM_W16 1
+#endif
+constexpr bool kStreamW16 = AMDCRC_STREAM_W16 != 0;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 #ifndef AMDCRC_LANE_LIST_MAX  // compile-time only (launch-shape sweeps build a variant; no run-time switch)
 #define AMDCRC_LANE_LIST_MAX 4096
@@ -345,7 +358,12 @@ constexpr uint64_t kXxh3SplitBlocks = 4096;
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
-ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main, bool w64_half_blocks = false) {
+ScanGeometry scan_geometry(const Device *d, int alg, uint64_t ntiles, uint64_t total_main, bool w64_half_blocks = false,
+                           bool w16 = false) {
+    if (w16) {  // crc32_stream_kernel<POLY, 16>: one 1024-thread workgroup per CU
+        const uint64_t blocks = std::min<uint64_t>((ntiles + 15) / 16, (uint64_t)d->cus);
+        return {blocks, 16};
+    }
     const uint64_t wpb = width_of(alg) == 32 ? 8 : w64_half_blocks ? (uint64_t)kW64StreamBlock / kWave : (uint64_t)kWavesPerBlock;
     const uint64_t per_cu = w64_half_blocks ? 1024 / kW64StreamBlock : width_of(alg) == 32 && total_main >= kSmallBatchBytes ? 2 : 1;
     const uint64_t cap = (uint64_t)d->cus * per_cu;
@@ -383,7 +401,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_claim = w->claim;
     }
     const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
-    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half).blocks;
+    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
@@ -503,6 +521,9 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     p.ntiles = T * count;
     p.seed_all = seed_all;
     p.stream = stream && ml % tile == 0 ? 1u : 0u;
+    // large W=32 launches: 16-byte lane words in one 1024-thread workgroup per CU (the same waves per
+    // CU as two 512-thread workgroups; the tiles hold 4 KiB groups either way)
+    if (p.stream && w32 && kStreamW16 && !small) p.stream = 2;
     if (pool && !p.stream) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
         const ScanGeometry geo = scan_geometry(d, alg, p.ntiles, ml * count);
@@ -688,24 +709,37 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
         return 0;
     }
     if (is_hash(alg)) {
-        // xxHash is not chunkable by seed: a host buffer is copied whole into a cached device buffer
+        // xxHash is not chunkable by seed: a host buffer is copied whole into device memory.  Up to
+        // one staging chunk the copy goes into a cached buffer; a larger one into a buffer of its own
+        // that is freed once the call has synchronised, so a large hash never stays pinned in HBM.
         const void *dp = input;
+        void *temp = nullptr;
         if (len && !is_device_ptr(input)) {
-            if (d->hash_stage.bytes < len) {
-                if (d->hash_stage.p) (void)hipFree(d->hash_stage.p);  // own stream synchronised after every call
-                d->hash_stage = DevBuf{};
-                HIP_TRY(hipMalloc(&d->hash_stage.p, len));
-                d->hash_stage.bytes = len;
+            if (len > kStageChunk) {
+                HIP_TRY(hipMalloc(&temp, len));
+                dp = temp;
+            } else {
+                if (d->hash_stage.bytes < len) {
+                    if (d->hash_stage.p) (void)hipFree(d->hash_stage.p);  // own stream synchronised after every call
+                    d->hash_stage = DevBuf{};
+                    HIP_TRY(hipMalloc(&d->hash_stage.p, kStageChunk));
+                    d->hash_stage.bytes = kStageChunk;
+                }
+                dp = d->hash_stage.p;
             }
-            HIP_TRY(hipMemcpyAsync(d->hash_stage.p, input, len, hipMemcpyHostToDevice, s));
-            dp = d->hash_stage.p;
+            const hipError_t ce = hipMemcpyAsync((void *)dp, input, len, hipMemcpyHostToDevice, s);
+            if (ce != hipSuccess) {
+                if (temp) (void)hipFree(temp);
+                return fail(AWS_CRT_AMD_ERR_HIP, std::string("hash staging copy: ") + hipGetErrorString(ce));
+            }
         }
         const uint64_t base = len ? (uint64_t)(uintptr_t)dp : 16;
         rc = strided_impl(d, alg, base, len, len, 1, nullptr, seed, d->h_res, s);
-        if (!rc) {
-            const hipError_t e = hipStreamSynchronize(s);
-            if (e != hipSuccess) rc = fail(AWS_CRT_AMD_ERR_HIP, hipGetErrorString(e));
+        {
+            const hipError_t e = hipStreamSynchronize(s);  // also before a failed launch's staging is freed
+            if (!rc && e != hipSuccess) rc = fail(AWS_CRT_AMD_ERR_HIP, hipGetErrorString(e));
         }
+        if (temp) (void)hipFree(temp);
         const volatile uint64_t *h = (const volatile uint64_t *)d->h_res;
         result[0] = rc ? 0 : h[0];
         if (osz == 16) result[1] = rc ? 0 : h[1];
@@ -965,6 +999,14 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
             const size_t osz = w / 8;
             hipStream_t s = (hipStream_t)hip_stream;
             void *d_out;
+            std::mutex *smu;
+            {
+                std::lock_guard<std::mutex> g(d->mu);
+                auto &m = d->mp_mu[s];
+                if (!m) m.reset(new std::mutex);
+                smu = m.get();
+            }
+            std::lock_guard<std::mutex> call(*smu);  // per stream, taken before d->mu (list_impl takes d->mu)
             {
                 std::lock_guard<std::mutex> g(d->mu);
                 DevBuf &ob = d->mp_out[s];

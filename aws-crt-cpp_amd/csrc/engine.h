@@ -44,7 +44,9 @@ struct ScanParams {
     // ---- geometry and constants
     uint32_t seg;                  // bytes per lane per tile (multiple of kGroupBytes)
     uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
-    uint32_t stream;               // W=32 strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel)
+    uint32_t stream;               // strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel /
+                                   // crc64_stream4_kernel); W=32: 1 = 8-byte lane words (512-thread workgroups),
+                                   // 2 = 16-byte lane words (one 1024-thread workgroup per CU)
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;
@@ -74,11 +76,13 @@ struct ScanParams {
 //                 63 lanes' words of a 256-byte row
 //   [3072, 3328)  T_0[e] = e * x^8: plain byte step for head / tail bytes
 //   [3328, 5376)  K-matrix image of x^(-64 l) (the streaming scan's 8-byte words), same layout
+//   [5376, 7424)  K-matrix image of x^(-128 l) (the streaming scan's 16-byte words), same layout
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 5376;
-constexpr int kBraidK64Word = 3328;  // first word of the x^(-64 l) K image
+constexpr int kBraidConstWords = 7424;
+constexpr int kBraidK64Word = 3328;   // first word of the x^(-64 l) K image
+constexpr int kBraidK128Word = 5376;  // first word of the x^(-128 l) K image
 
 struct XxhParams {
     const uint64_t *d_ptrs;  // device addresses (list) or null (strided)

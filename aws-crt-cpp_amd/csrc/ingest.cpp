@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -38,6 +39,9 @@
 #include <aws_crt_amd/checksums_batch.h>
 
 using namespace amdcrc;
+
+extern "C" int amdcrc_gpu_usable(void);      // engine.cpp
+extern "C" void amdcrc_note_fallback(void);  // abi_single.cpp: aws_crt_amd_fallback_count
 
 namespace {
 
@@ -334,6 +338,66 @@ void host_worker(JobImpl *job, size_t t, size_t threads) {
     }
 }
 
+// Worker streams of the fan-out calls (aws_crt_amd_checksum_list_devices / _checksum_devices),
+// cached per device like the ingest lanes: the engine keys its per-stream staging, workspaces and
+// sums by stream handle, so a stream created and destroyed per call would leave those behind on every
+// call.  A pooled stream carries the call's device result / seed buffer, grown geometrically.
+struct FanStream {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    void *buf = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_fan_mu;
+std::vector<std::vector<FanStream *>> g_fan_free;
+
+// the calling thread's current device must be `dev`
+FanStream *fan_take(int dev) {
+    {
+        std::lock_guard<std::mutex> g(g_fan_mu);
+        if ((int)g_fan_free.size() <= dev) g_fan_free.resize((size_t)dev + 1);
+        auto &v = g_fan_free[(size_t)dev];
+        if (!v.empty()) {
+            FanStream *f = v.back();
+            v.pop_back();
+            return f;
+        }
+    }
+    std::unique_ptr<FanStream> f(new FanStream);
+    f->dev = dev;
+    if (hipStreamCreateWithFlags(&f->st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    return f.release();
+}
+void fan_give(FanStream *f) {
+    if (!f) return;
+    std::lock_guard<std::mutex> g(g_fan_mu);
+    g_fan_free[(size_t)f->dev].push_back(f);
+}
+bool fan_reserve(FanStream *f, size_t bytes) {
+    if (f->bytes >= bytes) return true;
+    if (f->buf) {
+        if (hipStreamSynchronize(f->st) != hipSuccess) return false;  // nothing queued may still use it
+        (void)hipFree(f->buf);
+        f->buf = nullptr;
+        f->bytes = 0;
+    }
+    const size_t cap = std::max<size_t>(bytes, 2 * f->bytes);
+    if (hipMalloc(&f->buf, cap) != hipSuccess) return false;
+    f->bytes = cap;
+    return true;
+}
+
+// host-path threads for a job that runs on the CPU: the process's CPU share, at most one per buffer
+size_t host_threads(size_t count) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    size_t t = hw ? hw : 1;
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v > 0) t = std::min<size_t>(t, (size_t)v);
+    }
+    return std::max<size_t>(1, std::min(t, std::max<size_t>(count, 1)));
+}
+
 int visible_devices() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) {
@@ -386,6 +450,10 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, 
             J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
         const int vis = visible_devices();
         int G = ndevices <= 0 ? vis : std::min(ndevices, vis);
+        if (is_crc(alg) && G > 0 && !amdcrc_gpu_usable()) {
+            amdcrc_note_fallback();  // a visible device the engine cannot use (not gfx950, HIP error)
+            G = 0;
+        }
         if (!is_crc(alg) || G <= 0) {
             // xxHash (or no device): the host path, one thread per device the job would have used
             const size_t threads = (size_t)std::max(1, std::min(G > 0 ? G : 1, 16));
@@ -417,8 +485,17 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
         if (!job) return AWS_CRT_AMD_ERR_INVALID_ARG;
         JobImpl &J = job->impl;
         for (auto &t : J.workers) t.join();
+        J.workers.clear();
         int rc = J.rc.load();
-        if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
+        if ((rc == AWS_CRT_AMD_ERR_HIP || rc == AWS_CRT_AMD_ERR_NO_DEVICE) && is_crc(J.alg)) {
+            // a device worker failed: the whole job on the host path instead, as the single-buffer ABI
+            // does (counted in aws_crt_amd_fallback_count); the value is the same function
+            const size_t threads = host_threads(J.count);
+            for (size_t t = 0; t < threads; ++t) J.spawn(host_worker, &J, t, threads);
+            for (auto &t : J.workers) t.join();
+            amdcrc_note_fallback();
+            rc = 0;
+        } else if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
             // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
             const uint64_t poly = alg_poly(J.alg);
             const int w = alg_width(J.alg);
@@ -488,12 +565,10 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list_devices(int alg, const void *const
                     ls[j] = lens[ix[j]];
                     if (h_seeds) std::memcpy(seeds.data() + j * ssz, (const uint8_t *)h_seeds + ix[j] * ssz, ssz);
                 }
-                hipStream_t st = nullptr;
-                void *dbuf = nullptr;
-                int e = hipSetDevice(g) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
-                                hipMalloc(&dbuf, n * (osz + ssz)) == hipSuccess
-                            ? 0
-                            : AWS_CRT_AMD_ERR_HIP;
+                FanStream *fs = hipSetDevice(g) == hipSuccess ? fan_take(g) : nullptr;
+                int e = fs && fan_reserve(fs, n * (osz + ssz)) ? 0 : AWS_CRT_AMD_ERR_HIP;
+                hipStream_t st = fs ? fs->st : nullptr;
+                void *dbuf = e ? nullptr : fs->buf;
                 void *dseed = dbuf ? (uint8_t *)dbuf + n * osz : nullptr;
                 if (!e && h_seeds && hipMemcpyAsync(dseed, seeds.data(), n * ssz, hipMemcpyHostToDevice, st) != hipSuccess)
                     e = AWS_CRT_AMD_ERR_HIP;
@@ -503,8 +578,8 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_list_devices(int alg, const void *const
                     e = AWS_CRT_AMD_ERR_HIP;
                 if (!e)
                     for (size_t j = 0; j < n; ++j) std::memcpy((uint8_t *)h_out + ix[j] * osz, res.data() + j * osz, osz);
-                if (dbuf) (void)hipFree(dbuf);
-                if (st) (void)hipStreamDestroy(st);
+                if (st && e) (void)hipStreamSynchronize(st);  // nothing of this call stays queued
+                fan_give(fs);
                 if (e) {
                     int z = 0;
                     rc.compare_exchange_strong(z, e);
@@ -540,7 +615,7 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_devices(int alg, const struct aws_crt_a
         if (n && vis <= 0) return AWS_CRT_AMD_ERR_NO_DEVICE;
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) return AWS_CRT_AMD_ERR_HIP;
-        std::vector<hipStream_t> own(n, nullptr);
+        std::vector<FanStream *> own(n, nullptr);
         int rc = 0;
         for (size_t i = 0; i < n && !rc; ++i) {
             if (b[i].device < 0 || b[i].device >= vis) {
@@ -553,19 +628,19 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_devices(int alg, const struct aws_crt_a
             }
             hipStream_t st = (hipStream_t)b[i].hip_stream;
             if (!st) {
-                if (hipStreamCreateWithFlags(&own[i], hipStreamNonBlocking) != hipSuccess) {
+                if (!(own[i] = fan_take(b[i].device))) {
                     rc = AWS_CRT_AMD_ERR_HIP;
                     break;
                 }
-                st = own[i];
+                st = own[i]->st;
             }
             rc = aws_crt_amd_checksum_strided(alg, b[i].d_base, b[i].stride, b[i].len, b[i].count, b[i].d_seeds, b[i].d_out, st);
         }
         for (size_t i = 0; i < n; ++i) {  // await every device (also after a failure: nothing stays queued)
             if (hipSetDevice(b[i].device) != hipSuccess) continue;
-            hipStream_t st = own[i] ? own[i] : (hipStream_t)b[i].hip_stream;
+            hipStream_t st = own[i] ? own[i]->st : (hipStream_t)b[i].hip_stream;
             if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = AWS_CRT_AMD_ERR_HIP;
-            if (own[i]) (void)hipStreamDestroy(own[i]);
+            fan_give(own[i]);
         }
         (void)hipSetDevice(cur);
         return rc;

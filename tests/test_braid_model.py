@@ -334,3 +334,97 @@ def test_braid_w8_padded_model_vs_oracle(alg, rows):
             seed = rnd.choice([0, rnd.getrandbits(32)])
             assert braid_w8_model(br, data, 0x1000 + misalign, seed, rows) == oracle.crc(alg, data, seed), \
                 (alg, rows, n, misalign)
+
+
+# ---- the streaming scan on 16-byte words (crc32_stream_kernel<POLY, 16>)
+ROW16 = 1024
+
+
+class BraidW16:
+    """1024-byte rows, lane l owning the 16-byte word at 16l; the row step is slice-by-16 on
+    a = (u ^ d0, d1, d2, d3) with T'_t[e] = e * x^(8(t+1)) * x^(8*1008), byte i indexing T'_(15-i);
+    K_l = x^(-128 l)."""
+
+    def __init__(self, alg):
+        P = self.P = POLY[alg]
+        skip = xpow8n(ROW16 - 16, P)
+        self.Tp = [[mulmod(table_entry(e, t, P), skip, P) for e in range(256)] for t in range(16)]
+        self.K = []
+        kl = 0x80000000
+        for _ in range(64):
+            self.K.append(kl)
+            for _ in range(128):
+                kl = inv_mulx(kl, P)
+
+    def hi(self, d1, d2, d3):
+        """the twelve lookups of d1..d3 (independent of the braid state)"""
+        v = 0
+        for d, w in ((1, d1), (2, d2), (3, d3)):
+            for q in range(4):
+                v ^= self.Tp[15 - (4 * d + q)][(w >> (8 * q)) & 255]
+        return v
+
+    def lo(self, x):
+        v = 0
+        for q in range(4):
+            v ^= self.Tp[15 - q][(x >> (8 * q)) & 255]
+        return v
+
+
+def lds_w16_schedule(lane):
+    """(dword d, slot k) -> (byte i, table t, LDS byte address without the entry row) of the kernel's
+    Braid32W16::init: region B (tables 7..0) at 64 KiB, table t at (t & 7) * 32, copy at 4 * copy"""
+    j, c = (lane >> 3) & 3, lane & 7
+    out = {}
+    for d in range(4):
+        for k in range(4):
+            q = (k + j) & 3
+            t = 15 - (4 * d + q)
+            addr = (65536 if t < 8 else 0) + (t & 7) * 32 + 4 * c
+            out[(d, k)] = (4 * d + q, t, addr)
+    return out
+
+
+def test_w16_lds_schedule_conflict_free_and_complete():
+    for half in (range(32), range(32, 64)):
+        for d in range(4):
+            for k in range(4):
+                # ds_read_b32: bank = (address / 4) mod 32; the entry row (e * 256) adds 0 mod 32 banks
+                banks = [(lds_w16_schedule(l)[(d, k)][2] // 4) % 32 for l in half]
+                assert len(set(banks)) == 32, (d, k)
+    for lane in range(64):
+        sch = lds_w16_schedule(lane)
+        assert sorted(i for i, _, _ in sch.values()) == list(range(16))  # all 16 bytes, once each
+        for (d, k), (i, t, addr) in sch.items():
+            assert t == 15 - i and i // 4 == d
+            assert addr + 255 * 256 + 4 <= 131072  # inside the 128 KiB of tables
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
+@pytest.mark.parametrize("rows", [1, 4, 12])
+def test_braid_w16_model_vs_oracle(alg, rows):
+    """whole-tile buffers: the kernel's stream_rows_w16 chain (x = u ^ d0(w_r); d1..d3 of row r enter
+    with row r's chain step), shares with K_l = x^(-128 l), tiles with x^(8*TILE*(T-1-k))"""
+    br = BraidW16(alg)
+    P = br.P
+    rnd = random.Random(hash((alg, rows, "w16")) & 0xFFFF)
+    tile = ROW16 * rows
+    for ntiles in (1, 2, 3):
+        data = bytes(rnd.getrandbits(8) for _ in range(tile * ntiles))
+        seed = rnd.choice([0, rnd.getrandbits(32)])
+        fin = 0
+        for k in range(ntiles):
+            r = 0
+            for lane in range(64):
+                u = (~seed & M32) if (k == 0 and lane == 0) else 0
+                words = []
+                for c in range(rows):
+                    o = k * tile + ROW16 * c + 16 * lane
+                    words.append([int.from_bytes(data[o + 4 * d: o + 4 * d + 4], "little") for d in range(4)])
+                x = u ^ words[0][0]
+                for c in range(1, rows):
+                    x = br.lo(x) ^ br.hi(*words[c - 1][1:]) ^ words[c][0]
+                u = br.lo(x) ^ br.hi(*words[-1][1:])
+                r ^= mulmod(u, br.K[lane], P)
+            fin ^= mulmod(r, xpow8n(tile * (ntiles - 1 - k), P), P)
+        assert (~fin & M32) == oracle.crc(alg, data, seed), (alg, rows, ntiles)

@@ -38,3 +38,16 @@ def test_concurrent_callers_under_tsan():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "[PASS] ConcurrentCallers" in r.stdout, r.stdout
     assert "ThreadSanitizer" not in r.stderr, r.stderr
+
+
+def test_unreadable_device_buffer_raises():
+    """A device buffer that neither the GPU nor a read-back can reach (tests/cpp/unreadable_stubs.cpp
+    injects it) must not yield a silent CRC: the value-only calls raise AWS_ERROR_UNSUPPORTED_OPERATION
+    into Aws::Crt::LastError() (reference source/Api.cpp:469-472), xxHash returns false, and a host
+    buffer afterwards is served normally.  ASan + UBSan build."""
+    _build("build/host_unreadable")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
+    r = subprocess.run([os.path.join(CPP, "build", "host_unreadable")], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[PASS] UnreadableDeviceBufferRaises" in r.stdout, r.stdout
+    assert "is unreadable" in r.stderr  # the diagnostic line is printed too
