@@ -34,6 +34,7 @@ extern "C" int amdcrc_gpu_usable(void);
 extern "C" int amdcrc_is_device_ptr(const void *p);
 extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_t seed, uint64_t *out);
 extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n);
+extern "C" int amdcrc_gpu_xxh3_blocks(const void *d_ptr, uint64_t nblocks, uint64_t seed, uint64_t acc[8]);
 
 using amdcrc::guarded;
 
@@ -165,9 +166,41 @@ int compute(Kind k, uint64_t seed, const uint8_t *p, size_t n, aws_byte_buf *out
 
 }  // namespace
 
-// Streaming object: the host states of cpu_checksums.h (O(1) memory).  Device-resident chunks are
-// read back through a bounded bounce buffer: a stream's state is one serial chain, so there is no
-// batch to give the GPU.
+// Streaming object: the host states of cpu_checksums.h (O(1) memory).  Device-resident chunks of an
+// XXH3 stream of at least kDeviceStreamBytes are absorbed on the GPU: XXH3's accumulate step is a
+// pure sum within each 1 KiB block, so the chunk's whole blocks are summed by all CUs and one wave
+// runs the scramble chain from the stream's accumulators (xxh3_kernels.hip), while the few hundred
+// bytes around them go through the host state (cpu::xxh3_update_source).  XXH64 is one serial
+// chain per stream (four lanes, each round depending on the last), so its device chunks are read
+// back through a bounded bounce buffer and hashed on the host.
+constexpr size_t kDeviceStreamBytes = 1u << 20;
+
+namespace {
+struct DeviceChunk {
+    const uint8_t *d;
+};
+bool chunk_read(void *ctx, uint8_t *dst, uint64_t off, size_t len) {
+    return !len || amdcrc_copy_to_host(dst, ((DeviceChunk *)ctx)->d + off, len) == 0;
+}
+bool chunk_blocks(void *ctx, cpu::Xxh3State *s, uint64_t off, uint64_t nblocks) {
+    const uint8_t *d = ((DeviceChunk *)ctx)->d + off;
+    if (amdcrc_gpu_usable() && amdcrc_gpu_xxh3_blocks(d, nblocks, s->seed, s->acc) == 0) return true;
+    // the GPU path failed: the same blocks on the host path, read back in bounded pieces
+    g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    constexpr uint64_t kPiece = 1024;  // blocks (1 MiB)
+    uint8_t *bounce = (uint8_t *)std::malloc(kPiece * 1024);
+    if (!bounce) return false;
+    bool ok = true;
+    for (uint64_t b = 0; b < nblocks && ok; b += kPiece) {
+        const uint64_t m = nblocks - b < kPiece ? nblocks - b : kPiece;
+        ok = amdcrc_copy_to_host(bounce, d + 1024 * b, (size_t)(1024 * m)) == 0;
+        if (ok) cpu::xxh3_consume(s, bounce, (size_t)(16 * m));
+    }
+    std::free(bounce);
+    return ok;
+}
+}  // namespace
+
 struct aws_xxhash {
     aws_allocator *allocator;
     Kind kind;
@@ -297,6 +330,11 @@ AWS_XXHASH_API int aws_xxhash_update(aws_xxhash *h, aws_byte_cursor data) {
     if (!amdcrc_is_device_ptr(data.ptr)) {
         feed(data.ptr, data.len);
         return AWS_OP_SUCCESS;
+    }
+    if (h->kind != K_XXH64 && data.len >= kDeviceStreamBytes) {
+        DeviceChunk ctx{data.ptr};
+        const cpu::Xxh3Source src{&ctx, chunk_read, chunk_blocks};
+        return cpu::xxh3_update_source(&h->x3, data.len, src) ? AWS_OP_SUCCESS : aws_raise_error(AWS_ERROR_UNSUPPORTED_OPERATION);
     }
     constexpr size_t kChunk = 1u << 20;
     uint8_t *bounce = (uint8_t *)std::malloc(data.len < kChunk ? data.len : kChunk);

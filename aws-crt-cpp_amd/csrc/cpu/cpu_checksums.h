@@ -63,6 +63,20 @@ struct Xxh3State {
 };
 void xxh3_reset(Xxh3State *s, uint64_t seed);
 void xxh3_update(Xxh3State *s, const uint8_t *p, size_t n);
+// k stripes at the state's stripe position (scrambling at block ends); `last` becomes p's final stripe
+void xxh3_consume(Xxh3State *s, const uint8_t *p, size_t k);
+// xxh3_update over input the host cannot address directly (device memory): `read` copies bytes
+// [off, off + len) of the input into host memory; `blocks` absorbs `nblocks` whole 1 KiB blocks at
+// offset off into s->acc (called with s->stripes == 0, which it leaves 0).  Every byte outside
+// those blocks (the buffer top-up, stripes up to a block boundary, the last partial block and the
+// 1..64 buffered bytes) goes through `read` and the host path, so the result is xxh3_update's
+// exactly.  The state is updated only if every callback succeeds.
+struct Xxh3Source {
+    void *ctx;
+    bool (*read)(void *ctx, uint8_t *dst, uint64_t off, size_t len);
+    bool (*blocks)(void *ctx, Xxh3State *s, uint64_t off, uint64_t nblocks);
+};
+bool xxh3_update_source(Xxh3State *s, uint64_t n, const Xxh3Source &src);
 uint64_t xxh3_64_digest(const Xxh3State *s);
 void xxh3_128_digest(const Xxh3State *s, uint64_t out_hi_lo[2]);
 

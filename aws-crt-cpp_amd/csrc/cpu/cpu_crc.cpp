@@ -22,6 +22,11 @@
 #include <cpuid.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -249,6 +254,84 @@ uint64_t crc64nvme(const uint8_t *p, size_t n, uint64_t previous) {
     return crc_tier(ALG_CRC64NVME, p, n, previous, best_tier());
 }
 
+namespace {
+
+// Persistent workers for batch(): spawning a std::thread costs tens of microseconds, as much as
+// checksumming a few hundred KiB, so the threads stay parked between calls.  One batch at a time
+// uses the pool; a call that finds it busy runs on threads of its own.
+class Pool {
+  public:
+    bool try_run(size_t n, const std::function<void(size_t)> &fn) {
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            try {
+                while (workers_.size() + 1 < n) workers_.emplace_back([this, i = workers_.size() + 1] { loop(i); });
+            } catch (...) {
+                // fewer workers than asked for: the indices without one run on this thread below
+            }
+            fn_ = &fn;
+            n_ = n;
+            pending_ = std::min(n, workers_.size() + 1) - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        for (size_t i = workers_.size() + 1; i < n; ++i) fn(i);
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+        return true;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+  private:
+    void loop(size_t idx) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t)> *fn;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (idx >= n_) continue;  // not part of this batch
+                fn = fn_;
+            }
+            (*fn)(idx);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+Pool &pool() {
+    static Pool p;
+    return p;
+}
+
+}  // namespace
+
+// Host batch (aws_crt_amd_cpu_batch).  Work items are claimed dynamically by `threads` threads.  A
+// CRC buffer longer than the piece size is cut into pieces, each checksummed from seed 0 (the first
+// from the caller's seed) and folded in order with Combine (CRC.h:41-51) -- so a batch of fewer
+// buffers than threads, such as 8 x 64 MiB, still keeps every thread busy.  A hash is one serial
+// chain per buffer: one item per buffer.
 void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64_t *seeds, uint64_t *out, size_t count,
            int threads) {
     auto one = [&](size_t i) {
@@ -262,18 +345,62 @@ void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64
             default: xxh3_128(ptrs[i], lens[i], s, out + 2 * i); break;
         }
     };
-    if (threads <= 1 || count <= 1) {
+    const size_t nt = threads <= 1 ? 1 : (size_t)threads;
+    if (nt == 1 || count == 0) {
         for (size_t i = 0; i < count; ++i) one(i);
         return;
     }
-    const size_t nt = std::min<size_t>((size_t)threads, count);
-    std::vector<std::thread> pool;
-    pool.reserve(nt);
-    for (size_t t = 0; t < nt; ++t)
-        pool.emplace_back([&, t] {
-            for (size_t i = t; i < count; i += nt) one(i);
-        });
-    for (auto &th : pool) th.join();
+    // items: (buffer, piece) with pieces only for CRCs
+    size_t total = 0;
+    for (size_t i = 0; i < count; ++i) total += lens[i];
+    const bool crc = alg <= 2;
+    const size_t piece = crc ? std::max<size_t>((size_t)1 << 20, (total / (4 * nt) + 4095) & ~(size_t)4095) : ~(size_t)0;
+    std::vector<size_t> first(count + 1, 0);  // first item of buffer i
+    for (size_t i = 0; i < count; ++i) first[i + 1] = first[i] + (lens[i] > piece ? (lens[i] + piece - 1) / piece : 1);
+    const size_t nitems = first[count];
+    if (nitems == count && count == 1) {
+        one(0);
+        return;
+    }
+    std::vector<uint64_t> pv(crc ? nitems : 0);
+    std::atomic<size_t> next{0};
+    auto work = [&](size_t) {
+        for (;;) {
+            const size_t it = next.fetch_add(1, std::memory_order_relaxed);
+            if (it >= nitems) return;
+            const size_t i = (size_t)(std::upper_bound(first.begin(), first.end(), it) - first.begin()) - 1;
+            if (!crc || first[i + 1] - first[i] == 1) {
+                one(i);
+                if (crc) pv[it] = out[i];
+                continue;
+            }
+            const size_t k = it - first[i], off = k * piece, n = std::min(piece, lens[i] - off);
+            const uint64_t s = k == 0 && seeds ? seeds[i] : 0;
+            pv[it] = alg == 0 ? crc32(ptrs[i] + off, n, (uint32_t)s) : alg == 1 ? crc32c(ptrs[i] + off, n, (uint32_t)s)
+                                                                           : crc64nvme(ptrs[i] + off, n, s);
+        }
+    };
+    const size_t nrun = std::min(nt, nitems);
+    if (!pool().try_run(nrun, work)) {
+        std::vector<std::thread> ts;
+        for (size_t t = 1; t < nrun; ++t) ts.emplace_back(work, t);
+        work(0);
+        for (auto &th : ts) th.join();
+    }
+    if (!crc) return;
+    // fold the pieces of every split buffer: crc = Combine(crc, piece, |piece|)
+    const uint64_t poly = alg_poly(alg);
+    const int w = alg_width(alg);
+    for (size_t i = 0; i < count; ++i) {
+        const size_t np = first[i + 1] - first[i];
+        if (np == 1) continue;
+        uint64_t acc = pv[first[i]];
+        for (size_t k = 1; k < np; ++k) {
+            const size_t n = std::min(piece, lens[i] - k * piece);
+            acc = gf2_mulmod(acc, gf2_xpow8n(n, poly, w), poly, w) ^ pv[first[i] + k];
+        }
+        out[i] = acc;
+    }
 }
 
 }  // namespace cpu

@@ -14,6 +14,8 @@
 #include <immintrin.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "cpu_checksums.h"
 
 namespace amdcrc {
@@ -437,6 +439,60 @@ void xxh3_update(Xxh3State *s, const uint8_t *p, size_t n) {
     }
     memcpy(s->buf, p, n);
     s->bufn = (uint32_t)n;
+}
+
+void xxh3_consume(Xxh3State *s, const uint8_t *p, size_t k) {
+    if (!k) return;
+    consume(s->acc, s->stripes, p, k, s->secret);
+    memcpy(s->last, p + 64 * k - 64, 64);
+}
+
+// xxh3_update's steps with the bulk of whole blocks handed to src.blocks (the device)
+bool xxh3_update_source(Xxh3State *st, uint64_t n, const Xxh3Source &src) {
+    Xxh3State s = *st;
+    alignas(64) uint8_t tmp[64 * 15];
+    if (s.bufn + n <= sizeof(s.buf)) {
+        if (n && !src.read(src.ctx, s.buf + s.bufn, 0, (size_t)n)) return false;
+        s.bufn += (uint32_t)n;
+        s.total += n;
+        *st = s;
+        return true;
+    }
+    uint64_t off = 0;
+    if (s.bufn) {  // top the buffer up and consume all of it: more input follows
+        const size_t fill = sizeof(s.buf) - s.bufn;
+        if (!src.read(src.ctx, s.buf + s.bufn, 0, fill)) return false;
+        off = fill;
+        consume(s.acc, s.stripes, s.buf, sizeof(s.buf) / 64, s.secret);
+        memcpy(s.last, s.buf + sizeof(s.buf) - 64, 64);
+        s.bufn = 0;
+    }
+    if (n - off > sizeof(s.buf)) {  // bulk, leaving 1..64 bytes
+        uint64_t k = (n - off - 1) / 64;
+        const uint64_t h = std::min<uint64_t>((16 - s.stripes) % 16, k);  // stripes up to a block boundary
+        if (h) {
+            if (!src.read(src.ctx, tmp, off, (size_t)(64 * h))) return false;
+            xxh3_consume(&s, tmp, (size_t)h);
+            off += 64 * h, k -= h;
+        }
+        const uint64_t nbl = k / 16;  // whole blocks (s.stripes is 0 whenever nbl > 0)
+        if (nbl) {
+            if (!src.blocks(src.ctx, &s, off, nbl)) return false;
+            s.stripes = 0;
+            off += 1024 * nbl, k -= 16 * nbl;
+            if (!src.read(src.ctx, s.last, off - 64, 64)) return false;
+        }
+        if (k) {
+            if (!src.read(src.ctx, tmp, off, (size_t)(64 * k))) return false;
+            xxh3_consume(&s, tmp, (size_t)k);
+            off += 64 * k;
+        }
+    }
+    if (!src.read(src.ctx, s.buf, off, (size_t)(n - off))) return false;
+    s.bufn = (uint32_t)(n - off);
+    s.total += n;
+    *st = s;
+    return true;
 }
 
 namespace {

@@ -565,15 +565,23 @@ struct Braid32W16 : Braid32<POLY> {
         }
         return h;
     }
-    // the chain step: x = u ^ d0 of a row whose other lookups are h; returns the row's u' ^ wn
-    __device__ __forceinline__ uint32_t look_lo(uint32_t x, const Hi &h, uint32_t wn) const {
+    // the chain step in two parts: the four lookups of x = u ^ d0 (issued first), then the row's
+    // u' ^ wn once they return, with the row's other twelve lookups h
+    struct Lo {
         uint32_t v[4];
+    };
+    __device__ __forceinline__ Lo lo_issue(uint32_t x) const {
+        Lo l;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = look(0, k, x);
+        for (int k = 0; k < 4; ++k) l.v[k] = look(0, k, x);
+        return l;
+    }
+    __device__ __forceinline__ uint32_t lo_finish(const Lo &l, const Hi &h, uint32_t wn) const {
         const uint32_t o = xor3(xor3(xor3(h.v[0], h.v[1], h.v[2]), xor3(h.v[3], h.v[4], h.v[5]), xor3(h.v[6], h.v[7], h.v[8])),
                                 xor3(h.v[9], h.v[10], h.v[11]), wn);
-        return xor3(xor3(o, v[0], v[1]), v[2], v[3]);
+        return xor3(xor3(o, l.v[0], l.v[1]), l.v[2], l.v[3]);
     }
+    __device__ __forceinline__ uint32_t look_lo(uint32_t x, const Hi &h, uint32_t wn) const { return lo_finish(lo_issue(x), h, wn); }
 };
 
 struct W16Group {
@@ -1114,12 +1122,18 @@ template <int R, class B>
 __device__ __forceinline__ uint32_t stream_rows_w16(uint32_t x, const typename B::Hi &h, W16Group &cur, W16Group &nxt,
                                                     uint32_t voff, uint64_t snext, const B &eng) {
     if constexpr (R < kW16RowsPerGroup) {
+        // issue order: this row's load, the chain's four lookups, the row's twelve off-chain lookups;
+        // only then the XORs (a scheduling barrier keeps the compiler from reducing the previous row's
+        // twelve, and waiting for them, ahead of the chain's lookups)
         nxt.w[R] = gld_w16<R>(voff, snext);
+        typename B::Lo lo{};
+        if constexpr (R > 0) lo = eng.lo_issue(x);
+        const typename B::Hi hn = eng.look_hi(cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
         if constexpr (R == 0)
             x ^= cur.w[0].x;
         else
-            x = eng.look_lo(x, h, cur.w[R].x);
-        const typename B::Hi hn = eng.look_hi(cur.w[R]);
+            x = eng.lo_finish(lo, h, cur.w[R].x);
         __builtin_amdgcn_sched_barrier(0);
         return stream_rows_w16<R + 1, B>(x, hn, cur, nxt, voff, snext, eng);
     } else {

@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -108,6 +109,7 @@ struct Device {
     hipEvent_t pin_free[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
     DevBuf hash_stage;        // whole-buffer device copy for GPU-dispatched host xxHash
+    DevBuf xstream_sums;      // streaming XXH3 on device chunks: block sums of one pass
     DevBuf ceil_sink;         // read-ceiling diagnostics: one word per wave
     void *d_small = nullptr;  // results / seeds for the single path
     void *h_res = nullptr;    // pinned, coherent host slot the single path's last launch stores into
@@ -419,6 +421,123 @@ struct Batch {
 int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, size_t len, size_t count, uint64_t seed_all,
                  hipStream_t s);
 
+// ---- XXH64 over few long device buffers: the stream-ordered host route.
+// XXH64 is one serial chain per buffer (four lanes whose every round depends on the last): a
+// dependent 64-bit multiply-add-rotate per 32-byte stripe, about 41 cycles per round on a gfx950
+// SIMD (1.7 GiB/s per buffer) against about 1.3 ns on one host core.  A batch of fewer buffers than
+// kX64HostMaxBuffers therefore goes D2H in 64 MiB slices (one hipMemcpy2DAsync per slice: a row of
+// every buffer) and is hashed by host threads, one buffer each, in stream-ordered host functions;
+// the results go back H2D on the same stream, so the call keeps the batch ABI's asynchronous,
+// stream-ordered contract.  Larger batches keep the GPU kernels.
+#ifndef AMDCRC_X64_HOST_MAX  // compile-time only (A/B builds: 0 keeps every XXH64 batch on the GPU kernels)
+#define AMDCRC_X64_HOST_MAX 32
+#endif
+constexpr size_t kX64HostMaxBuffers = AMDCRC_X64_HOST_MAX;
+constexpr size_t kX64HostMinBytes = 1u << 20;
+constexpr size_t kX64StageBytes = 64u << 20;
+constexpr size_t kX64StageExtra = 16 * 64;  // seeds, then results (at most 64 buffers)
+static_assert(kX64HostMaxBuffers <= 64, "staging extra");
+
+std::mutex g_x64_mu;
+std::vector<void *> g_x64_free;  // pinned staging buffers (portable) not owned by a queued job
+
+struct X64Job;
+struct X64Chunk {
+    X64Job *job;
+    size_t rowbytes;
+    bool first, last;
+};
+struct X64Job {
+    size_t count = 0;
+    uint8_t *pin = nullptr;  // kX64StageBytes of rows, then kX64StageExtra
+    uint64_t *h_seed = nullptr, *h_res = nullptr;
+    bool seeds = false;
+    uint64_t seed_all = 0;
+    std::vector<cpu::Xxh64State> st;
+    std::vector<X64Chunk> chunks;
+};
+
+void x64_chunk_fn(void *u) noexcept {
+    const X64Chunk *c = (const X64Chunk *)u;
+    X64Job *j = c->job;
+    auto row = [&](size_t i) {
+        if (c->first) cpu::xxh64_reset(&j->st[i], j->seeds ? j->h_seed[i] : j->seed_all);
+        cpu::xxh64_update(&j->st[i], j->pin + i * c->rowbytes, c->rowbytes);
+        if (c->last) j->h_res[i] = cpu::xxh64_digest(&j->st[i]);
+    };
+    // one host thread per buffer (the calling runtime thread takes buffer 0)
+    std::vector<std::thread> ts;
+    size_t spawned = 1;
+    try {
+        for (; spawned < j->count; ++spawned) ts.emplace_back(row, spawned);
+    } catch (...) {
+    }
+    row(0);
+    for (auto &t : ts) t.join();
+    for (size_t i = spawned; i < j->count; ++i) row(i);  // threads that could not be started
+}
+void x64_free_fn(void *u) noexcept {
+    X64Job *j = (X64Job *)u;
+    {
+        std::lock_guard<std::mutex> g(g_x64_mu);
+        try {
+            g_x64_free.push_back(j->pin);
+        } catch (...) {
+            (void)0;  // the staging buffer is dropped (leaked) rather than freed from a callback
+        }
+    }
+    delete j;
+}
+
+int xxh64_host_route(uint64_t base, size_t stride, size_t len, size_t count, const void *d_seeds, uint64_t seed_all,
+                     void *d_out, hipStream_t s) {
+    std::unique_ptr<X64Job> j(new X64Job);
+    {
+        std::lock_guard<std::mutex> g(g_x64_mu);
+        if (!g_x64_free.empty()) {
+            j->pin = (uint8_t *)g_x64_free.back();
+            g_x64_free.pop_back();
+        }
+    }
+    if (!j->pin) HIP_TRY(hipHostMalloc((void **)&j->pin, kX64StageBytes + kX64StageExtra, hipHostMallocPortable));
+    auto give_back = [&]() {
+        std::lock_guard<std::mutex> g(g_x64_mu);
+        g_x64_free.push_back(j->pin);
+    };
+    j->count = count;
+    j->h_seed = (uint64_t *)(j->pin + kX64StageBytes);
+    j->h_res = j->h_seed + 64;
+    j->seeds = d_seeds != nullptr;
+    j->seed_all = seed_all;
+    j->st.resize(count);
+    const size_t slice = std::min<size_t>(len, (kX64StageBytes / count) & ~(size_t)63);
+    for (size_t off = 0; off < len; off += slice)
+        j->chunks.push_back({j.get(), std::min(slice, len - off), off == 0, off + slice >= len});
+    hipError_t e = hipSuccess;
+    if (g_time_events[0]) e = hipEventRecord((hipEvent_t)g_time_events[0], s);
+    if (!e && d_seeds) e = hipMemcpyAsync(j->h_seed, d_seeds, 8 * count, hipMemcpyDefault, s);
+    size_t off = 0, queued = 0;
+    for (; !e && queued < j->chunks.size(); ++queued) {
+        X64Chunk &c = j->chunks[queued];
+        e = hipMemcpy2DAsync(j->pin, c.rowbytes, (const void *)(uintptr_t)(base + off), stride, c.rowbytes, count,
+                             hipMemcpyDeviceToHost, s);
+        if (!e) e = hipLaunchHostFunc(s, x64_chunk_fn, &c);
+        off += c.rowbytes;
+    }
+    if (!e) e = hipMemcpyAsync(d_out, j->h_res, 8 * count, hipMemcpyDefault, s);  // d_out may be pinned host memory (the single path)
+    if (!e && g_time_events[1]) e = hipEventRecord((hipEvent_t)g_time_events[1], s);
+    g_time_events[0] = g_time_events[1] = nullptr;
+    if (!e) e = hipLaunchHostFunc(s, x64_free_fn, j.get());
+    if (e) {
+        // whatever was queued refers to the job: let it drain, then release the job here
+        (void)hipStreamSynchronize(s);
+        give_back();
+        return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh64 host route: ") + hipGetErrorString(e));
+    }
+    j.release();  // x64_free_fn owns it now
+    return 0;
+}
+
 int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, size_t count, const void *d_seeds,
                  uint64_t seed_all, void *d_out, hipStream_t s) {
     if (count == 0) return 0;
@@ -427,6 +546,8 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         const Batch b{base, d_seeds, d_out};
         return scan_batches(d, alg, &b, 1, stride, len, count, seed_all, s);
     }
+    if (alg == AWS_CRT_AMD_XXH64 && count <= kX64HostMaxBuffers && len >= kX64HostMinBytes && !capturing(s))
+        return xxh64_host_route(base, stride, len, count, d_seeds, seed_all, d_out, s);
     {
         XxhParams xp{};
         xp.base = base;
@@ -792,6 +913,45 @@ extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_
 }
 extern "C" int amdcrc_copy_to_host(void *dst, const void *src, size_t n) {
     return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+// Streaming XXH3 (abi_single.cpp aws_xxhash_update): nblocks whole 1 KiB blocks of device memory
+// absorbed into the stream's eight accumulators acc (in / out), in passes of at most 256 MiB (16 MiB
+// of block sums); the accumulators stay on the device between passes.  Synchronous.
+extern "C" int amdcrc_gpu_xxh3_blocks(const void *d_ptr, uint64_t nblocks, uint64_t seed, uint64_t acc[8]) {
+    return guarded(err_sink, [&]() -> int {
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        if (!is_device_ptr(d_ptr)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "xxh3 stream: not device memory");
+        std::lock_guard<std::mutex> g(d->single_mu);
+        if ((rc = ensure_stage(d, 4096))) return rc;
+        hipStream_t s = d->own_stream;
+        constexpr uint64_t kPassBlocks = 256 * 1024;
+        const uint64_t pass = std::min<uint64_t>(nblocks, kPassBlocks);
+        if (d->xstream_sums.bytes < pass * 64) {
+            if (d->xstream_sums.p) {
+                HIP_TRY(hipStreamSynchronize(s));  // the engine's own stream only
+                (void)hipFree(d->xstream_sums.p);
+            }
+            d->xstream_sums = DevBuf{};
+            HIP_TRY(hipMalloc(&d->xstream_sums.p, pass * 64));
+            d->xstream_sums.bytes = pass * 64;
+        }
+        uint64_t *d_acc = (uint64_t *)d->d_small;  // 64 B: the single path's slots (under single_mu)
+        HIP_TRY(hipMemcpyAsync(d_acc, acc, 64, hipMemcpyHostToDevice, s));
+        for (uint64_t b = 0; b < nblocks; b += kPassBlocks) {
+            const uint64_t m = std::min(kPassBlocks, nblocks - b);
+            const int e = amdcrc_launch_xxh3_stream((const uint8_t *)d_ptr + 1024 * b, m, seed, (uint64_t *)d->xstream_sums.p, d_acc, s);
+            if (e) {
+                (void)hipStreamSynchronize(s);
+                return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh3 stream launch: ") + hipGetErrorString((hipError_t)e));
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(d->h_res, d_acc, 64, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::memcpy(acc, d->h_res, 64);
+        return 0;
+    });
 }
 
 // ================================================================== C ABI

@@ -136,5 +136,6 @@ int amdcrc_launch_scan(int alg, const amdcrc::ScanParams *p, int nblocks, void *
 int amdcrc_launch_xxh64(const amdcrc::XxhParams *p, void *stream, void *const *events);
 int amdcrc_launch_xxh3_blocksum(const amdcrc::XxhParams *p, void *stream, void *start_event);
 int amdcrc_launch_xxh3(int bits, const amdcrc::XxhParams *p, void *stream, void *const *events);
+int amdcrc_launch_xxh3_stream(const void *d_ptr, uint64_t nblocks, uint64_t seed, uint64_t *d_sums, uint64_t *d_acc, void *stream);
 int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint32_t *sink, int nblocks, void *stream, void *const *events);
 }

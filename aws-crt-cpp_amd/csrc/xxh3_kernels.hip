@@ -311,12 +311,86 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// The scramble chain of the split long path over nb blocks' accumulator sums S[8 blk + c], starting
+// from accumulator value acc_in (lane l: accumulator c = l & 7, replicated over the lane's 8 groups);
+// returns the accumulator after the last block's scramble.  Lane l loads the sum of block g + (l >> 3)
+// for its accumulator (one coalesced 512-byte load per 8 blocks, sixteen loads in flight); the
+// per-block values reach the lanes of their accumulator by shuffles that do not depend on the
+// accumulators.  One scramble chain per lane per block.
+__device__ __forceinline__ uint64_t scramble_chain(const uint64_t *S, uint64_t nb, uint64_t acc_in, uint64_t stv, int lane) {
+    const int c8 = lane & 7, s8 = lane >> 3;
+    const uint64_t accv = acc_in;
+    constexpr int G = 8, DS = 16;
+    // loads are unconditional (addresses clamped to the last block) so that the wait before a
+    // group's shuffles counts only that group's load: DS groups stay in flight
+    auto ldg = [&](uint64_t g) -> uint64_t {
+        uint64_t blk = g * G + (uint64_t)s8;
+        blk = blk < nb ? blk : nb - 1;
+        return *(const __attribute__((address_space(1))) uint64_t *)(S + blk * 8 + c8);
+    };
+    // the chain carries u = acc + v (the next block's sum already added): per block
+    //   a = u ^ (u >> 47) ^ key;  u' = a * P32_1 + v_next
+    // = one v_xor3 after the shift, then v_mad_u64_u32 (low half, v_next as the addend) beside
+    // v_mul_lo_u32 (high half), then one add
+    const uint32_t kl = (uint32_t)stv, kh = (uint32_t)(stv >> 32);
+    auto step = [&](uint32_t &ul, uint32_t &uh, uint64_t vnext) {
+        const uint32_t al = ul ^ (uh >> 15) ^ kl, ah = uh ^ kh;
+        uint32_t c = ah * (uint32_t)P32_1;
+        asm("" : "+v"(c));  // keep the high product off the low mad's chain
+        const uint64_t m = (uint64_t)al * (uint32_t)P32_1 + vnext;
+        ul = (uint32_t)m;
+        uh = (uint32_t)(m >> 32) + c;
+    };
+    // start from the state whose step yields accv + v0: a = accv * P^-1, u0 = xorshift^-1(a ^ key)
+    // (x ^ (x >> 47) is its own inverse on 64 bits), so every block is the same step
+    const uint64_t b0 = (accv * kP32_1Inv) ^ stv, u0 = b0 ^ (b0 >> 47);
+    uint32_t ul = (uint32_t)u0, uh = (uint32_t)(u0 >> 32);
+    uint64_t ya[G], yb[G];
+    auto perm = [&](uint64_t xv, uint64_t (&v)[G]) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) v[j] = shfl64(xv, 8 * j + c8);
+    };
+    uint64_t x[DS];
+#pragma unroll
+    for (int d = 0; d < DS; ++d) x[d] = ldg(d);
+    const uint64_t ng = (nb + G - 1) / G, nround = (nb / G) / DS;
+    uint64_t g = 0;
+    perm(x[0], ya);
+    for (uint64_t r = 0; r < nround; ++r, g += DS) {
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+            uint64_t (&cur)[G] = (d & 1) ? yb : ya;
+            uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
+            perm(x[(d + 1) % DS], nxt);  // group g + d + 1 (x[0] already holds g + DS)
+            x[d] = ldg(g + DS + d);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < G; ++j) step(ul, uh, cur[j]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // at most DS groups remain (the last may be partial); their sums are in the ring, and the
+    // first of them already in ya (DS is even)
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+        if (g + d < ng) {
+            uint64_t (&cur)[G] = (d & 1) ? yb : ya;
+            uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
+            if (d + 1 < DS && g + d + 1 < ng) perm(x[d + 1], nxt);
+            const uint64_t cnt = nb - (g + d) * G < (uint64_t)G ? nb - (g + d) * G : (uint64_t)G;
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if ((uint64_t)j < cnt) step(ul, uh, cur[j]);
+        }
+    }
+    step(ul, uh, 0);  // the last block's scramble
+    return ((uint64_t)uh << 32) | ul;
+}
+
 // SPLIT: the full blocks' class sums were written by xxh3_blocksum_kernel (64 B per block at
-// p.d_sums + 8 (i nb + blk)); this wave only scrambles, one accumulator per lane: lane l owns
-// accumulator c = l & 7 and loads its sum for block g + (l >> 3) (one coalesced 512-byte load per 8
-// blocks, sixteen loads in flight); the per-block values reach the lanes of their accumulator by
-// shuffles that do not depend on the accumulators.  One scramble chain per lane per block (two in
-// the 4-class layout of the one-pass path) halves the serial instruction stream of a block.
+// p.d_sums + 8 (i nb + blk)); this wave only scrambles (scramble_chain: one accumulator per lane,
+// against two in the 4-class layout of the one-pass path, halves the serial instruction stream of a
+// block).
 template <int BITS, bool ALIGNED, bool SPLIT = false>
 __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *ptr, uint64_t n, uint64_t seed, int lane) {
     const int s = lane >> 2, wp = lane & 3;
@@ -328,75 +402,7 @@ __device__ void xxh3_long_wave(const XxhParams &p, uint64_t i, const uint8_t *pt
     const uint8_t *q = ptr + 16 * lane;
     uint64_t accv = 0;  // SPLIT: accumulator l & 7
     if (SPLIT) {
-        const uint64_t *S = p.d_sums + i * nb * 8;
-        const int c8 = lane & 7, s8 = lane >> 3;
-        const uint64_t stv = sec64(128 + 8 * c8, seed);
-        accv = init[c8];
-        constexpr int G = 8, DS = 16;
-        // loads are unconditional (addresses clamped to the last block) so that the wait before a
-        // group's shuffles counts only that group's load: DS groups stay in flight
-        auto ldg = [&](uint64_t g) -> uint64_t {
-            uint64_t blk = g * G + (uint64_t)s8;
-            blk = blk < nb ? blk : nb - 1;
-            return *(const __attribute__((address_space(1))) uint64_t *)(S + blk * 8 + c8);
-        };
-        // the chain carries u = acc + v (the next block's sum already added): per block
-        //   a = u ^ (u >> 47) ^ key;  u' = a * P32_1 + v_next
-        // = one v_xor3 after the shift, then v_mad_u64_u32 (low half, v_next as the addend) beside
-        // v_mul_lo_u32 (high half), then one add
-        const uint32_t kl = (uint32_t)stv, kh = (uint32_t)(stv >> 32);
-        auto step = [&](uint32_t &ul, uint32_t &uh, uint64_t vnext) {
-            const uint32_t al = ul ^ (uh >> 15) ^ kl, ah = uh ^ kh;
-            uint32_t c = ah * (uint32_t)P32_1;
-            asm("" : "+v"(c));  // keep the high product off the low mad's chain
-            const uint64_t m = (uint64_t)al * (uint32_t)P32_1 + vnext;
-            ul = (uint32_t)m;
-            uh = (uint32_t)(m >> 32) + c;
-        };
-        // start from the state whose step yields accv + v0: a = accv * P^-1, u0 = xorshift^-1(a ^ key)
-        // (x ^ (x >> 47) is its own inverse on 64 bits), so every block is the same step
-        const uint64_t b0 = (accv * kP32_1Inv) ^ stv, u0 = b0 ^ (b0 >> 47);
-        uint32_t ul = (uint32_t)u0, uh = (uint32_t)(u0 >> 32);
-        uint64_t ya[G], yb[G];
-        auto perm = [&](uint64_t xv, uint64_t (&v)[G]) {
-#pragma unroll
-            for (int j = 0; j < G; ++j) v[j] = shfl64(xv, 8 * j + c8);
-        };
-        uint64_t x[DS];
-#pragma unroll
-        for (int d = 0; d < DS; ++d) x[d] = ldg(d);
-        const uint64_t ng = (nb + G - 1) / G, nround = (nb / G) / DS;
-        uint64_t g = 0;
-        perm(x[0], ya);
-        for (uint64_t r = 0; r < nround; ++r, g += DS) {
-#pragma unroll
-            for (int d = 0; d < DS; ++d) {
-                uint64_t (&cur)[G] = (d & 1) ? yb : ya;
-                uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
-                perm(x[(d + 1) % DS], nxt);  // group g + d + 1 (x[0] already holds g + DS)
-                x[d] = ldg(g + DS + d);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < G; ++j) step(ul, uh, cur[j]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // at most DS groups remain (the last may be partial); their sums are in the ring, and the
-        // first of them already in ya (DS is even)
-#pragma unroll
-        for (int d = 0; d < DS; ++d) {
-            if (g + d < ng) {
-                uint64_t (&cur)[G] = (d & 1) ? yb : ya;
-                uint64_t (&nxt)[G] = (d & 1) ? ya : yb;
-                if (d + 1 < DS && g + d + 1 < ng) perm(x[d + 1], nxt);
-                const uint64_t cnt = nb - (g + d) * G < (uint64_t)G ? nb - (g + d) * G : (uint64_t)G;
-#pragma unroll
-                for (int j = 0; j < G; ++j)
-                    if ((uint64_t)j < cnt) step(ul, uh, cur[j]);
-            }
-        }
-        step(ul, uh, 0);  // the last block's scramble
-        accv = ((uint64_t)uh << 32) | ul;
+        accv = scramble_chain(p.d_sums + i * nb * 8, nb, init[lane & 7], sec64(128 + 8 * (lane & 7), seed), lane);
     } else {
         // D blocks per round: their lane contributions and class sums are independent of the
         // accumulators, so all D reductions issue together and only the scrambles stay serial
@@ -557,7 +563,36 @@ __global__ __launch_bounds__(256) void xxh3_wave_kernel(const XxhParams p) {
         xxh3_long_wave<BITS, false>(p, i, ptr, n, seed, lane);
 }
 
+// Streaming XXH3 (aws_xxhash_update on device memory, abi_single.cpp): the stream's accumulators
+// acc_io[8] (device memory) absorb nb whole blocks whose sums xxh3_blocksum_kernel wrote to S; one
+// wave, every block scrambled.
+__global__ __launch_bounds__(64) void xxh3_stream_scramble_kernel(const uint64_t *S, uint64_t nb, uint64_t seed, uint64_t *acc_io) {
+    const int lane = threadIdx.x;
+    const int c8 = lane & 7;
+    const uint64_t accv = scramble_chain(S, nb, acc_io[c8], sec64(128 + 8 * c8, seed), lane);
+    if (lane < 8) acc_io[lane] = accv;
+}
+
 }  // namespace
+
+// Streaming XXH3: nblocks whole 1 KiB blocks at d_ptr into the accumulators at d_acc (device, 8 x u64):
+// the block sums over all CUs (d_sums: nblocks x 64 B), then the scramble chain in one wave.
+extern "C" int amdcrc_launch_xxh3_stream(const void *d_ptr, uint64_t nblocks, uint64_t seed, uint64_t *d_sums, uint64_t *d_acc,
+                                         void *stream) {
+    if (nblocks == 0) return 0;
+    XxhParams p{};
+    p.base = (uint64_t)(uintptr_t)d_ptr;
+    p.stride = 0;
+    p.len = nblocks * 1024 + 1;  // (len - 1) / 1024 == nblocks whole blocks
+    p.nbuf = 1;
+    p.seed_all = seed;
+    p.d_sums = d_sums;
+    int e = amdcrc_launch_xxh3_blocksum(&p, stream, nullptr);
+    if (e) return e;
+    hipLaunchKernelGGL(xxh3_stream_scramble_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint64_t *)d_sums, nblocks,
+                       seed, d_acc);
+    return (int)hipGetLastError();
+}
 
 // Phase 1 of the split path: one wave per kSumBlocks blocks of every buffer (p->d_sums set, p->len > 240)
 extern "C" int amdcrc_launch_xxh3_blocksum(const XxhParams *p, void *stream, void *start_event) {

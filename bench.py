@@ -84,21 +84,56 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_share():
-    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, set by the pool) capped by
-    the affinity mask; the model and the machine's logical CPU count are reported beside it."""
-    aff = len(os.sched_getaffinity(0))
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(aff, share) if share > 0 else aff
-    model = "unknown"
+def cpu_topology():
+    """Sockets and physical cores of the machine (/proc/cpuinfo), the cgroup CPU quota (cgroup v2
+    cpu.max, in cores, None when unlimited), the affinity mask and the pool's share (OMP_NUM_THREADS)."""
+    model, phys, cur = "unknown", set(), {}
     try:
         for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model == "unknown":
+                model = v
+            elif k in ("physical id", "core id"):
+                cur[k] = v
+            elif not k and cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
     except OSError:
         pass
-    return threads, model, aff
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    return {"cpu_model": model, "sockets": len({p for p, _ in phys}) or None, "physical_cores": len(phys) or None,
+            "logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota_cores": quota,
+            "pool_share_threads": share}
+
+
+def cpu_share():
+    """Threads for the CPU baseline: every physical core this process may use -- the
+    affinity mask, capped by the cgroup CPU quota and by the share the GPU pool gives one GPU
+    (OMP_NUM_THREADS, 16 on the pool's boxes; the pool's rules forbid using more).  The machine's
+    topology is reported beside it."""
+    topo = cpu_topology()
+    limits = [topo["affinity_cpus"]]
+    if topo["cgroup_cpu_quota_cores"]:
+        limits.append(max(1, int(topo["cgroup_cpu_quota_cores"])))
+    if topo["pool_share_threads"]:
+        limits.append(topo["pool_share_threads"])
+    if topo["physical_cores"]:
+        limits.append(topo["physical_cores"])
+    threads = min(limits)
+    limit = ("pool share (OMP_NUM_THREADS)" if topo["pool_share_threads"] == threads else
+             "cgroup CPU quota" if topo["cgroup_cpu_quota_cores"] and int(topo["cgroup_cpu_quota_cores"]) == threads else
+             "physical cores" if topo["physical_cores"] == threads else "affinity mask")
+    return threads, topo, limit
 
 
 def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
@@ -106,7 +141,7 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
     (numpy), 1 thread and the box's CPU share, median of `reps` reps of >= rep_seconds each."""
     from oracle import oracle  # checker and secondary figure only
 
-    threads, model, aff = cpu_share()
+    threads, topo, limit = cpu_share()
     base = host.ctypes.data
     ptrs = [base + i * L for i in range(count)]
     lens = [L] * count
@@ -136,11 +171,15 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
     if alg in oracle.ALG_INDEX:
         ov = rate(oracle.prepared_batch(alg, ptrs, lens, threads), count * L)
     third = third_party_rates(alg, host, count, L, threads, gpu_results, rate)
-    return {"value": round(v, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+    hashed = alg in ("xxh64", "xxh3_64", "xxh3_128")
+    busy = min(threads, count) if hashed else threads
+    return {"value": round(v, 2), "unit": "GiB/s", "cores": busy, "kind": "port",
             "impl": f"engine host path ({eng.cpu_tier()} tier)",
             "sample": f"{count} x {L >> 10} KiB ({count * L >> 20} MiB) copied to host, median of {reps} reps "
-                      f"of >= {rep_seconds:g} s, {threads} std::threads round-robin",
-            "single_thread_gibs": round(v1, 2), "cpu_model": model, "logical_cpus_visible": aff,
+                      f"of >= {rep_seconds:g} s, {threads} persistent threads claiming work items "
+                      + ("(one per buffer: a hash is one serial chain)" if hashed else
+                         "(buffers cut into >= 1 MiB pieces folded with Combine, so every thread is busy)"),
+            "threads_limit": limit, "single_thread_gibs": round(v1, 2), "topology": topo,
             "oracle_hw_tier_gibs": round(ov, 2) if ov is not None else None, "parity_with_gpu": parity,
             "third_party": third}
 
@@ -219,8 +258,17 @@ def widest(k, g):
     return max(b - a for a, b in zip(c, c[1:]))
 
 
-KERNEL = {"crc32": "crc32_stream_kernel", "crc32c": "crc32_stream_kernel", "crc64nvme": "crc64_stream4_kernel",
-          "xxh64": "xxh64_wave_kernel", "xxh3_64": "xxh3_blocksum_kernel + xxh3_wave_kernel"}
+def kernel_name(alg, nbuf, L):
+    """the dominant kernel (or route) of a uniform batch of nbuf x L bytes (engine.cpp dispatch)"""
+    if alg in ("crc32", "crc32c"):
+        return "crc32_stream_kernel"
+    if alg == "crc64nvme":
+        return "crc_lanes_kernel" if L <= 4096 and nbuf >= 65536 else "crc64_stream4_kernel"
+    if alg == "xxh64":
+        if nbuf <= 32 and L >= 1 << 20:
+            return "xxh64 host route (D2H slices + host threads, stream-ordered; DESIGN.md §3.4)"
+        return "xxh64_row_kernel" if nbuf <= 1024 else "xxh64_wave_kernel"
+    return "xxh3_blocksum_kernel + xxh3_wave_kernel"
 
 
 def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
@@ -288,7 +336,7 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
                        f"{alg.upper()}, device-resident, {nb} rotating batches, {per} per launch",
            "value": round(gibs, 2), "unit": "GiB/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
-           "roofline": roofline(per * step_bytes, kms, KERNEL.get(alg, alg))}
+           "roofline": roofline(per * step_bytes, kms, kernel_name(alg, nbuf, L))}
     if do_cpu:
         # the whole step's buffers (buffers round-robin over the threads, so a sample
         # of fewer buffers than threads would leave cores idle)
@@ -493,11 +541,43 @@ def main():
         elapsed = float(t.item())
     value = world * args.steps * step_bytes / max(elapsed, 1e-9) / 2**30
 
+    # the same K steps submitted one launch per batch (--coalesce 1), timed the same way: the rate a
+    # caller that never queues batches together sees (reported beside `value`, never as it)
+    one_per_launch = None
+    if G > 1 and args.steps > 0:
+        subs1 = prepare(args.steps, 1)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for bs, st in subs1:
+            bs.run(st)
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el1], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el1 = float(t.item())
+        one_per_launch = {"value": round(world * args.steps * step_bytes / max(el1, 1e-9) / 2**30, 2), "unit": "GiB/s",
+                          "ms_per_step": round(el1 / args.steps * 1e3, 4),
+                          "launch": f"one launch per batch, {args.steps} launches over {len(streams)} streams"}
+
+    # every rank checks a sample of its own results against the engine's host path (the first 64
+    # buffers of the first resident batch, which the timed region and the warm-up both wrote)
+    torch.cuda.synchronize()
+    nchk = min(count, 64)
+    hs = data[: nchk * L].cpu().numpy()
+    got = eng.as_unsigned(outs[0])[: nchk * per]
+    want = eng.cpu_batch(ALG[alg], [hs.ctypes.data + i * L for i in range(nchk)], [L] * nchk, threads=8)
+    if alg == "xxh3_128":
+        got = [(got[2 * i] << 64) | got[2 * i + 1] for i in range(nchk)]
+    rank_parity = got == want
+
     # dominant kernel: launches of G batches (the timed region's launch shape), then one-batch launches
     nt = max(1, args.timing_launches)
     gsz = widest(max(args.steps, 1), G)  # batches per launch in the timed region
     kms, kmed = time_launches(eng, lambda i, st: launch_group(i * gsz, i * gsz + gsz, st), streams[0], nt)
-    roof = roofline(gsz * step_bytes, kms, KERNEL.get(alg, alg))
+    roof = roofline(gsz * step_bytes, kms, kernel_name(alg, count, L))
     roof["kernel_ms_median"] = round(kmed, 5)
     roof["timing_launches"] = nt
     if not args.only_coalesced:
@@ -528,6 +608,16 @@ def main():
         roof["read_ceiling"] = {"kernel_ms": round(rcg_ms, 5), "frac": roofline(gsz * step_bytes, rcg_ms, "")["frac"],
                                 "scan_frac_of_ceiling": round(rcg_ms / kms, 4),
                                 "kernel": "read_ceiling_kernel: the scan's launch shape, 256-B non-temporal rows XOR-reduced"}
+
+    # per-rank record (device, kernel time, fraction, parity), gathered on rank 0
+    mine = {"rank": rank, "local_rank": local, "device": torch.cuda.get_device_name(dev), "device_index": dev.index,
+            "kernel_ms": roof["kernel_ms"], "frac": roof["frac"], "parity_sample_buffers": nchk, "parity": rank_parity}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+    parity_all = all(r["parity"] for r in ranks)
 
     cpu = e2e = None
     configs = {}
@@ -579,6 +669,9 @@ def main():
                        "streams": len(streams),
                        "parallelism": f"buffers sharded over {world} GPU(s), no collective"},
             "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
+            "parity": parity_all,
+            "ranks": ranks,
+            "one_batch_per_launch": one_per_launch,
             "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_pinned": e2e,

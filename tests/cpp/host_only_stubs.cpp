@@ -11,3 +11,4 @@ extern "C" int amdcrc_is_device_ptr(const void *) { return 0; }
 extern "C" int amdcrc_gpu_single(int, const void *, size_t, uint64_t, uint64_t *) { return -1; }
 extern "C" int amdcrc_copy_to_host(void *, const void *, size_t) { return -1; }
 extern "C" const char *aws_crt_amd_last_error(void) { return "no device (host-only build)"; }
+extern "C" int amdcrc_gpu_xxh3_blocks(const void *, uint64_t, uint64_t, uint64_t *) { return -1; }

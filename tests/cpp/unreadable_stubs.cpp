@@ -16,3 +16,4 @@ extern "C" int amdcrc_is_device_ptr(const void *p) { return unreadable(p) ? 1 : 
 extern "C" int amdcrc_gpu_single(int, const void *, size_t, uint64_t, uint64_t *) { return -1; }
 extern "C" int amdcrc_copy_to_host(void *, const void *, size_t) { return -1; }
 extern "C" const char *aws_crt_amd_last_error(void) { return "injected: device buffer unreadable"; }
+extern "C" int amdcrc_gpu_xxh3_blocks(const void *, uint64_t, uint64_t, uint64_t *) { return -1; }

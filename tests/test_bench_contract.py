@@ -36,3 +36,6 @@ def test_bench_json_line():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
+    # every rank checked a sample of its results against the host path (BASELINE multi-GPU runs)
+    assert d["parity"] is True and len(d["ranks"]) == 1 and d["ranks"][0]["parity"] is True
+    assert d["one_batch_per_launch"]["value"] > 0

@@ -133,3 +133,36 @@ def test_running_crc_and_combine(L):
             if off == len(data):
                 break
         assert off == len(data) and run == one == oracle.crc(alg, data)
+
+
+@pytest.mark.parametrize("alg", list(ALG))
+def test_threaded_batch_splits_long_buffers(L, alg):
+    """aws_crt_amd_cpu_batch with more threads than buffers: CRC buffers longer than a piece are
+    checksummed in pieces on every thread and folded with Combine (the first piece from the caller's
+    seed); hashes stay one item per buffer.  Few long buffers, ragged lengths, seeds, repeated calls
+    on the persistent pool, and the same call from several Python threads at once (the pool is
+    busy: those calls run on threads of their own)."""
+    import threading
+
+    rng = random.Random(0xBA7C + len(alg))
+    bufs = [rng.randbytes(n) for n in (3 << 20, (5 << 20) + 13, 17, 0, (1 << 20) + 1)]
+    seeds = [rng.getrandbits(64 if alg in ("crc64nvme", "xxh64", "xxh3_64", "xxh3_128") else 32) for _ in bufs]
+    want = [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)]
+    for _ in range(3):
+        assert cpu_batch(L, alg, bufs, seeds, threads=8) == want
+    assert cpu_batch(L, alg, bufs[:1], seeds[:1], threads=16) == want[:1]
+    errs = []
+
+    def worker():
+        try:
+            for _ in range(3):
+                assert cpu_batch(L, alg, bufs, seeds, threads=6) == want
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs

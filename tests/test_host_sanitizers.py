@@ -51,3 +51,17 @@ def test_unreadable_device_buffer_raises():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "[PASS] UnreadableDeviceBufferRaises" in r.stdout, r.stdout
     assert "is unreadable" in r.stderr  # the diagnostic line is printed too
+
+
+def test_device_stream_xxh3_split_logic():
+    """Streaming XXH3 over device chunks (abi_single.cpp, cpu::xxh3_update_source): with the engine
+    stand-ins of tests/cpp/devstream_stubs.cpp (a readable "device" buffer; the GPU block absorb
+    modelled on the host, then made to fail), every split of up to 4 MiB into host-sized and
+    >= 1 MiB device chunks, at every buffer-fill and stripe-position class, digests to the one-shot
+    XXH3-64 / XXH3-128 of the same bytes, with and without seed; failed absorbs fall back (counted)
+    to the same value.  ASan + UBSan build."""
+    _build("build/host_devstream")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
+    r = subprocess.run([os.path.join(CPP, "build", "host_devstream")], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[PASS] DeviceStreamXxh3Splits" in r.stdout and "[PASS] DeviceStreamXxh3Fallback" in r.stdout, r.stdout

@@ -118,3 +118,68 @@ def test_bounded_memory_1gib_stream(L):
     small = np.tile(chunk, 64)
     assert stream(L, "xxh64", [chunk] * 64, 7) == oracle.xxh64(small, 7)
     assert stream(L, "xxh3_64", [chunk] * 64, 7) == oracle.xxh3_64(small, 7)
+
+
+def _dev_stream(L, kind, base, sizes, seed):
+    """digest of the device bytes [base, base + sum(sizes)) streamed in `sizes` chunks"""
+    new, size = KINDS[kind]
+    h = getattr(L, new)(None, seed)
+    assert h
+    try:
+        off = 0
+        for s in sizes:
+            assert L.aws_xxhash_update(h, Cursor(s, base + off if s else None)) == 0
+            off += s
+        out = ctypes.create_string_buffer(size)
+        b = Buf(0, ctypes.cast(out, ctypes.c_void_p), size, None)
+        assert L.aws_xxhash_finalize(h, ctypes.byref(b)) == 0
+        return int.from_bytes(out.raw, "big")
+    finally:
+        L.aws_xxhash_destroy(h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["xxh3_64", "xxh3_128"])
+def test_device_stream_xxh3_every_edge(L, engine, kind):
+    """Streaming XXH3 on device memory (abi_single.cpp aws_xxhash_update): chunks of >= 1 MiB are
+    absorbed on the GPU (block sums over all CUs, then the scramble chain from the stream's
+    accumulators), the bytes around them through the host state.  The first device chunk starts after
+    host-sized prefixes at every XXH3 length-class edge (16, 128, 240 bytes, the 256-byte buffer, 1 KiB
+    blocks, stripe positions), device chunks follow each other at shifted stripe positions, and every
+    split digests to the oracle's one-shot value, with zero fallbacks (conftest)."""
+    import torch
+
+    M = 1 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xD5)
+    n_max = 3 * M + 4096
+    d = torch.randint(0, 256, (n_max,), dtype=torch.uint8, device="cuda", generator=g)
+    h = d.cpu().numpy()
+    prefixes = [0, 1, 16, 17, 128, 129, 240, 241, 255, 256, 257, 1000, 1023, 1024, 1025, 1087, 1088, 64 * 15 + 1, 4096]
+    for n in (3 * M + 4096, 2 * M + 777, M + 64 * 16 + 5):
+        for seed in (0, 0x9E3779B97F4A7C15):
+            want = oracle.checksum(kind, h[:n], seed)
+            for pre in prefixes:
+                for tail in ([], [M + 13], [3, M - 1, 17, M + 64 * 7 + 1]):
+                    sizes = [pre] + tail
+                    if sum(sizes) > n:
+                        continue
+                    sizes.append(n - sum(sizes))
+                    assert _dev_stream(L, kind, d.data_ptr(), sizes, seed) == want, (kind, n, seed, sizes)
+
+
+@pytest.mark.gpu
+def test_device_stream_xxh3_large_chunk(L, engine):
+    """One 300 MiB device chunk (more than one 256 MiB absorb pass) after an unaligned 5-byte prefix,
+    and 64 MiB chunks back to back, against the oracle's one-shot XXH3-64 / XXH3-128."""
+    import torch
+
+    n = 300 << 20
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xD6)
+    d = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    h = d.cpu().numpy()
+    for kind in ("xxh3_64", "xxh3_128"):
+        want = oracle.checksum(kind, h, 7)
+        assert _dev_stream(L, kind, d.data_ptr(), [5, n - 5], 7) == want
+        assert _dev_stream(L, kind, d.data_ptr(), [64 << 20] * 4 + [n - (256 << 20)], 7) == want
