@@ -363,21 +363,29 @@ void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64
         return;
     }
     std::vector<uint64_t> pv(crc ? nitems : 0);
+    // items are claimed in runs (one shared counter touched by every thread of a two-socket host
+    // costs more than checksumming a short buffer): about 16 claims per thread, at least one item
+    const size_t run = std::max<size_t>(1, nitems / (16 * nt));
     std::atomic<size_t> next{0};
     auto work = [&](size_t) {
         for (;;) {
-            const size_t it = next.fetch_add(1, std::memory_order_relaxed);
-            if (it >= nitems) return;
-            const size_t i = (size_t)(std::upper_bound(first.begin(), first.end(), it) - first.begin()) - 1;
-            if (!crc || first[i + 1] - first[i] == 1) {
-                one(i);
-                if (crc) pv[it] = out[i];
-                continue;
+            const size_t it0 = next.fetch_add(run, std::memory_order_relaxed);
+            if (it0 >= nitems) return;
+            const size_t it1 = std::min(nitems, it0 + run);
+            size_t i = (size_t)(std::upper_bound(first.begin(), first.end(), it0) - first.begin()) - 1;
+            for (size_t it = it0; it < it1; ++it) {
+                while (first[i + 1] <= it) ++i;
+                if (!crc || first[i + 1] - first[i] == 1) {
+                    one(i);
+                    if (crc) pv[it] = out[i];
+                    continue;
+                }
+                const size_t k = it - first[i], off = k * piece, n = std::min(piece, lens[i] - off);
+                const uint64_t s = k == 0 && seeds ? seeds[i] : 0;
+                pv[it] = alg == 0   ? crc32(ptrs[i] + off, n, (uint32_t)s)
+                         : alg == 1 ? crc32c(ptrs[i] + off, n, (uint32_t)s)
+                                    : crc64nvme(ptrs[i] + off, n, s);
             }
-            const size_t k = it - first[i], off = k * piece, n = std::min(piece, lens[i] - off);
-            const uint64_t s = k == 0 && seeds ? seeds[i] : 0;
-            pv[it] = alg == 0 ? crc32(ptrs[i] + off, n, (uint32_t)s) : alg == 1 ? crc32c(ptrs[i] + off, n, (uint32_t)s)
-                                                                           : crc64nvme(ptrs[i] + off, n, s);
         }
     };
     const size_t nrun = std::min(nt, nitems);

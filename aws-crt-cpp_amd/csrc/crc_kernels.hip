@@ -809,7 +809,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // uniform batches): the workgroup's even share [wb0, wb1) is split into one static tile per wave
     // and a pool the waves claim from an LDS counter as they run dry, so a wave the memory system
     // serves late scans less of its workgroup's share.
-    const bool dyn = !LIST && p.nstatic != 0;
+    const bool dyn = p.nstatic != 0;  // strided batches, and lists when the host asks (engine.cpp list_impl)
     uint64_t t0, t1, pool_base = 0, pool_size = 0;
     if (dyn) {
         const uint64_t wb0 = (uint64_t)blockIdx.x * p.ntiles / gridDim.x, wb1 = ((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x;
@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void stream_issue(W16Group &g, uint32_t voff, uint64_
     }
 }
 #define AMDCRC_R4V(g) "+v"(g.w[0]), "+v"(g.w[1]), "+v"(g.w[2]), "+v"(g.w[3])
-__device__ __forceinline__ void ring_drain(W16Group &a, W16Group &b, W16Group &c) {
+[[maybe_unused]] __device__ __forceinline__ void ring_drain(W16Group &a, W16Group &b, W16Group &c) {
     asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R4V(a)::"memory");
     asm volatile("" : AMDCRC_R4V(b));
     asm volatile("" : AMDCRC_R4V(c));
@@ -1533,11 +1533,11 @@ constexpr uint32_t kB64TabBytes = 131072;
 constexpr uint32_t kB64T0Off = kB64TabBytes;        // plain byte table, 256 x u64 (head / tail)
 constexpr uint32_t kB64Lds = kB64T0Off + 2048;
 
-template <uint64_t POLY>
+template <uint64_t POLY, uint32_t ROW = kB64Row>
 struct Braid64Basis {
-    uint64_t b[9][8];  // b[t][i] = T'_t[1 << i] (t < 8); b[8][i] = T_0[1 << i]
+    uint64_t b[9][8];  // b[t][i] = T'_t[1 << i] (t < 8) for rows of ROW bytes; b[8][i] = T_0[1 << i]
     constexpr Braid64Basis() : b() {
-        const uint64_t skip = gf2_xpow8n(kB64Row - 8, POLY, 64);
+        const uint64_t skip = gf2_xpow8n(ROW - 8, POLY, 64);
         for (int i = 0; i < 8; ++i) {
             for (int t = 0; t < 8; ++t) b[t][i] = gf2_mulmod(gf2_table_entry(1u << i, t, POLY), skip, POLY, 64);
             b[8][i] = gf2_table_entry(1u << i, 0, POLY);
@@ -1545,26 +1545,26 @@ struct Braid64Basis {
     }
 };
 
-template <uint64_t POLY, int K>
+template <uint64_t POLY, int K, uint32_t ROW = kB64Row>
 __device__ __forceinline__ uint64_t basis64(uint32_t e) {
-    constexpr Braid64Basis<POLY> B{};
+    constexpr Braid64Basis<POLY, ROW> B{};
     uint64_t v = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0ull;
     return v;
 }
 
-template <uint64_t POLY>
+template <uint64_t POLY, uint32_t ROW = kB64Row>
 __device__ __forceinline__ uint64_t basis64_rt(uint32_t t, uint32_t e) {  // t wave-uniform
     switch (t) {
-        case 0: return basis64<POLY, 0>(e);
-        case 1: return basis64<POLY, 1>(e);
-        case 2: return basis64<POLY, 2>(e);
-        case 3: return basis64<POLY, 3>(e);
-        case 4: return basis64<POLY, 4>(e);
-        case 5: return basis64<POLY, 5>(e);
-        case 6: return basis64<POLY, 6>(e);
-        default: return basis64<POLY, 7>(e);
+        case 0: return basis64<POLY, 0, ROW>(e);
+        case 1: return basis64<POLY, 1, ROW>(e);
+        case 2: return basis64<POLY, 2, ROW>(e);
+        case 3: return basis64<POLY, 3, ROW>(e);
+        case 4: return basis64<POLY, 4, ROW>(e);
+        case 5: return basis64<POLY, 5, ROW>(e);
+        case 6: return basis64<POLY, 6, ROW>(e);
+        default: return basis64<POLY, 7, ROW>(e);
     }
 }
 
@@ -1625,13 +1625,22 @@ struct Braid64 {
     __device__ __forceinline__ uint64_t step_x(uint64_t a, uint64_t wn) const {
         const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
         // COPIES = 4: slots 0..3 read dword ma, slots 4..7 dword mb (per lane half, see the layout)
+#ifdef AMDCRC_XP64_NOBFI  // experiment builds only: the byte sources without the per-lane dword select
+        const uint32_t ma = lo, mb = hi;
+#else
         const uint32_t ma = COPIES == 8 ? lo : (lo & lowmask) | (hi & ~lowmask);
         const uint32_t mb = COPIES == 8 ? hi : (hi & lowmask) | (lo & ~lowmask);
+#endif
         uint64_t v[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+#ifdef AMDCRC_XP64_NOLDS  // experiment builds only: the address perms without the table reads
+            v[k] = __builtin_amdgcn_perm(cst[k], ma, sel[k]);
+            v[4 + k] = (uint64_t)__builtin_amdgcn_perm(csth[k], mb, sel[k]) << 32;
+#else
             v[k] = lds64(L, __builtin_amdgcn_perm(cst[k], ma, sel[k]));
             v[4 + k] = lds64(L, __builtin_amdgcn_perm(csth[k], mb, sel[k]));
+#endif
         }
         uint32_t rl = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]), (uint32_t)v[3], (uint32_t)v[4]);
         rl = xor3(xor3(rl, (uint32_t)v[5], (uint32_t)v[6]), (uint32_t)v[7], (uint32_t)wn);
@@ -1821,7 +1830,7 @@ __device__ __forceinline__ void b64_build_tables(char *lds) {
 // the 4-copy layout (Braid64<POLY, 4>) from 512 threads: thread i fills the table of byte
 // t = i >> 6 of a (T'_(7-t), wave-uniform) for entries (i & 63) + 64 n, n < 4, two 16-byte stores
 // (4 copies) each; then T0
-template <uint64_t POLY>
+template <uint64_t POLY, uint32_t ROW = kB64Row>
 __device__ __forceinline__ void b64x4_build_tables(char *lds) {
     const uint32_t i = threadIdx.x;
     if (i >= 512) return;  // eight waves build the eight tables
@@ -1829,7 +1838,7 @@ __device__ __forceinline__ void b64x4_build_tables(char *lds) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const uint32_t e = (i & 63u) + 64u * n;
-        const uint64_t v = basis64_rt<POLY>(7u - t, e);
+        const uint64_t v = basis64_rt<POLY, ROW>(7u - t, e);
         const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
         char *row = lds + (e << 8) + (t << 5);
         *(v4u *)(row + (((i >> 2) & 1u) << 4)) = vv;
@@ -2009,7 +2018,11 @@ __device__ __forceinline__ void stream64_issue(B64Group &g, uint32_t voff, uint6
 // per buffer; the buffer's last group finalises.
 template <class B>
 __device__ __forceinline__ void stream64_finish(const ScanParams &p, const Tile &d, uint64_t u, const B &eng, int lane) {
+#ifdef AMDCRC_XP64_NOFINISH  // experiment builds only: tiles end without the lane shares' product and reduction
+    const uint64_t r = __builtin_amdgcn_readfirstlane((uint32_t)u);
+#else
     const uint64_t r = wave_xor64_s(eng.mulK(u));
+#endif
     if (d.T == 1) {
         if (lane == 0) finalize<false>(p, d.b, r, eng);
         return;
@@ -2142,6 +2155,158 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// W = 64 scan of many short uniform buffers (the C4 per-GPU shard: 131,072 x 8 KiB), 16 lanes per
+// buffer.  A wave scans four buffers at once, one per 16-lane row: lane t of row r owns the 8-byte
+// word at 8t of every 128-byte row of buffer 4s + r, so the braid step's tables fold in the skip over
+// the row's other 15 words (T'_t[e] = e * x^(8(t+1)) * x^(8*120)), and lane t's share of its buffer's
+// register is u * x^(-64 t).  One tile finish -- the nibble-table product (31 LDS reads) and a 16-lane
+// reduction -- then covers four buffers instead of one: at 8 KiB per buffer the per-buffer finish of
+// crc64_stream4_kernel took an eighth of the launch (profiles/r03/crc64_xp).  The table layout (4
+// copies, conflict-free for any data) and the three-slot ring are crc64_stream4_kernel's; each lane
+// streams its own buffer, so the ring's addresses are per lane.
+constexpr uint32_t kR16Row = 128;                           // bytes per buffer row (16 lanes x 8 B)
+constexpr uint32_t kR16Group = kR16Row * kB64RowsPerGroup;  // 1 KiB of each buffer per ring slot
+constexpr int kR16Block = 512;
+
+template <int R>
+__device__ __forceinline__ uint64_t gld_r16(uint64_t a) {
+    return __builtin_nontemporal_load((gu64 *)(a + R * kR16Row));
+}
+template <int R>
+__device__ __forceinline__ void r16_issue(B64Group &g, uint64_t a) {
+    if constexpr (R < kB64RowsPerGroup) {
+        g.w[R] = gld_r16<R>(a);
+        r16_issue<R + 1>(g, a);
+    }
+}
+template <int R, class B>
+__device__ __forceinline__ uint64_t r16_rows(uint64_t x, B64Group &cur, B64Group &nxt, uint64_t anext, const B &eng) {
+    if constexpr (R < kB64RowsPerGroup) {
+        nxt.w[R] = gld_r16<R>(anext);
+        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return r16_rows<R + 1>(x, cur, nxt, anext, eng);
+    } else {
+        return eng.step(x);
+    }
+}
+// XOR over the 16 lanes of each row, left in every lane of the row
+__device__ __forceinline__ uint32_t row16_xor(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return v;
+}
+
+template <uint64_t POLY>
+__global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanParams p) {
+    using B = Braid64<POLY, 4>;
+    __shared__ __attribute__((aligned(16))) char lds[kB64x4Lds];
+    constexpr int kWaves = kR16Block / 64;
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t row = (uint32_t)lane >> 4, t = (uint32_t)lane & 15u;
+    const uint64_t nsets = (p.nbuf + 3) / 4;
+    const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6));
+    const uint64_t s0 = rfl64(gw * nsets / nw), s1 = rfl64((gw + 1) * nsets / nw);
+    const Edges e0 = buffer_edges<false>(p, 0);
+    const uint64_t hoff = e0.headend - p.base, ml = e0.tail - e0.headend;
+    const uint32_t G = (uint32_t)(ml / kR16Group);  // groups per buffer (the host checks ml % kR16Group == 0)
+    const uint32_t nq = (uint32_t)((s1 - s0) * G);  // groups of this wave
+    const bool work = s0 < s1;
+    const uint64_t dummy = (uint64_t)p.d_kvals + 8u * t;  // placeholder rows: the 16 KiB constant block
+    // this lane's buffer of set s: main-region address + 8 t (rows past the batch read the constants)
+    auto lane_base = [&](uint64_t s) -> uint64_t {
+        uint64_t a[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t b = 4 * s + (uint64_t)r;
+            if (b < p.nbuf) {
+                const BatchPos bp = batch_pos(p, b);
+                a[r] = karg64(p.bbase, bp.j) + bp.i * p.stride + hoff + 8u * t;
+            } else {
+                a[r] = dummy;
+            }
+        }
+        return row == 0 ? a[0] : row == 1 ? a[1] : row == 2 ? a[2] : a[3];
+    };
+    uint32_t fq = 0, fg = 0;  // prefetch cursor: groups issued, group within the set
+    uint64_t fs = s0;
+    uint64_t fbase = work ? lane_base(fs) : dummy;
+    auto f_addr = [&]() -> uint64_t { return fq < nq ? fbase + (uint64_t)fg * kR16Group : dummy; };
+    auto f_next = [&]() {
+        ++fq;
+        if (++fg == G) {
+            fg = 0;
+            if (++fs < s1) fbase = lane_base(fs);
+        }
+    };
+    const uint64_t kl = *(gu64 *)(p.d_kvals + t);  // K_t = x^(-64 t)
+    B64Group ra, rb, rc;
+    if (work) {
+        r16_issue<0>(ra, f_addr());
+        f_next();
+    }
+    b64x4_build_tables<POLY, kR16Row>(lds);
+    b64x4_build_nib<POLY>(lds, kl);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    if (!work) return;
+    r16_issue<0>(rb, f_addr());
+    f_next();
+
+    uint64_t s = s0;  // scan cursor: set s, group g
+    uint32_t g = 0, q = 0;
+    uint64_t u = 0;
+    auto step = [&](B64Group &cur, B64Group &nxt) {
+        if (g == 0) {
+            // head states of the set's four buffers (wave-uniform), each entering its row's lane 0
+            uint64_t h[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = 4 * s + (uint64_t)r < p.nbuf ? head_state<false>(p, 4 * s + r, eng) : 0ull;
+            const uint64_t hr = row == 0 ? h[0] : row == 1 ? h[1] : row == 2 ? h[2] : h[3];
+            u = t == 0 ? hr : 0ull;
+        }
+        const uint64_t an = f_addr();
+        f_next();
+        u = r16_rows<0>(u, cur, nxt, an, eng);
+        ++q;
+        if (++g == G) {
+            g = 0;
+            const uint64_t v = eng.mulK(u);
+            const uint32_t lo = row16_xor((uint32_t)v), hi = row16_xor((uint32_t)(v >> 32));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t b = 4 * s + (uint64_t)r;
+                const uint64_t fin = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
+                if (b < p.nbuf && lane == 0) finalize<false>(p, b, fin, eng);
+            }
+            ++s;
+        }
+    };
+    for (;;) {
+        step(ra, rc);
+        if (q >= nq) break;
+        step(rb, ra);
+        if (q >= nq) break;
+        step(rc, rb);
+        if (q >= nq) break;
+    }
+    // the trailing placeholder rows: their registers stay live until the loads have landed
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]), "+v"(ra.w[5]),
+                 "+v"(ra.w[6]), "+v"(ra.w[7])::"memory");
+    asm volatile("" : "+v"(rb.w[0]), "+v"(rb.w[1]), "+v"(rb.w[2]), "+v"(rb.w[3]), "+v"(rb.w[4]), "+v"(rb.w[5]), "+v"(rb.w[6]),
+                 "+v"(rb.w[7]));
+    asm volatile("" : "+v"(rc.w[0]), "+v"(rc.w[1]), "+v"(rc.w[2]), "+v"(rc.w[3]), "+v"(rc.w[4]), "+v"(rc.w[5]), "+v"(rc.w[6]),
+                 "+v"(rc.w[7]));
+}
 
 // ------------------------------------------------------------------------------------------
 // xxHash64 (aws_xxhash64_compute, XXHash.cpp:17).  The published algorithm is four serial chains
@@ -2640,9 +2805,12 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
     const bool list = p->list_mode != 0;
     switch (alg) {
         case ALG_CRC32:
+#if AMDCRC_STREAM_W16
             if (p->stream == 2 && !list)
                 launch(crc32_stream_kernel<kPoly32, 16>, nblocks, kW16Block, s, p, ev);
-            else if (p->stream && !list)
+            else
+#endif
+            if (p->stream && !list)
                 launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
@@ -2650,9 +2818,12 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC32C:
+#if AMDCRC_STREAM_W16
             if (p->stream == 2 && !list)
                 launch(crc32_stream_kernel<kPoly32C, 16>, nblocks, kW16Block, s, p, ev);
-            else if (p->stream && !list)
+            else
+#endif
+            if (p->stream && !list)
                 launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
@@ -2660,7 +2831,9 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc32_braid_kernel<kPoly32C, false>, nblocks, kBraidBlock, s, p, ev);
             break;
         case ALG_CRC64NVME:
-            if (p->stream && !list)  // 4-copy tables
+            if (p->stream == 3 && !list)  // many short buffers: 16 lanes per buffer
+                launch(crc64_rows16_kernel<kPoly64Nvme>, nblocks, kR16Block, s, p, ev);
+            else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);

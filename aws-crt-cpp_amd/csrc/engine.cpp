@@ -333,12 +333,17 @@ inline bool is_hash(int alg) { return alg >= AWS_CRT_AMD_XXH64; }
 #define AMDCRC_SMALL_BATCH (256ull << 20)
 #endif
 constexpr uint64_t kSmallBatchBytes = AMDCRC_SMALL_BATCH;
-// W=32 streaming scans of at least kSmallBatchBytes: the 16-byte-word kernel (crc_kernels.hip
-// Braid32W16); 0 keeps the 8-byte-word kernel there too
-#ifndef AMDCRC_STREAM_W16  // compile-time only (A/B builds)
-#define AMDCRC_STREAM_W16 1
-#endif
+// W=32 streaming scans of at least kSmallBatchBytes on 16-byte words (crc_kernels.hip Braid32W16,
+// AMDCRC_STREAM_W16 in engine.h): measured 1-5 % slower than the 8-byte-word kernel, so off
 constexpr bool kStreamW16 = AMDCRC_STREAM_W16 != 0;
+// Strided CRC64NVME batches of many short buffers (main regions of whole 1 KiB groups, at most
+// kRows16MaxBytes, at least a set of four buffers per wave slot) take crc64_rows16_kernel
+#ifndef AMDCRC_ROWS16  // compile-time only (A/B builds)
+#define AMDCRC_ROWS16 1
+#endif
+constexpr bool kRows16 = AMDCRC_ROWS16 != 0;
+constexpr uint64_t kRows16MinBuffers = 4 * 4096;
+constexpr uint64_t kRows16MaxBytes = 256u << 10;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
 #ifndef AMDCRC_LANE_LIST_MAX  // compile-time only (launch-shape sweeps build a variant; no run-time switch)
 #define AMDCRC_LANE_LIST_MAX 4096
@@ -403,7 +408,8 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         p.d_claim = w->claim;
     }
     const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
-    const uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
+    uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
+    if (p.stream == 3) blocks = std::min<uint64_t>((p.nbuf + 4 * 8 - 1) / (4 * 8), 2 * (uint64_t)d->cus);  // 4 buffers per wave
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
@@ -422,38 +428,49 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
                  hipStream_t s);
 
 // ---- XXH64 over few long device buffers: the stream-ordered host route.
-// XXH64 is one serial chain per buffer (four lanes whose every round depends on the last): a
-// dependent 64-bit multiply-add-rotate per 32-byte stripe, about 41 cycles per round on a gfx950
-// SIMD (1.7 GiB/s per buffer) against about 1.3 ns on one host core.  A batch of fewer buffers than
-// kX64HostMaxBuffers therefore goes D2H in 64 MiB slices (one hipMemcpy2DAsync per slice: a row of
-// every buffer) and is hashed by host threads, one buffer each, in stream-ordered host functions;
-// the results go back H2D on the same stream, so the call keeps the batch ABI's asynchronous,
-// stream-ordered contract.  Larger batches keep the GPU kernels.
+// XXH64 is one serial chain per buffer (four lanes whose every round depends on the last): on a
+// gfx950 SIMD a round is issue-bound at about 41 cycles (tools/chainbench: 31.5 for the six chain
+// instructions, 9 more for the two DPP moves that bring the next stripe's product in), 1.7 GiB/s
+// per buffer, against about 1.3 ns per round on one host core.  A batch of at most kX64HostMaxBuffers
+// long buffers therefore goes to the host: slices of every buffer (one hipMemcpy2DAsync per slice)
+// are copied D2H on the device's copy stream into two pinned halves, alternately, while the caller's
+// stream runs host functions that hash the previous slice with one thread per buffer; the results go
+// back H2D on the caller's stream.  The call keeps the batch ABI's asynchronous, stream-ordered
+// contract (the copies wait for the caller's stream; later work on it waits for the results).
 #ifndef AMDCRC_X64_HOST_MAX  // compile-time only (A/B builds: 0 keeps every XXH64 batch on the GPU kernels)
-#define AMDCRC_X64_HOST_MAX 32
+#define AMDCRC_X64_HOST_MAX 16
 #endif
 constexpr size_t kX64HostMaxBuffers = AMDCRC_X64_HOST_MAX;
 constexpr size_t kX64HostMinBytes = 1u << 20;
-constexpr size_t kX64StageBytes = 64u << 20;
-constexpr size_t kX64StageExtra = 16 * 64;  // seeds, then results (at most 64 buffers)
+constexpr size_t kX64Half = 32u << 20;             // one pinned half: a slice of every buffer
+constexpr size_t kX64StageExtra = 16 * 64;          // seeds, then results (at most 64 buffers)
 static_assert(kX64HostMaxBuffers <= 64, "staging extra");
 
+// staging of one queued job: two pinned halves (+ seeds / results) and the events that order them;
+// reused by later jobs (returned by the job's last host function, which may make no HIP call)
+struct X64Stage {
+    int dev = -1;
+    uint8_t *pin = nullptr;  // 2 * kX64Half, then kX64StageExtra
+    hipEvent_t start = nullptr, copied[2] = {nullptr, nullptr}, hashed[2] = {nullptr, nullptr};
+};
 std::mutex g_x64_mu;
-std::vector<void *> g_x64_free;  // pinned staging buffers (portable) not owned by a queued job
+std::vector<X64Stage *> g_x64_free;
+std::map<int, hipStream_t> g_x64_copy;  // per device: the D2H copy stream of the route
 
 struct X64Job;
 struct X64Chunk {
     X64Job *job;
+    const uint8_t *rows;
     size_t rowbytes;
     bool first, last;
 };
 struct X64Job {
+    X64Stage *st = nullptr;
     size_t count = 0;
-    uint8_t *pin = nullptr;  // kX64StageBytes of rows, then kX64StageExtra
     uint64_t *h_seed = nullptr, *h_res = nullptr;
     bool seeds = false;
     uint64_t seed_all = 0;
-    std::vector<cpu::Xxh64State> st;
+    std::vector<cpu::Xxh64State> xs;
     std::vector<X64Chunk> chunks;
 };
 
@@ -461,9 +478,9 @@ void x64_chunk_fn(void *u) noexcept {
     const X64Chunk *c = (const X64Chunk *)u;
     X64Job *j = c->job;
     auto row = [&](size_t i) {
-        if (c->first) cpu::xxh64_reset(&j->st[i], j->seeds ? j->h_seed[i] : j->seed_all);
-        cpu::xxh64_update(&j->st[i], j->pin + i * c->rowbytes, c->rowbytes);
-        if (c->last) j->h_res[i] = cpu::xxh64_digest(&j->st[i]);
+        if (c->first) cpu::xxh64_reset(&j->xs[i], j->seeds ? j->h_seed[i] : j->seed_all);
+        cpu::xxh64_update(&j->xs[i], c->rows + i * c->rowbytes, c->rowbytes);
+        if (c->last) j->h_res[i] = cpu::xxh64_digest(&j->xs[i]);
     };
     // one host thread per buffer (the calling runtime thread takes buffer 0)
     std::vector<std::thread> ts;
@@ -481,47 +498,69 @@ void x64_free_fn(void *u) noexcept {
     {
         std::lock_guard<std::mutex> g(g_x64_mu);
         try {
-            g_x64_free.push_back(j->pin);
+            g_x64_free.push_back(j->st);
         } catch (...) {
-            (void)0;  // the staging buffer is dropped (leaked) rather than freed from a callback
+            (void)0;  // the stage is dropped (leaked) rather than freed from a callback
         }
     }
     delete j;
 }
 
-int xxh64_host_route(uint64_t base, size_t stride, size_t len, size_t count, const void *d_seeds, uint64_t seed_all,
+int x64_take_stage(int dev, X64Stage **out, hipStream_t *copy) {
+    std::lock_guard<std::mutex> g(g_x64_mu);
+    hipStream_t &cs = g_x64_copy[dev];
+    if (!cs) HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    *copy = cs;
+    for (size_t i = 0; i < g_x64_free.size(); ++i)
+        if (g_x64_free[i]->dev == dev) {
+            *out = g_x64_free[i];
+            g_x64_free.erase(g_x64_free.begin() + (long)i);
+            return 0;
+        }
+    std::unique_ptr<X64Stage> st(new X64Stage);
+    st->dev = dev;
+    HIP_TRY(hipHostMalloc((void **)&st->pin, 2 * kX64Half + kX64StageExtra, hipHostMallocPortable));
+    HIP_TRY(hipEventCreateWithFlags(&st->start, hipEventDisableTiming));
+    for (int h = 0; h < 2; ++h) {
+        HIP_TRY(hipEventCreateWithFlags(&st->copied[h], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&st->hashed[h], hipEventDisableTiming));
+    }
+    *out = st.release();
+    return 0;
+}
+
+int xxh64_host_route(int dev, uint64_t base, size_t stride, size_t len, size_t count, const void *d_seeds, uint64_t seed_all,
                      void *d_out, hipStream_t s) {
     std::unique_ptr<X64Job> j(new X64Job);
-    {
-        std::lock_guard<std::mutex> g(g_x64_mu);
-        if (!g_x64_free.empty()) {
-            j->pin = (uint8_t *)g_x64_free.back();
-            g_x64_free.pop_back();
-        }
-    }
-    if (!j->pin) HIP_TRY(hipHostMalloc((void **)&j->pin, kX64StageBytes + kX64StageExtra, hipHostMallocPortable));
-    auto give_back = [&]() {
-        std::lock_guard<std::mutex> g(g_x64_mu);
-        g_x64_free.push_back(j->pin);
-    };
+    hipStream_t cs;
+    int rc = x64_take_stage(dev, &j->st, &cs);
+    if (rc) return rc;
+    X64Stage *st = j->st;
     j->count = count;
-    j->h_seed = (uint64_t *)(j->pin + kX64StageBytes);
+    j->h_seed = (uint64_t *)(st->pin + 2 * kX64Half);
     j->h_res = j->h_seed + 64;
     j->seeds = d_seeds != nullptr;
     j->seed_all = seed_all;
-    j->st.resize(count);
-    const size_t slice = std::min<size_t>(len, (kX64StageBytes / count) & ~(size_t)63);
-    for (size_t off = 0; off < len; off += slice)
-        j->chunks.push_back({j.get(), std::min(slice, len - off), off == 0, off + slice >= len});
+    j->xs.resize(count);
+    const size_t slice = std::min<size_t>(len, (kX64Half / count) & ~(size_t)63);
+    for (size_t off = 0, k = 0; off < len; off += slice, ++k)
+        j->chunks.push_back({j.get(), st->pin + (k & 1) * kX64Half, std::min(slice, len - off), off == 0, off + slice >= len});
     hipError_t e = hipSuccess;
     if (g_time_events[0]) e = hipEventRecord((hipEvent_t)g_time_events[0], s);
     if (!e && d_seeds) e = hipMemcpyAsync(j->h_seed, d_seeds, 8 * count, hipMemcpyDefault, s);
-    size_t off = 0, queued = 0;
-    for (; !e && queued < j->chunks.size(); ++queued) {
-        X64Chunk &c = j->chunks[queued];
-        e = hipMemcpy2DAsync(j->pin, c.rowbytes, (const void *)(uintptr_t)(base + off), stride, c.rowbytes, count,
-                             hipMemcpyDeviceToHost, s);
+    if (!e) e = hipEventRecord(st->start, s);  // the copies read what the caller's stream produced
+    if (!e) e = hipStreamWaitEvent(cs, st->start, 0);
+    size_t off = 0;
+    for (size_t k = 0; !e && k < j->chunks.size(); ++k) {
+        X64Chunk &c = j->chunks[k];
+        const int h = (int)(k & 1);
+        if (k >= 2) e = hipStreamWaitEvent(cs, st->hashed[h], 0);  // the half's previous slice is hashed
+        if (!e) e = hipMemcpy2DAsync((void *)c.rows, c.rowbytes, (const void *)(uintptr_t)(base + off), stride, c.rowbytes, count,
+                                     hipMemcpyDeviceToHost, cs);
+        if (!e) e = hipEventRecord(st->copied[h], cs);
+        if (!e) e = hipStreamWaitEvent(s, st->copied[h], 0);
         if (!e) e = hipLaunchHostFunc(s, x64_chunk_fn, &c);
+        if (!e) e = hipEventRecord(st->hashed[h], s);
         off += c.rowbytes;
     }
     if (!e) e = hipMemcpyAsync(d_out, j->h_res, 8 * count, hipMemcpyDefault, s);  // d_out may be pinned host memory (the single path)
@@ -530,8 +569,12 @@ int xxh64_host_route(uint64_t base, size_t stride, size_t len, size_t count, con
     if (!e) e = hipLaunchHostFunc(s, x64_free_fn, j.get());
     if (e) {
         // whatever was queued refers to the job: let it drain, then release the job here
+        (void)hipStreamSynchronize(cs);
         (void)hipStreamSynchronize(s);
-        give_back();
+        {
+            std::lock_guard<std::mutex> g(g_x64_mu);
+            g_x64_free.push_back(st);
+        }
         return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh64 host route: ") + hipGetErrorString(e));
     }
     j.release();  // x64_free_fn owns it now
@@ -547,7 +590,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         return scan_batches(d, alg, &b, 1, stride, len, count, seed_all, s);
     }
     if (alg == AWS_CRT_AMD_XXH64 && count <= kX64HostMaxBuffers && len >= kX64HostMinBytes && !capturing(s))
-        return xxh64_host_route(base, stride, len, count, d_seeds, seed_all, d_out, s);
+        return xxh64_host_route(d->id, base, stride, len, count, d_seeds, seed_all, d_out, s);
     {
         XxhParams xp{};
         xp.base = base;
@@ -642,6 +685,19 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     p.ntiles = T * count;
     p.seed_all = seed_all;
     p.stream = stream && ml % tile == 0 ? 1u : 0u;
+    // many short CRC64NVME buffers whose main regions are whole 1 KiB groups: 16 lanes per buffer
+    // (crc64_rows16_kernel), one tile finish per four buffers
+    if (!w32 && kRows16 && count >= kRows16MinBuffers && ml >= 1024 && ml <= kRows16MaxBytes && ml % 1024 == 0) {
+        p.stream = 3;
+        p.base = base;
+        p.stride = stride;
+        p.len = len;
+        p.tiles_per_buf = 1;
+        p.nbuf = count;
+        p.ntiles = count;
+        p.seed_all = seed_all;
+        return launch_scan(d, alg, p, count, 1, ml * count, s);
+    }
     // large W=32 launches: 16-byte lane words in one 1024-thread workgroup per CU (the same waves per
     // CU as two 512-thread workgroups; the tiles hold 4 KiB groups either way)
     if (p.stream && w32 && kStreamW16 && !small) p.stream = 2;
@@ -727,6 +783,9 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         std::vector<uint64_t> sorted(mains);
         std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
         seg = choose_seg(d, total, sorted[count / 2]);
+#ifdef AMDCRC_XP_LIST_SEG_DIV  // experiment builds only: smaller list tiles (balance vs finishes)
+        seg = std::max<uint32_t>(kGroupBytes, seg / AMDCRC_XP_LIST_SEG_DIV);
+#endif
         tile = (uint64_t)seg * kWave;
     }
     // descriptor block: ptrs[count] lens[count] prefix[count+1] wavebuf[nwaves]
@@ -740,6 +799,13 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     const uint64_t ntiles = prefix[count];
     const ScanGeometry geo = scan_geometry(d, xxh ? ALG_CRC32 : alg, ntiles, total);
     const uint64_t nw = std::max<uint64_t>(geo.blocks, 1) * geo.waves_per_block;
+    // W=32 lists with at least two tiles per wave slot: one static tile per wave, the rest of each
+    // workgroup's share claimed from its LDS pool (the kernel's dyn mode), so waves whose tiles are
+    // mostly front pad take more tiles
+    uint64_t nstatic = 0;
+#ifdef AMDCRC_XP_LIST_POOL  // experiment builds only
+    if (!xxh && width_of(alg) == 32 && ntiles >= 2 * nw) nstatic = nw;
+#endif
     const size_t words = count * 2 + (count + 1) + nw;
     uint64_t *h;
     int rc0 = stage_begin(d, s, words * 8, (void **)&h);
@@ -751,7 +817,12 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     std::memcpy(h + 2 * count, prefix.data(), (count + 1) * 8);
     uint64_t *wb = h + 3 * count + 1;
     for (uint64_t w = 0; w < nw; ++w) {
-        const uint64_t t0 = w * ntiles / nw;
+        uint64_t t0 = w * ntiles / nw;
+        if (nstatic) {  // the kernel's dyn split: static tile wb0 + wave of the workgroup's share
+            const uint64_t blk = w / geo.waves_per_block, wv = w % geo.waves_per_block;
+            const uint64_t wb0 = blk * ntiles / geo.blocks, wb1 = (blk + 1) * ntiles / geo.blocks;
+            t0 = std::min(wb0 + wv, wb1);
+        }
         const uint64_t b = (uint64_t)(std::upper_bound(prefix.begin(), prefix.end(), t0) - prefix.begin()) - 1;
         wb[w] = std::min<uint64_t>(b, count - 1);
     }
@@ -779,6 +850,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     p.ntiles = ntiles;
     p.d_seeds = d_seeds;
     p.d_out = d_out;
+    p.nstatic = nstatic;
     return launch_scan(d, alg, p, count, tmax, total, s);
 }
 

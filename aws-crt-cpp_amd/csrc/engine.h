@@ -22,8 +22,19 @@ constexpr int kVecPerGroup = kGroupBytes / 16;
 // crc64_stream4_kernel workgroup size, two per CU.  One 1024-thread workgroup per CU measured a 3 %
 // shorter isolated C5 launch (95.8 vs 98.8 us) but 4-7 % less C5 throughput over three streams
 // (launches of other streams no longer co-reside): 512.
-constexpr int kW64StreamBlock = 512;
+#ifndef AMDCRC_W64_BLOCK  // compile-time only (geometry experiments)
+#define AMDCRC_W64_BLOCK 512
+#endif
+constexpr int kW64StreamBlock = AMDCRC_W64_BLOCK;
 constexpr int kMaxBatches = 32;  // batches per strided launch (kernel arguments, 768 bytes)
+
+// The 16-byte-word CRC32 streaming scan (crc_kernels.hip Braid32W16: slice-by-16 rows, one
+// global_load_dwordx4 per lane per row, one 1024-thread workgroup per CU) for launches of >= 256 MiB.
+// Parity-green, but measured slower than the 8-byte-word scan on every shape, so
+// the release build neither dispatches nor instantiates it; -DAMDCRC_STREAM_W16=1 builds it back.
+#ifndef AMDCRC_STREAM_W16  // compile-time only (A/B builds)
+#define AMDCRC_STREAM_W16 0
+#endif
 
 struct ScanParams {
     // ---- batch description: strided (base != 0) or list (d_ptrs != 0)

@@ -89,5 +89,18 @@ def main(nbatch=20, reps=30):
     print(json.dumps(res))
 
 
+def set_sched(mode):
+    """hipSetDeviceFlags before the device's context exists (AMDCRC_PROBE_SCHED=spin|yield|blocking):
+    how the host waits in hipDeviceSynchronize -- the completion-to-host leg of a timed region"""
+    import ctypes
+
+    flags = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}[mode]
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipSetDeviceFlags(ctypes.c_uint(flags))
+    print(json.dumps({"sched": mode, "hipSetDeviceFlags_rc": rc}), flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("AMDCRC_PROBE_SCHED"):
+        set_sched(os.environ["AMDCRC_PROBE_SCHED"])
     main(*(int(a) for a in sys.argv[1:]))

@@ -221,6 +221,19 @@ def third_party_rates(alg, host, count, L, threads, gpu_results, rate):
     return {"impl": name, "gibs": round(vn, 2), "threads": threads, "single_thread_gibs": round(v1, 2), "parity_with_gpu": True}
 
 
+def pmc_traffic(alg, nbuf, L, batches_per_launch):
+    """HBM bytes per launch of this shape from the committed rocprofv3 FETCH_SIZE passes
+    (profiles/pmc_traffic.json), with its source, or None"""
+    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        for rec in json.load(open(pmc))["records"]:
+            if rec.get("workload") == f"{alg}:{nbuf}x{L}" and rec.get("batches_per_launch", 1) == batches_per_launch:
+                return rec.get("hbm_bytes_per_launch"), rec.get("source", "profiles/pmc_traffic.json")
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def time_launches(eng, launch, st, nt):
     """Mean dispatch duration (ms) of nt launches serialised on stream st behind a GPU-side hold."""
     import torch
@@ -265,7 +278,7 @@ def kernel_name(alg, nbuf, L):
     if alg == "crc64nvme":
         return "crc_lanes_kernel" if L <= 4096 and nbuf >= 65536 else "crc64_stream4_kernel"
     if alg == "xxh64":
-        if nbuf <= 32 and L >= 1 << 20:
+        if nbuf <= 16 and L >= 1 << 20:
             return "xxh64 host route (D2H slices + host threads, stream-ordered; DESIGN.md §3.4)"
         return "xxh64_row_kernel" if nbuf <= 1024 else "xxh64_wave_kernel"
     return "xxh3_blocksum_kernel + xxh3_wave_kernel"
@@ -336,7 +349,10 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
                        f"{alg.upper()}, device-resident, {nb} rotating batches, {per} per launch",
            "value": round(gibs, 2), "unit": "GiB/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
-           "roofline": roofline(per * step_bytes, kms, kernel_name(alg, nbuf, L))}
+           "roofline": dict(roofline(per * step_bytes, kms, kernel_name(alg, nbuf, L)), timing_launches=timing)}
+    trf = pmc_traffic(alg, nbuf, L, per)
+    if trf:
+        rec["roofline"]["traffic"], rec["roofline"]["traffic_source"] = trf
     if do_cpu:
         # the whole step's buffers (buffers round-robin over the threads, so a sample
         # of fewer buffers than threads would leave cores idle)
@@ -585,16 +601,9 @@ def main():
         roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(step_bytes, kms1, "")["frac"],
                                 "bytes_per_launch": step_bytes}
     roof["traffic"] = None
-    pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            doc = json.load(open(pmc))
-            for rec in doc["records"] if "records" in doc else [doc]:
-                if rec.get("workload") == f"{alg}:{count}x{L}" and rec.get("batches_per_launch", 1) == gsz:
-                    roof["traffic"] = rec.get("hbm_bytes_per_launch")
-                    roof["traffic_source"] = rec.get("source", "profiles/pmc_traffic.json")
-        except Exception:
-            pass
+    trf = pmc_traffic(alg, count, L, gsz)
+    if trf:
+        roof["traffic"], roof["traffic_source"] = trf
 
     # secondary denominator: the streaming-read ceiling of a one-batch launch and
     # of a launch of the timed region's size (the same bytes, read by an XOR-reduce kernel)
@@ -606,6 +615,7 @@ def main():
         rcg_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, gsz * step_bytes, stream=st), streams[0],
                                   max(2, nt // 4))
         roof["read_ceiling"] = {"kernel_ms": round(rcg_ms, 5), "frac": roofline(gsz * step_bytes, rcg_ms, "")["frac"],
+                                "timing_launches": max(2, nt // 4),
                                 "scan_frac_of_ceiling": round(rcg_ms / kms, 4),
                                 "kernel": "read_ceiling_kernel: the scan's launch shape, 256-B non-temporal rows XOR-reduced"}
 

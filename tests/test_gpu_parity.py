@@ -227,6 +227,58 @@ def test_crc64_short_strided_batches_lane_path(engine):
                 assert got[i] == oracle.crc("crc64nvme", h[base + i * stride: base + i * stride + L], seeds[j][i]), (j, i)
 
 
+@pytest.mark.parametrize("count,L,stride,off,seeded", [
+    (16384, 8192, 8192, 0, False),          # the C4 shard's buffer size, exactly a set of four per wave slot
+    (16387, 8212, 8224, 3, True),           # a partial last set; 13 head and 7 tail bytes per buffer; seeds
+    (20000, 2048, 2048, 0, True),           # two groups per buffer
+    (16400, 65552, 65552, 5, False),        # 64 KiB main regions, 11 head and 5 tail bytes
+])
+def test_crc64_rows16_short_buffers(engine, count, L, stride, off, seeded):
+    """Strided CRC64NVME batches of >= 16384 short buffers whose main regions are whole 1 KiB groups
+    take crc64_rows16_kernel (16 lanes per buffer, four buffers per wave): whole sets, a partial last
+    set, unaligned heads and tails, seeds."""
+    import torch
+
+    d = dev_random(stride * count + off + 64, 0x1616 + count)
+    rng = random.Random(count)
+    seeds = [rng.getrandbits(64) for _ in range(count)] if seeded else None
+    out = engine.checksum_strided(ALG["crc64nvme"], d, stride, L, count,
+                                  seeds=seeds_tensor("crc64nvme", seeds) if seeded else None, base_offset=off)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    got = engine.as_unsigned(out)
+    ptrs = [h.ctypes.data + off + i * stride for i in range(count)]
+    if not seeded:
+        assert got == oracle.batch("crc64nvme", ptrs, [L] * count, 8)
+    else:
+        for i in list(range(0, count, 211)) + [count - 1, count - 2, count - 3]:
+            assert got[i] == oracle.crc("crc64nvme", h[off + i * stride: off + i * stride + L], seeds[i]), i
+
+
+def test_crc64_rows16_multi_batch(engine):
+    """Three queued batches of 16384 x 8 KiB through aws_crt_amd_checksum_batches (one rows16 launch
+    over 49152 buffers, sets crossing batch boundaries), seeds on one batch."""
+    import torch
+
+    L, count, nb = 8192, 16384, 3
+    d = dev_random(nb * L * count, 0x1617)
+    rng = random.Random(0x1617)
+    seeds = [[rng.getrandbits(64) for _ in range(count)] if j == 2 else None for j in range(nb)]
+    outs = [torch.empty(count, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    engine.checksum_batches(ALG["crc64nvme"], [(d.data_ptr() + j * L * count, seeds_tensor("crc64nvme", seeds[j]) if seeds[j] else None,
+                                                outs[j]) for j in range(nb)], L, L, count)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    for j in range(nb):
+        ptrs = [h.ctypes.data + (j * count + i) * L for i in range(count)]
+        if seeds[j] is None:
+            assert engine.as_unsigned(outs[j]) == oracle.batch("crc64nvme", ptrs, [L] * count, 8), j
+        else:
+            got = engine.as_unsigned(outs[j])
+            for i in range(0, count, 331):
+                assert got[i] == oracle.crc("crc64nvme", h[(j * count + i) * L:(j * count + i + 1) * L], seeds[j][i]), i
+
+
 def test_xxh64_list_many_buffers_per_wave(engine):
     """Ragged XXH64 lists of more than 1024 buffers put several buffers in one wave
     (xxh64_quad_kernel, bpw = ceil(n / 1024)): 5000 buffers of random length 0..3000 at random
