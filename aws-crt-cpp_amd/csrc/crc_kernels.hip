@@ -35,6 +35,7 @@ using namespace amdcrc;
 namespace {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const v4u gv4u;
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 typedef __attribute__((address_space(1))) const uint64_t gu64;
@@ -809,7 +810,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     // uniform batches): the workgroup's even share [wb0, wb1) is split into one static tile per wave
     // and a pool the waves claim from an LDS counter as they run dry, so a wave the memory system
     // serves late scans less of its workgroup's share.
-    const bool dyn = p.nstatic != 0;  // strided batches, and lists when the host asks (engine.cpp list_impl)
+    const bool dyn = !LIST && p.nstatic != 0;
     uint64_t t0, t1, pool_base = 0, pool_size = 0;
     if (dyn) {
         const uint64_t wb0 = (uint64_t)blockIdx.x * p.ntiles / gridDim.x, wb1 = ((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x;
@@ -1238,7 +1239,7 @@ __device__ __forceinline__ void sx_store32(unsigned int *a, unsigned int v) {  /
 }
 
 // publish the wave's merged tiles of one group and, if they complete it, finish the group at once
-template <class B>
+template <class B, bool LIST = false>
 __device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g, const B &eng, int lane) {
     if (g.slot == ~0ull) return;
     if (!AMDCRC_GUARD_OK(g.slot < p.ntiles && g.b < p.nbuf, 4, g.slot)) return;
@@ -1255,7 +1256,7 @@ __device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g
     if (lane != 0) return;
     (void)sx_swap64_ret(&p.d_acc1[slot], 0ull);
     if (G == 1) {
-        finalize<false>(p, g.b, grp, eng);
+        finalize<LIST>(p, g.b, grp, eng);
         return;
     }
     (void)sx_xor64_ret(&p.d_acc[g.b], (unsigned long long)grp);  // performed before it is counted
@@ -1263,7 +1264,7 @@ __device__ __forceinline__ void stream_publish(const ScanParams &p, BGroupAcc &g
     if (c == G - 1) {
         const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[g.b], 0ull);
         sx_store32(&p.d_cnt[g.b], 0u);
-        finalize<false>(p, g.b, fin, eng);
+        finalize<LIST>(p, g.b, fin, eng);
     }
 }
 
@@ -1272,13 +1273,13 @@ struct LocalBufs {
     uint64_t b0, b1;
 };
 
-template <class B>
+template <class B, bool LIST = false>
 __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane, BGroupAcc &acc,
                                               const LocalBufs &lb) {
     const uint32_t r = wave_xor_s(eng.mulK(u, lane));
     if (!AMDCRC_GUARD_OK(d.b < p.nbuf && d.k < d.T, 2, d.b)) return;
     if (d.T == 1) {
-        if (lane == 0) finalize<false>(p, d.b, r, eng);
+        if (lane == 0) finalize<LIST>(p, d.b, r, eng);
         return;
     }
     const uint64_t g0 = d.k & ~31ull, gend = d.T - g0 < 32 ? d.T : g0 + 32;
@@ -1293,13 +1294,13 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
             const unsigned long long now =
                 __hip_atomic_fetch_xor(slot, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ^ add;
             const unsigned long long full = d.T >= 32 ? 0xFFFFFFFF00000000ull : (((1ull << d.T) - 1) << 32);
-            if ((now & 0xFFFFFFFF00000000ull) == full) finalize<false>(p, d.b, (uint32_t)now, eng);
+            if ((now & 0xFFFFFFFF00000000ull) == full) finalize<LIST>(p, d.b, (uint32_t)now, eng);
         }
         return;
     }
     const uint64_t slot = d.tbase + g0;
     if (slot != acc.slot) {
-        stream_publish(p, acc, eng, lane);
+        stream_publish<B, LIST>(p, acc, eng, lane);
         acc.slot = slot;
         acc.val = 0;
         acc.b = d.b;
@@ -1498,7 +1499,13 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     };
     // the first step is peeled (it publishes the constants, whose loads are then out of the loop),
     // so the loop header sees the same two ring slots in flight from the prologue and the back edge
+    // The loop body runs whole rotations of three steps with no exit between them, and the last one
+    // or two steps follow it.  With a break after each step (the round-2 loop) the compiler's wait-count
+    // pass reached the loop header with a merged state in which the slot about to be loaded still had
+    // loads in flight, and drained most of the ring at the top of every rotation (vmcnt 7..2 before the
+    // first step's row loads); without the breaks every row waits exactly vmcnt(16).
     step(ra, rc, true);
+#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
     while (q < nq) {
         step(rb, ra, false);
         if (q >= nq) break;
@@ -1506,8 +1513,273 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         if (q >= nq) break;
         step(ra, rc, false);
     }
+#else
+    while (q + 3 <= nq) {
+        step(rb, ra, false);
+        step(rc, rb, false);
+        step(ra, rc, false);
+    }
+    if (q < nq) {
+        step(rb, ra, false);
+        if (q < nq) step(rc, rb, false);
+    }
+#endif
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
     stream_publish(p, acc, eng, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// Ragged lists on the streaming scan (crc32_list_stream_kernel, round 3).  crc32_braid_kernel<POLY,
+// true> runs lists on a two-slot ring whose merged code paths (front-padded groups, tile walks) leave
+// the compiler inexact wait counts; this kernel is crc32_stream_kernel's one-path three-slot ring on
+// 8-byte words, with the list's tiles read through raw buffer resources:
+//  * Tile k of a buffer reads from base = its first real byte (the main start for k = 0, main start
+//    + k*TILE - pad after) with TILE - adj records (adj = pad for k = 0, else 0).  A lane's row offset
+//    is its offset in the virtual tile minus adj, clamped to the record count: the rows of the front
+//    pad come out negative (wrapped), clamp to the limit, and the range check returns zeros -- the
+//    virtual zeros the braid needs, with no masking in the scan and no traffic.  Past the wave's last
+//    group the placeholder rows go through a zero-record resource (no traffic either).
+//  * The head state enters lane l0 = (pad mod 512) / 8 at the start of the tile's first scanned group
+//    divided by X^j (X = x^(8*512), the row step; j = the pad's row in that group): the lane's words
+//    before the pad are zero, so its j row steps bring it to exactly s_h where the first real word
+//    joins (the X^(-j) columns follow the braid constants, kBraidXinvWord).
+//  * Waves own host-chosen tile ranges balanced by scanned groups (engine.cpp list_impl): d_wave_buf
+//    holds the start buffer of each wave, then the start tiles (nw + 1) and the group prefix (nw + 1).
+struct LCur {          // one tile of one buffer (wave-uniform)
+    uint64_t b, k, T;  // buffer, tile within it, tiles of the buffer
+    uint64_t t;        // global tile index
+    uint64_t vb;       // virtual start of the buffer's tile 0 (main start - pad)
+    uint64_t base;     // resource base of this tile
+    uint32_t pad;      // the buffer's front pad
+    uint32_t adj, nrec, gs;  // offset adjustment, records, first scanned group (G: none)
+};
+
+__device__ __forceinline__ void lcur_tile(LCur &c, uint64_t k, uint64_t tile_bytes, uint32_t G, bool has_main) {
+    c.k = k;
+    c.adj = k == 0 ? c.pad : 0u;
+    c.base = c.vb + k * tile_bytes + c.adj;
+    c.nrec = (uint32_t)(tile_bytes - c.adj);
+    c.gs = !has_main ? G : k == 0 ? c.pad / kWaveGroupBytes : 0u;
+}
+
+// the cursor on tile t of buffer b
+__device__ __forceinline__ void lcur_at(const ScanParams &p, LCur &c, uint64_t b, uint64_t t, uint64_t tile_bytes, uint32_t G) {
+    const Edges e = buffer_edges<true>(p, b);
+    const uint64_t mainlen = e.tail - e.headend;
+    const uint64_t t0 = sload64(p.d_tile_prefix + b), t1 = sload64(p.d_tile_prefix + b + 1);
+    c.b = b;
+    c.T = t1 - t0;
+    c.t = t;
+    c.pad = mainlen ? (uint32_t)(c.T * tile_bytes - mainlen) : 0u;
+    c.vb = e.headend - c.pad;
+    lcur_tile(c, t - t0, tile_bytes, G, mainlen != 0);
+}
+
+__device__ __forceinline__ void lcur_next(const ScanParams &p, LCur &c, uint64_t tile_bytes, uint32_t G) {
+    if (c.k + 1 < c.T)
+        lcur_tile(c, c.k + 1, tile_bytes, G, true), ++c.t;
+    else
+        lcur_at(p, c, c.b + 1, c.t + 1, tile_bytes, G);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint64_t base, uint32_t nrec) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)rfl64(base), (short)0, (int)__builtin_amdgcn_readfirstlane(nrec),
+                                             0x00020000);
+}
+
+template <int R>
+__device__ __forceinline__ uint64_t bld_w8(__amdgpu_buffer_rsrc_t rs, uint32_t o0, uint32_t lim) {
+    const uint32_t o = __builtin_elementwise_min(o0 + (uint32_t)(R * kW8Row), lim);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 2);  // aux 2: non-temporal
+    return ((uint64_t)v.y << 32) | v.x;
+}
+
+// stream_rows_w8 with the next group's rows read through a buffer resource
+template <int R, class B>
+__device__ __forceinline__ uint32_t list_rows_w8(uint32_t x, typename B::Hi h, W8Group &cur, W8Group &nxt,
+                                                 __amdgpu_buffer_rsrc_t rs, uint32_t o0, uint32_t lim, const B &eng) {
+    if constexpr (R < kW8RowsPerGroup) {
+        nxt.w[R] = bld_w8<R>(rs, o0, lim);
+        typename B::Hi hn;
+        if constexpr (R == 0) {
+            x ^= (uint32_t)cur.w[0];
+            hn = eng.look_hi((uint32_t)(cur.w[0] >> 32));
+        } else {
+            x = eng.look_lo(x, h, (uint32_t)cur.w[R]);
+            hn = eng.look_hi((uint32_t)(cur.w[R] >> 32));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return list_rows_w8<R + 1, B>(x, hn, cur, nxt, rs, o0, lim, eng);
+    } else {
+        return eng.look_lo(x, h, 0u);
+    }
+}
+template <int R>
+__device__ __forceinline__ void list_issue(W8Group &g, __amdgpu_buffer_rsrc_t rs, uint32_t o0, uint32_t lim) {
+    if constexpr (R < kW8RowsPerGroup) {
+        g.w[R] = bld_w8<R>(rs, o0, lim);
+        list_issue<R + 1>(g, rs, o0, lim);
+    }
+}
+
+template <uint32_t POLY>
+__global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const ScanParams p) {
+    using SS = StreamShape<8>;
+    using B = Braid32W8<POLY>;
+    constexpr int WAVES = SS::kWaves;
+    __shared__ __attribute__((aligned(16))) char lds[SS::kLds];
+    char *const cb = lds + SS::kTab;
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t *wtile = p.d_wave_buf + nw, *wq = p.d_wave_buf + 2 * nw + 1;
+    const uint64_t t0 = sload64(wtile + gw), t1 = sload64(wtile + gw + 1);
+    const uint32_t nq = (uint32_t)(sload64(wq + gw + 1) - sload64(wq + gw));  // groups of this wave
+    const uint32_t G = p.seg / kGroupBytes;
+    const uint64_t tile_bytes = (uint64_t)p.seg * kWave;
+    const uint32_t lo8 = 8u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
+    const bool work = t0 < t1;
+    const uint64_t *xinv = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidXinvWord);
+
+    // scan cursor (sc) and prefetch cursor (fc, group fg): both start on the wave's first tile
+    LCur sc{};
+    if (work) lcur_at(p, sc, sload64(p.d_wave_buf + gw), t0, tile_bytes, G);
+    LCur fc = sc;
+    // the prefetch cursor skips tiles without a main region (there are nq groups ahead of it)
+    if (nq)
+        while (fc.gs >= G) lcur_next(p, fc, tile_bytes, G);
+    uint32_t fq = 0, fg = fc.gs;
+    auto f_rsrc = [&]() { return fq < nq ? list_rsrc(fc.base, fc.nrec) : list_rsrc(dummy, 0u); };
+    auto f_off = [&]() { return fq < nq ? fg * kWaveGroupBytes + lo8 - fc.adj : lo8; };
+    auto f_lim = [&]() { return fq < nq ? fc.nrec : 0u; };
+    auto f_next = [&]() {
+        if (++fq >= nq) return;
+        if (++fg == G) {
+            do lcur_next(p, fc, tile_bytes, G);
+            while (fc.gs >= G);
+            fg = fc.gs;
+        }
+    };
+    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + SS::kKWord + 4 * threadIdx.x);
+    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
+    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + SS::kBlock);
+    // the two primed slots are issued unconditionally (a wave without groups issues zero-record
+    // placeholders): conditional issues give the compiler's wait-count pass paths where one slot is
+    // in flight and the other is not, and its merged state at the scan loop's header then drained
+    // the ring once per loop iteration
+    W8Group ra, rb, rc;
+    list_issue<0>(ra, f_rsrc(), f_off(), f_lim());
+    f_next();
+    {
+        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint32_t e = (uint32_t)lane + 64u * n;
+            const uint32_t te = basis_w8_rt<POLY>(t, e);
+            char *row = lds + (e << 8) + (t << 5);
+            *(uint4 *)row = make_uint4(te, te, te, te);
+            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
+        }
+        if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
+    }
+    if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    list_issue<0>(rb, f_rsrc(), f_off(), f_lim());
+    f_next();
+    bool consts_ready = false;
+    auto publish_consts = [&]() {
+        *(v4u *)(cb + 16 * threadIdx.x) = kq;
+        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * threadIdx.x) = pce0;
+        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * (threadIdx.x + SS::kBlock)) = pce1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(cb + (kConstFlagOff - kBKOff)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto await_consts = [&]() {
+        if (consts_ready) return;
+        while (__hip_atomic_load((uint32_t *)(cb + (kConstFlagOff - kBKOff)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+               (uint32_t)WAVES)
+            __builtin_amdgcn_s_sleep(1);
+        consts_ready = true;
+    };
+    // a buffer without a main region (under 16 aligned bytes): its head fold is the whole CRC
+    auto finish_empty = [&]() {
+        const uint32_t s_h = head_state<true>(p, sc.b, eng);
+        if (lane == 0) finalize<true>(p, sc.b, s_h, eng);
+    };
+    // leading tiles without a main region
+    if (work)
+        while (sc.gs >= G) {
+            finish_empty();
+            if (sc.t + 1 >= t1) break;
+            lcur_next(p, sc, tile_bytes, G);
+        }
+    if (!nq) {
+        publish_consts();
+        ring_drain(ra, rb, rb);
+        return;
+    }
+
+    uint32_t g = sc.gs, u = 0, q = 0;
+    // a tile's first scanned group: the head state (tile 0) enters its lane, divided by X^j
+    auto tile_begin = [&]() {
+        g = sc.gs;
+        u = 0;
+        if (sc.k == 0) {
+            uint32_t s_h = head_state<true>(p, sc.b, eng);
+            const uint32_t j = (sc.pad >> 9) & 7u;
+            if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
+            if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
+        }
+    };
+    tile_begin();
+    BGroupAcc acc{};
+    acc.slot = ~0ull;
+    const LocalBufs lb{0, 0};
+    auto step = [&](W8Group &cur, W8Group &nxt, bool first) {
+        const __amdgpu_buffer_rsrc_t rs = f_rsrc();
+        const uint32_t fo = f_off(), fl = f_lim();
+        f_next();
+        u = list_rows_w8<0, B>(u, typename B::Hi{}, cur, nxt, rs, fo, fl, eng);
+        if (first) publish_consts();
+        ++q;
+        if (++g == G) {
+            await_consts();
+            Tile d;
+            d.b = sc.b, d.k = sc.k, d.T = sc.T, d.tbase = sc.t - sc.k;
+            d.vbase = 0, d.pad = 0, d.ngroups = G;
+            stream_finish<B, true>(p, d, u, eng, lane, acc, lb);
+            if (q < nq) {
+                // the next tile with a main region, finishing the empty buffers on the way
+                for (;;) {
+                    lcur_next(p, sc, tile_bytes, G);
+                    if (sc.gs < G) break;
+                    finish_empty();
+                }
+                tile_begin();
+            }
+        }
+    };
+    step(ra, rc, true);
+    while (q + 3 <= nq) {  // whole rotations, then the rest (see crc32_stream_kernel)
+        step(rb, ra, false);
+        step(rc, rb, false);
+        step(ra, rc, false);
+    }
+    if (q < nq) {
+        step(rb, ra, false);
+        if (q < nq) step(rc, rb, false);
+    }
+    ring_drain(ra, rb, rc);  // the trailing placeholder rows
+    // trailing tiles without a main region
+    while (sc.t + 1 < t1) {
+        lcur_next(p, sc, tile_bytes, G);
+        finish_empty();
+    }
+    stream_publish<B, true>(p, acc, eng, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2145,6 +2417,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
             if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
         }
     };
+#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
     for (;;) {
         step(ra, rc);
         if (q >= nq) break;
@@ -2153,6 +2426,19 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
         step(rc, rb);
         if (q >= nq) break;
     }
+#else
+    // whole rotations of three steps, then the rest (the breaks drained the ring at every loop
+    // header: see crc32_stream_kernel)
+    while (q + 3 <= nq) {
+        step(ra, rc);
+        step(rb, ra);
+        step(rc, rb);
+    }
+    if (q < nq) {
+        step(ra, rc);
+        if (q < nq) step(rb, ra);
+    }
+#endif
 }
 
 
@@ -2220,19 +2506,22 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
     const bool work = s0 < s1;
     const uint64_t dummy = (uint64_t)p.d_kvals + 8u * t;  // placeholder rows: the 16 KiB constant block
     // this lane's buffer of set s: main-region address + 8 t (rows past the batch read the constants)
+    // (the four row bases are wave-uniform: computed on the scalar unit, so a multi-batch launch reads
+    // its batch bases with scalar loads -- a per-lane kernarg load is a vector load whose wait drained
+    // the payload ring once per set)
     auto lane_base = [&](uint64_t s) -> uint64_t {
         uint64_t a[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint64_t b = 4 * s + (uint64_t)r;
+            const uint64_t b = rfl64(4 * s + (uint64_t)r);
             if (b < p.nbuf) {
                 const BatchPos bp = batch_pos(p, b);
-                a[r] = karg64(p.bbase, bp.j) + bp.i * p.stride + hoff + 8u * t;
+                a[r] = rfl64(karg64(p.bbase, bp.j) + bp.i * p.stride + hoff);
             } else {
-                a[r] = dummy;
+                a[r] = rfl64((uint64_t)p.d_kvals);
             }
         }
-        return row == 0 ? a[0] : row == 1 ? a[1] : row == 2 ? a[2] : a[3];
+        return (row == 0 ? a[0] : row == 1 ? a[1] : row == 2 ? a[2] : a[3]) + 8u * t;
     };
     uint32_t fq = 0, fg = 0;  // prefetch cursor: groups issued, group within the set
     uint64_t fs = s0;
@@ -2291,6 +2580,7 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
             ++s;
         }
     };
+#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
     for (;;) {
         step(ra, rc);
         if (q >= nq) break;
@@ -2299,6 +2589,19 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
         step(rc, rb);
         if (q >= nq) break;
     }
+#else
+    // whole rotations of three steps, then the rest (the breaks drained the ring at every loop
+    // header: see crc32_stream_kernel)
+    while (q + 3 <= nq) {
+        step(ra, rc);
+        step(rb, ra);
+        step(rc, rb);
+    }
+    if (q < nq) {
+        step(ra, rc);
+        if (q < nq) step(rb, ra);
+    }
+#endif
     // the trailing placeholder rows: their registers stay live until the loads have landed
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]), "+v"(ra.w[5]),
                  "+v"(ra.w[6]), "+v"(ra.w[7])::"memory");
@@ -2812,6 +3115,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
 #endif
             if (p->stream && !list)
                 launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
+            else if (list && p->stream == 4)
+                launch(crc32_list_stream_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32, true>, nblocks, kBraidBlock, s, p, ev);
             else
@@ -2825,6 +3130,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
 #endif
             if (p->stream && !list)
                 launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
+            else if (list && p->stream == 4)
+                launch(crc32_list_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
                 launch(crc32_braid_kernel<kPoly32C, true>, nblocks, kBraidBlock, s, p, ev);
             else

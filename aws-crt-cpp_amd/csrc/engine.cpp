@@ -208,6 +208,16 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
                 for (int i = 0; i < wbits; ++i) kl = inv_mulx32(kl, poly);
             }
         }
+        // X^(-j) columns (X = x^(8*512), the 8-byte-word row step), u64 each: column i = X^(-j) * x^i
+        uint32_t xj = 0x80000000u;  // x^0
+        for (int j = 0; j < 8; ++j) {
+            uint32_t col = xj;
+            for (int i = 0; i < 32; ++i) {
+                c[kBraidXinvWord + 2 * (32 * j + i)] = col;
+                col = (uint32_t)gf2_mulx(col, poly);
+            }
+            for (int i = 0; i < 8 * 512; ++i) xj = inv_mulx32(xj, poly);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
@@ -362,6 +372,26 @@ constexpr uint64_t kLaneStrided64Max = AMDCRC_LANE64_MAX;
 constexpr uint64_t kLaneStrided64MinBuffers = 65536;
 // Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
 constexpr uint64_t kXxh3SplitBlocks = 4096;
+// Ragged CRC32 / CRC32C lists: crc32_list_stream_kernel (0 keeps crc32_braid_kernel<POLY, true>), with
+// tiles for kListStreamTilesPerSlot per wave slot (finer tiles even out the waves' scanned groups), on
+// two 512-thread workgroups per CU once a list holds kListTwoPerCuBytes of main bytes
+#ifndef AMDCRC_LIST_STREAM  // compile-time only (A/B builds)
+#define AMDCRC_LIST_STREAM 1
+#endif
+#ifndef AMDCRC_LIST_TILES_PER_SLOT
+#define AMDCRC_LIST_TILES_PER_SLOT 1
+#endif
+#ifndef AMDCRC_LIST_TWO_PER_CU
+#define AMDCRC_LIST_TWO_PER_CU (64ull << 20)
+#endif
+constexpr bool kListStream = AMDCRC_LIST_STREAM != 0;
+constexpr uint64_t kListStreamTilesPerSlot = AMDCRC_LIST_TILES_PER_SLOT;
+constexpr uint64_t kListTwoPerCuBytes = AMDCRC_LIST_TWO_PER_CU;
+uint64_t list_stream_blocks(const Device *d, uint64_t ntiles, uint64_t total_main) {
+    const uint64_t per_cu = total_main >= kListTwoPerCuBytes ? 2 : 1;
+    return std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 7) / 8, (uint64_t)d->cus * per_cu));
+}
+
 struct ScanGeometry {
     uint64_t blocks, waves_per_block;
 };
@@ -410,6 +440,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
     uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
     if (p.stream == 3) blocks = std::min<uint64_t>((p.nbuf + 4 * 8 - 1) / (4 * 8), 2 * (uint64_t)d->cus);  // 4 buffers per wave
+    if (p.list_mode && p.stream == 4) blocks = list_stream_blocks(d, p.ntiles, total_main);  // the waves list_stream split for
     if (blocks == 0) return 0;
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
@@ -745,6 +776,80 @@ int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
     return 0;
 }
 
+// Ragged CRC32 / CRC32C lists on crc32_list_stream_kernel.  Every buffer's main
+// region is T = ceil(main / TILE) tiles, front-padded to whole tiles; tile 0 scans its groups from the
+// one holding the pad's end.  The waves' tile ranges are cut at the tile boundaries nearest to an even
+// split of the scanned groups.  Descriptor block: ptrs[count] lens[count] tile prefix[count + 1], then
+// per wave its start buffer [nw], start tile [nw + 1] and group prefix [nw + 1].
+int list_stream(Device *d, int alg, const void *const *ptrs, const size_t *lens, size_t count,
+                const std::vector<uint64_t> &mains, uint64_t total, uint32_t seg, const void *d_seeds, void *d_out,
+                hipStream_t s) {
+    const uint64_t tile = (uint64_t)seg * kWave, G = seg / kGroupBytes, gbytes = tile / G;
+    std::vector<uint64_t> prefix(count + 1, 0), gp(count + 1, 0), gs(count, 0);
+    uint64_t tmax = 1;
+    for (size_t i = 0; i < count; ++i) {
+        const uint64_t T = mains[i] ? (mains[i] + tile - 1) / tile : 1;
+        gs[i] = mains[i] ? (T * tile - mains[i]) / gbytes : G;  // first scanned group of tile 0
+        tmax = std::max(tmax, T);
+        prefix[i + 1] = prefix[i] + T;
+        gp[i + 1] = gp[i] + (mains[i] ? T * G - gs[i] : 0);
+    }
+    const uint64_t ntiles = prefix[count], ng = gp[count];
+    const uint64_t blocks = list_stream_blocks(d, ntiles, total), nw = blocks * 8;
+    // group prefix at tile t (t < ntiles), and the tile holding group q (q < ng)
+    auto tile_buf = [&](uint64_t t) { return (uint64_t)(std::upper_bound(prefix.begin(), prefix.end(), t) - prefix.begin()) - 1; };
+    auto gstart = [&](uint64_t t) {
+        if (t >= ntiles) return ng;
+        const uint64_t b = tile_buf(t), k = t - prefix[b];
+        return mains[b] == 0 || k == 0 ? gp[b] : gp[b] + (G - gs[b]) + (k - 1) * G;
+    };
+    const size_t words = count * 2 + (count + 1) + nw + 2 * (nw + 1);
+    uint64_t *h;
+    int rc = stage_begin(d, s, words * 8, (void **)&h);
+    if (rc) return rc;
+    for (size_t i = 0; i < count; ++i) {
+        h[i] = (uint64_t)(uintptr_t)ptrs[i];
+        h[count + i] = lens[i];
+    }
+    std::memcpy(h + 2 * count, prefix.data(), (count + 1) * 8);
+    uint64_t *wbuf = h + 3 * count + 1, *wtile = wbuf + nw, *wq = wtile + nw + 1;
+    for (uint64_t w = 0; w <= nw; ++w) {
+        uint64_t t;
+        if (w == 0) {
+            t = 0;
+        } else if (w == nw || ng == 0) {
+            t = ntiles;
+        } else {
+            const uint64_t q = w * ng / nw;
+            const uint64_t b = (uint64_t)(std::upper_bound(gp.begin(), gp.end(), q) - gp.begin()) - 1;  // main > 0
+            const uint64_t qq = q - gp[b], g0 = G - gs[b];
+            const uint64_t k = qq < g0 ? 0 : 1 + (qq - g0) / G;
+            const uint64_t gt = k == 0 ? g0 : G, at = k == 0 ? 0 : g0 + (k - 1) * G;
+            t = prefix[b] + k + (2 * (qq - at) > gt ? 1 : 0);  // the nearer boundary of that tile
+        }
+        wtile[w] = std::max<uint64_t>(t, w ? wtile[w - 1] : 0);
+        wq[w] = gstart(wtile[w]);
+        if (w < nw) wbuf[w] = wtile[w] < ntiles ? tile_buf(wtile[w]) : count - 1;
+    }
+    const uint64_t *dd;
+    if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;
+    ScanParams p{};
+    p.seg = seg;
+    p.list_mode = 1;
+    p.stream = 4;
+    p.nbatch = 1;
+    p.bcount = count;
+    p.d_ptrs = dd;
+    p.d_lens = dd + count;
+    p.d_tile_prefix = dd + 2 * count;
+    p.d_wave_buf = dd + 3 * count + 1;
+    p.nbuf = count;
+    p.ntiles = ntiles;
+    p.d_seeds = d_seeds;
+    p.d_out = d_out;
+    return launch_scan(d, alg, p, count, tmax, total, s);
+}
+
 int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, size_t count, const void *d_seeds,
               void *d_out, hipStream_t s) {
     if (count == 0) return 0;
@@ -779,15 +884,17 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     }
     uint32_t seg = kGroupBytes;
     uint64_t tile = 0;
+    const bool lstream = kListStream && !xxh && width_of(alg) == 32;
     if (!xxh) {
         std::vector<uint64_t> sorted(mains);
         std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
-        seg = choose_seg(d, total, sorted[count / 2]);
+        seg = choose_seg(d, total, sorted[count / 2], lstream ? kListStreamTilesPerSlot : 1);
 #ifdef AMDCRC_XP_LIST_SEG_DIV  // experiment builds only: smaller list tiles (balance vs finishes)
         seg = std::max<uint32_t>(kGroupBytes, seg / AMDCRC_XP_LIST_SEG_DIV);
 #endif
         tile = (uint64_t)seg * kWave;
     }
+    if (lstream) return list_stream(d, alg, ptrs, lens, count, mains, total, seg, d_seeds, d_out, s);
     // descriptor block: ptrs[count] lens[count] prefix[count+1] wavebuf[nwaves]
     std::vector<uint64_t> prefix(count + 1, 0);
     uint64_t tmax = 1;
@@ -799,13 +906,9 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     const uint64_t ntiles = prefix[count];
     const ScanGeometry geo = scan_geometry(d, xxh ? ALG_CRC32 : alg, ntiles, total);
     const uint64_t nw = std::max<uint64_t>(geo.blocks, 1) * geo.waves_per_block;
-    // W=32 lists with at least two tiles per wave slot: one static tile per wave, the rest of each
-    // workgroup's share claimed from its LDS pool (the kernel's dyn mode), so waves whose tiles are
-    // mostly front pad take more tiles
-    uint64_t nstatic = 0;
-#ifdef AMDCRC_XP_LIST_POOL  // experiment builds only
-    if (!xxh && width_of(alg) == 32 && ntiles >= 2 * nw) nstatic = nw;
-#endif
+    // (a workgroup tile pool for lists, as strided batches have, was tried in round 3 and dropped: its
+    // claims do not skip tiles without a main region -- empty or sub-16-byte buffers -- which the
+    // static walk skips)
     const size_t words = count * 2 + (count + 1) + nw;
     uint64_t *h;
     int rc0 = stage_begin(d, s, words * 8, (void **)&h);
@@ -817,12 +920,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     std::memcpy(h + 2 * count, prefix.data(), (count + 1) * 8);
     uint64_t *wb = h + 3 * count + 1;
     for (uint64_t w = 0; w < nw; ++w) {
-        uint64_t t0 = w * ntiles / nw;
-        if (nstatic) {  // the kernel's dyn split: static tile wb0 + wave of the workgroup's share
-            const uint64_t blk = w / geo.waves_per_block, wv = w % geo.waves_per_block;
-            const uint64_t wb0 = blk * ntiles / geo.blocks, wb1 = (blk + 1) * ntiles / geo.blocks;
-            t0 = std::min(wb0 + wv, wb1);
-        }
+        const uint64_t t0 = w * ntiles / nw;
         const uint64_t b = (uint64_t)(std::upper_bound(prefix.begin(), prefix.end(), t0) - prefix.begin()) - 1;
         wb[w] = std::min<uint64_t>(b, count - 1);
     }
@@ -850,7 +948,6 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     p.ntiles = ntiles;
     p.d_seeds = d_seeds;
     p.d_out = d_out;
-    p.nstatic = nstatic;
     return launch_scan(d, alg, p, count, tmax, total, s);
 }
 

@@ -45,7 +45,8 @@ struct ScanParams {
     const uint64_t *d_ptrs;        // list: device addresses
     const uint64_t *d_lens;        // list: lengths
     const uint64_t *d_tile_prefix; // list: exclusive prefix of T_b (nbuf + 1 entries)
-    const uint64_t *d_wave_buf;    // list: buffer index holding each wave's first tile
+    const uint64_t *d_wave_buf;    // list: buffer index holding each wave's first tile (stream 4: then the
+                                   // waves' first tiles, nw + 1, and their group prefix, nw + 1)
     uint64_t nbuf;
     uint64_t ntiles;
     // ---- seeds (previous CRC, finalised) and results
@@ -57,7 +58,8 @@ struct ScanParams {
     uint32_t list_mode;            // 1: d_ptrs/d_lens/d_tile_prefix/d_wave_buf describe the batch
     uint32_t stream;               // strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel /
                                    // crc64_stream4_kernel); W=32: 1 = 8-byte lane words (512-thread workgroups),
-                                   // 2 = 16-byte lane words (one 1024-thread workgroup per CU)
+                                   // 2 = 16-byte lane words (one 1024-thread workgroup per CU); 3 = CRC64NVME
+                                   // rows of 16 lanes (crc64_rows16_kernel); lists: 4 = crc32_list_stream_kernel
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;
@@ -88,10 +90,13 @@ struct ScanParams {
 //   [3072, 3328)  T_0[e] = e * x^8: plain byte step for head / tail bytes
 //   [3328, 5376)  K-matrix image of x^(-64 l) (the streaming scan's 8-byte words), same layout
 //   [5376, 7424)  K-matrix image of x^(-128 l) (the streaming scan's 16-byte words), same layout
+//   [7424, 7936)  columns (u64) of X^(-j), X = x^(8*512), j < 8: the list streaming scan's head-state
+//                 entry (crc32_list_stream_kernel)
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 7424;
+constexpr int kBraidConstWords = 7936;
+constexpr int kBraidXinvWord = 7424;  // first word of the X^(-j) columns
 constexpr int kBraidK64Word = 3328;   // first word of the x^(-64 l) K image
 constexpr int kBraidK128Word = 5376;  // first word of the x^(-128 l) K image
 

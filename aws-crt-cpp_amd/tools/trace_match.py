@@ -40,17 +40,18 @@ def bench_entries(rec):
     """(label, events kernel_ms, launches timed) in the order bench.py timed them"""
     roof = rec["roofline"]
     nt = roof.get("timing_launches")
-    ent = [("headline launch", roof["kernel_ms"], nt)]
+    ent = [("headline launch", roof["kernel_ms"], nt, roof.get("kernel"))]
     sb = roof.get("single_batch")
     if sb:
-        ent.append(("one-batch launch", sb["kernel_ms"], nt))
+        ent.append(("one-batch launch", sb["kernel_ms"], nt, roof.get("kernel")))
         if "read_ceiling_kernel_ms" in sb:
-            ent.append(("read ceiling, one batch", sb["read_ceiling_kernel_ms"], nt))
+            ent.append(("read ceiling, one batch", sb["read_ceiling_kernel_ms"], nt, "read_ceiling_kernel"))
     if roof.get("read_ceiling"):
         ent.append(("read ceiling, headline size", roof["read_ceiling"]["kernel_ms"],
-                    roof["read_ceiling"].get("timing_launches", max(2, (nt or 8) // 4))))
+                    roof["read_ceiling"].get("timing_launches", max(2, (nt or 8) // 4)), "read_ceiling_kernel"))
     for k, v in (rec.get("configs") or {}).items():
-        ent.append((k, v["roofline"]["kernel_ms"], v["roofline"].get("timing_launches", 2 if "xxh64" in k else 6)))
+        ent.append((k, v["roofline"]["kernel_ms"], v["roofline"].get("timing_launches", 2 if "xxh64" in k else 6),
+                    v["roofline"].get("kernel")))
     return ent
 
 
@@ -59,12 +60,17 @@ def main(trace_csv, bench_log):
     secs = [s for s in sections(trace_csv) if s]
     ents = bench_entries(rec)
     rows = []
-    for (label, ev_ms, k), sec in zip(ents, secs):
+    for (label, ev_ms, k, kname), sec in zip(ents, secs):
+        if kname and "host route" in str(kname):
+            # no kernel dispatch: D2H copies and host hashing, bracketed by the bench's events
+            rows.append({"section": label, "bench_events_ms": ev_ms, "rocprof_avg_ms": None, "kernels": [],
+                         "note": "host route: no kernel dispatch to match"})
+            continue
         # the section's timed launches: its first k dispatches of its first kernel (what follows the
         # launches -- the next leg's warm-up, copies -- is not part of it); a host-routed leg (XXH64
         # host route) has copies only, and its events bracket them
         sec = [x for x in sec if x[0] == sec[0][0]][: k or len(sec)]
-        names = {n.split("(")[0] for n, _ in sec}
+        names = {n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0] for n, _ in sec}
         avg_ms = sum(d for _, d in sec) / len(sec) / 1e6
         rows.append({"section": label, "bench_events_ms": ev_ms, "rocprof_avg_ms": round(avg_ms, 5),
                      "dispatches": len(sec), "kernels": sorted(names),

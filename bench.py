@@ -620,7 +620,9 @@ def main():
                                 "kernel": "read_ceiling_kernel: the scan's launch shape, 256-B non-temporal rows XOR-reduced"}
 
     # per-rank record (device, kernel time, fraction, parity), gathered on rank 0
+    props = torch.cuda.get_device_properties(dev)
     mine = {"rank": rank, "local_rank": local, "device": torch.cuda.get_device_name(dev), "device_index": dev.index,
+            "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")) or None,
             "kernel_ms": roof["kernel_ms"], "frac": roof["frac"], "parity_sample_buffers": nchk, "parity": rank_parity}
     if world > 1:
         ranks = [None] * world

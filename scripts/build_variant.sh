@@ -1,0 +1,7 @@
+#!/bin/bash
+# Build an A/B variant of the library into ab/lib<NAME>.so with extra compile flags (own build dir).
+#   scripts/build_variant.sh B "-DAMDCRC_LIST_STREAM=0"
+set -e
+cd "$(dirname "$0")/../aws-crt-cpp_amd"
+n=$1; shift
+make -s -j8 BUILD=build_$n LIB=../ab/lib$n.so HIPFLAGS_EXTRA="$*" ../ab/lib$n.so

@@ -371,6 +371,40 @@ def test_list_front_pads_at_group_boundaries(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("shape", ["long_and_short", "empties_between", "odd_lengths", "one_buffer"])
+@pytest.mark.parametrize("alg", ["crc32", "crc32c"])
+def test_list_stream_shapes(engine, alg, shape):
+    """Ragged CRC32 / CRC32C lists on the list streaming scan: buffers of more than 32
+    tiles beside short ones (cross-tile combine through the group slots and the buffer word), empty
+    and sub-16-byte buffers between long ones (tiles without a main region on the waves' range
+    edges), lengths just past a tile at every alignment (front pads of nearly a whole tile), and one
+    buffer alone; seeds on every buffer."""
+    import torch
+
+    rng = random.Random(0x5712 + ALG[alg] + len(shape))
+    if shape == "long_and_short":
+        lens = [rng.choice([40 << 20, (24 << 20) + 48]) for _ in range(3)] + [rng.randrange(4097, 70000) for _ in range(120)]
+    elif shape == "empties_between":
+        lens = [rng.choice([0, 1, 7, 15, 16, 17, 31, 65536, 65536 + 16, 131072 - 16]) for _ in range(3000)]
+    elif shape == "odd_lengths":
+        lens = [rng.choice([4097, 4096 * 3 + 1, 65537, 65536 + 4095, 131073]) + rng.randrange(0, 32) for _ in range(1500)]
+    else:
+        lens = [(96 << 20) + 4096 + 13]
+    rng.shuffle(lens)
+    offs, pos = [], 0
+    for ln in lens:
+        pos = (pos + 15) // 16 * 16 + rng.randrange(16)
+        offs.append(pos)
+        pos += ln
+    d = dev_random(pos + 64, 0x5712 + len(lens))
+    seeds = [rng.getrandbits(32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64"])
 def test_checksum_batches(engine, alg):
     """aws_crt_amd_checksum_batches: 37 batches of one shape (more than one launch holds), each with its
