@@ -1531,55 +1531,41 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
 // ------------------------------------------------------------------------------------------
 // Ragged lists on the streaming scan (crc32_list_stream_kernel, round 3).  crc32_braid_kernel<POLY,
 // true> runs lists on a two-slot ring whose merged code paths (front-padded groups, tile walks) leave
-// the compiler inexact wait counts; this kernel is crc32_stream_kernel's one-path three-slot ring on
-// 8-byte words, with the list's tiles read through raw buffer resources:
-//  * Tile k of a buffer reads from base = its first real byte (the main start for k = 0, main start
-//    + k*TILE - pad after) with TILE - adj records (adj = pad for k = 0, else 0).  A lane's row offset
-//    is its offset in the virtual tile minus adj, clamped to the record count: the rows of the front
-//    pad come out negative (wrapped), clamp to the limit, and the range check returns zeros -- the
-//    virtual zeros the braid needs, with no masking in the scan and no traffic.  Past the wave's last
-//    group the placeholder rows go through a zero-record resource (no traffic either).
-//  * The head state enters lane l0 = (pad mod 512) / 8 at the start of the tile's first scanned group
-//    divided by X^j (X = x^(8*512), the row step; j = the pad's row in that group): the lane's words
-//    before the pad are zero, so its j row steps bring it to exactly s_h where the first real word
-//    joins (the X^(-j) columns follow the braid constants, kBraidXinvWord).
-//  * Waves own host-chosen tile ranges balanced by scanned groups (engine.cpp list_impl): d_wave_buf
-//    holds the start buffer of each wave, then the start tiles (nw + 1) and the group prefix (nw + 1).
-struct LCur {          // one tile of one buffer (wave-uniform)
-    uint64_t b, k, T;  // buffer, tile within it, tiles of the buffer
-    uint64_t t;        // global tile index
-    uint64_t vb;       // virtual start of the buffer's tile 0 (main start - pad)
-    uint64_t base;     // resource base of this tile
-    uint32_t pad;      // the buffer's front pad
-    uint32_t adj, nrec, gs;  // offset adjustment, records, first scanned group (G: none)
+// the compiler inexact wait counts.  This kernel is crc32_stream_kernel's one-path three-slot ring on
+// 8-byte words, with no tiles at all:
+//  * A buffer's main region is front-padded to whole 4 KiB groups (pad < 4096) and the list is one
+//    sequence of groups.  Wave w scans groups [wq[w], wq[w+1]) of it -- an even split, cut anywhere,
+//    so every wave scans the same bytes (+-1 group) whatever the buffer lengths.
+//  * Group g of a buffer reads through a raw buffer resource based at its first real byte, with the
+//    group's real bytes as records (4096, or 4096 - pad for group 0).  A lane's row offset is its
+//    offset in the virtual group minus the pad (group 0), clamped to the record count: the pad's rows
+//    come out negative (wrapped), clamp to the limit, and the range check returns zeros -- the virtual
+//    zeros the braid needs, with no masking and no traffic.  Past the wave's last group the
+//    placeholder rows go through a zero-record resource.
+//  * The part of a buffer one wave scans ends with its share XOR_l u_l K_l (relative to the part's
+//    end) moved to the buffer's end: times x^(8*4096*m) for the m groups after the part, one scalar
+//    column product per set bit of m (columns of x^(8*4096*2^i) follow the braid constants).  A
+//    buffer inside one wave finishes at once; otherwise every part XORs its share into the buffer's
+//    accumulator and adds its group count, and the part that completes the count finishes it.
+//  * The head state enters lane l0 = (pad mod 512) / 8 at the start of group 0 divided by X^j
+//    (X = x^(8*512), the row step; j = the pad's row): the lane's words before the pad are zero, so
+//    its j row steps bring it to exactly s_h where the first real word joins (X^(-j) columns).
+//  * Buffers without a main region (under 16 aligned bytes) are folded whole by the wave whose range
+//    holds their place in the sequence.
+// Host side: engine.cpp list_stream (d_wave_buf = start buffer per wave, nw + 1; d_tile_prefix = start
+// group within it, nw + 1; then the group prefix wq, nw + 1; ntiles = groups in the list).
+struct LBuf {        // the cursor's buffer (wave-uniform)
+    uint64_t b;      // buffer index
+    uint64_t vb;     // virtual start of group 0 (main start - pad)
+    uint32_t vg;     // groups (0: no main region)
+    uint32_t pad;    // virtual zero bytes in front of main (< 4096)
 };
-
-__device__ __forceinline__ void lcur_tile(LCur &c, uint64_t k, uint64_t tile_bytes, uint32_t G, bool has_main) {
-    c.k = k;
-    c.adj = k == 0 ? c.pad : 0u;
-    c.base = c.vb + k * tile_bytes + c.adj;
-    c.nrec = (uint32_t)(tile_bytes - c.adj);
-    c.gs = !has_main ? G : k == 0 ? c.pad / kWaveGroupBytes : 0u;
-}
-
-// the cursor on tile t of buffer b
-__device__ __forceinline__ void lcur_at(const ScanParams &p, LCur &c, uint64_t b, uint64_t t, uint64_t tile_bytes, uint32_t G) {
+__device__ __forceinline__ LBuf lbuf_at(const ScanParams &p, uint64_t b) {
     const Edges e = buffer_edges<true>(p, b);
-    const uint64_t mainlen = e.tail - e.headend;
-    const uint64_t t0 = sload64(p.d_tile_prefix + b), t1 = sload64(p.d_tile_prefix + b + 1);
-    c.b = b;
-    c.T = t1 - t0;
-    c.t = t;
-    c.pad = mainlen ? (uint32_t)(c.T * tile_bytes - mainlen) : 0u;
-    c.vb = e.headend - c.pad;
-    lcur_tile(c, t - t0, tile_bytes, G, mainlen != 0);
-}
-
-__device__ __forceinline__ void lcur_next(const ScanParams &p, LCur &c, uint64_t tile_bytes, uint32_t G) {
-    if (c.k + 1 < c.T)
-        lcur_tile(c, c.k + 1, tile_bytes, G, true), ++c.t;
-    else
-        lcur_at(p, c, c.b + 1, c.t + 1, tile_bytes, G);
+    const uint64_t m = e.tail - e.headend;
+    const uint64_t vg = (m + kWaveGroupBytes - 1) / kWaveGroupBytes;
+    const uint32_t pad = (uint32_t)(vg * kWaveGroupBytes - m);
+    return LBuf{b, e.headend - pad, (uint32_t)vg, pad};
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint64_t base, uint32_t nrec) {
@@ -1633,42 +1619,39 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
-    const uint64_t *wtile = p.d_wave_buf + nw, *wq = p.d_wave_buf + 2 * nw + 1;
-    const uint64_t t0 = sload64(wtile + gw), t1 = sload64(wtile + gw + 1);
+    const uint64_t *wbuf = p.d_wave_buf, *woff = p.d_tile_prefix, *wq = p.d_tile_prefix + nw + 1;
+    const uint64_t b0 = sload64(wbuf + gw), b_end = sload64(wbuf + gw + 1);
+    const uint32_t g0 = (uint32_t)sload64(woff + gw);
     const uint32_t nq = (uint32_t)(sload64(wq + gw + 1) - sload64(wq + gw));  // groups of this wave
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint64_t tile_bytes = (uint64_t)p.seg * kWave;
     const uint32_t lo8 = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const bool work = t0 < t1;
     const uint64_t *xinv = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidXinvWord);
+    const uint64_t *gsh = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGshiftWord);
 
-    // scan cursor (sc) and prefetch cursor (fc, group fg): both start on the wave's first tile
-    LCur sc{};
-    if (work) lcur_at(p, sc, sload64(p.d_wave_buf + gw), t0, tile_bytes, G);
-    LCur fc = sc;
-    // the prefetch cursor skips tiles without a main region (there are nq groups ahead of it)
+    // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
+    const bool owns = b0 < b_end || nq;  // b0 < nbuf then (the host's wbuf is nbuf only past the groups)
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0};
+    uint32_t fq = 0, fg = g0;
     if (nq)
-        while (fc.gs >= G) lcur_next(p, fc, tile_bytes, G);
-    uint32_t fq = 0, fg = fc.gs;
-    auto f_rsrc = [&]() { return fq < nq ? list_rsrc(fc.base, fc.nrec) : list_rsrc(dummy, 0u); };
-    auto f_off = [&]() { return fq < nq ? fg * kWaveGroupBytes + lo8 - fc.adj : lo8; };
-    auto f_lim = [&]() { return fq < nq ? fc.nrec : 0u; };
+        while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
+    auto f_adj = [&]() -> uint32_t { return fg == 0 ? fc.pad : 0u; };
+    auto f_rsrc = [&]() {
+        return fq < nq ? list_rsrc(fc.vb + (uint64_t)fg * kWaveGroupBytes + f_adj(), kWaveGroupBytes - f_adj())
+                       : list_rsrc(dummy, 0u);
+    };
+    auto f_off = [&]() { return fq < nq ? lo8 - f_adj() : lo8; };
+    auto f_lim = [&]() { return fq < nq ? kWaveGroupBytes - f_adj() : 0u; };
     auto f_next = [&]() {
         if (++fq >= nq) return;
-        if (++fg == G) {
-            do lcur_next(p, fc, tile_bytes, G);
-            while (fc.gs >= G);
-            fg = fc.gs;
+        if (++fg == fc.vg) {
+            do fc = lbuf_at(p, fc.b + 1);
+            while (fc.vg == 0);
+            fg = 0;
         }
     };
     const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + SS::kKWord + 4 * threadIdx.x);
-    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x), pce1 = *(gu32 *)(pcs + threadIdx.x + SS::kBlock);
     // the two primed slots are issued unconditionally (a wave without groups issues zero-record
-    // placeholders): conditional issues give the compiler's wait-count pass paths where one slot is
-    // in flight and the other is not, and its merged state at the scan loop's header then drained
-    // the ring once per loop iteration
+    // placeholders), so the compiler's wait-count pass sees one prologue shape
     W8Group ra, rb, rc;
     list_issue<0>(ra, f_rsrc(), f_off(), f_lim());
     f_next();
@@ -1691,10 +1674,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     list_issue<0>(rb, f_rsrc(), f_off(), f_lim());
     f_next();
     bool consts_ready = false;
-    auto publish_consts = [&]() {
+    auto publish_consts = [&]() {  // the K image only (no tile columns)
         *(v4u *)(cb + 16 * threadIdx.x) = kq;
-        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * threadIdx.x) = pce0;
-        *(uint32_t *)(cb + (kPcolOff - kBKOff) + 4 * (threadIdx.x + SS::kBlock)) = pce1;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add((uint32_t *)(cb + (kConstFlagOff - kBKOff)), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
@@ -1705,40 +1686,58 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             __builtin_amdgcn_s_sleep(1);
         consts_ready = true;
     };
-    // a buffer without a main region (under 16 aligned bytes): its head fold is the whole CRC
+    // scan cursor: buffer sc, group g, the part's first group ga
+    LBuf sc = fc;
+    if (owns) sc = lbuf_at(p, b0);
+    // a buffer without a main region: its head fold is the whole CRC
     auto finish_empty = [&]() {
         const uint32_t s_h = head_state<true>(p, sc.b, eng);
         if (lane == 0) finalize<true>(p, sc.b, s_h, eng);
     };
-    // leading tiles without a main region
-    if (work)
-        while (sc.gs >= G) {
+    // leading buffers without a main region (with groups to scan, the first buffer that has some may
+    // lie past b_end: the next wave then starts inside it)
+    if (owns)
+        while (sc.vg == 0) {
             finish_empty();
-            if (sc.t + 1 >= t1) break;
-            lcur_next(p, sc, tile_bytes, G);
+            if (!nq && sc.b + 1 >= b_end) break;
+            sc = lbuf_at(p, sc.b + 1);
         }
     if (!nq) {
         publish_consts();
         ring_drain(ra, rb, rb);
         return;
     }
-
-    uint32_t g = sc.gs, u = 0, q = 0;
-    // a tile's first scanned group: the head state (tile 0) enters its lane, divided by X^j
-    auto tile_begin = [&]() {
-        g = sc.gs;
+    uint32_t g = g0, ga = g0, u = 0, q = 0;
+    // a part's first group: the head state (group 0) enters its lane, divided by X^j
+    auto part_begin = [&]() {
+        ga = g;
         u = 0;
-        if (sc.k == 0) {
+        if (g == 0) {
             uint32_t s_h = head_state<true>(p, sc.b, eng);
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
-    tile_begin();
-    BGroupAcc acc{};
-    acc.slot = ~0ull;
-    const LocalBufs lb{0, 0};
+    // the part [ga, g) ends: its share, moved to the buffer's end, finishes the buffer or joins it
+    auto part_finish = [&]() {
+        uint32_t r = wave_xor_s(eng.mulK(u, lane));
+        for (uint32_t m = sc.vg - g, i = 0; m; m >>= 1, ++i)
+            if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
+        if (lane != 0) return;
+        if (ga == 0 && g == sc.vg) {
+            finalize<true>(p, sc.b, r, eng);
+            return;
+        }
+        (void)sx_xor64_ret(&p.d_acc[sc.b], (unsigned long long)r);  // performed before it is counted
+        const uint32_t n = g - ga, c = sx_add32_ret(&p.d_cnt[sc.b], n);
+        if (c + n == sc.vg) {
+            const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[sc.b], 0ull);
+            sx_store32(&p.d_cnt[sc.b], 0u);
+            finalize<true>(p, sc.b, fin, eng);
+        }
+    };
+    part_begin();
     auto step = [&](W8Group &cur, W8Group &nxt, bool first) {
         const __amdgpu_buffer_rsrc_t rs = f_rsrc();
         const uint32_t fo = f_off(), fl = f_lim();
@@ -1746,20 +1745,18 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         u = list_rows_w8<0, B>(u, typename B::Hi{}, cur, nxt, rs, fo, fl, eng);
         if (first) publish_consts();
         ++q;
-        if (++g == G) {
+        if (++g == sc.vg || q == nq) {
             await_consts();
-            Tile d;
-            d.b = sc.b, d.k = sc.k, d.T = sc.T, d.tbase = sc.t - sc.k;
-            d.vbase = 0, d.pad = 0, d.ngroups = G;
-            stream_finish<B, true>(p, d, u, eng, lane, acc, lb);
+            part_finish();
             if (q < nq) {
-                // the next tile with a main region, finishing the empty buffers on the way
+                // the next buffer with a main region, finishing the empty ones on the way
                 for (;;) {
-                    lcur_next(p, sc, tile_bytes, G);
-                    if (sc.gs < G) break;
+                    sc = lbuf_at(p, sc.b + 1);
+                    if (sc.vg) break;
                     finish_empty();
                 }
-                tile_begin();
+                g = 0;
+                part_begin();
             }
         }
     };
@@ -1774,12 +1771,11 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (q < nq) step(rc, rb, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
-    // trailing tiles without a main region
-    while (sc.t + 1 < t1) {
-        lcur_next(p, sc, tile_bytes, G);
+    // trailing buffers without a main region
+    while (sc.b + 1 < b_end) {
+        sc = lbuf_at(p, sc.b + 1);
         finish_empty();
     }
-    stream_publish<B, true>(p, acc, eng, lane);
 }
 
 // ------------------------------------------------------------------------------------------

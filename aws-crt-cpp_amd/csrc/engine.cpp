@@ -218,6 +218,16 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
             }
             for (int i = 0; i < 8 * 512; ++i) xj = inv_mulx32(xj, poly);
         }
+        // columns of x^(8*4096*2^i), i < 32 (the list streaming scan's part shifts)
+        uint64_t sq = gf2_xpow8n(4096, poly, 32);
+        for (int i = 0; i < 32; ++i) {
+            uint32_t col = (uint32_t)sq;
+            for (int j = 0; j < 32; ++j) {
+                c[kBraidGshiftWord + 2 * (32 * i + j)] = col;
+                col = (uint32_t)gf2_mulx(col, poly);
+            }
+            sq = gf2_mulmod(sq, sq, poly, 32);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
@@ -372,24 +382,20 @@ constexpr uint64_t kLaneStrided64Max = AMDCRC_LANE64_MAX;
 constexpr uint64_t kLaneStrided64MinBuffers = 65536;
 // Strided XXH3 batches whose buffers hold at least this many full 1 KiB blocks take the split path
 constexpr uint64_t kXxh3SplitBlocks = 4096;
-// Ragged CRC32 / CRC32C lists: crc32_list_stream_kernel (0 keeps crc32_braid_kernel<POLY, true>), with
-// tiles for kListStreamTilesPerSlot per wave slot (finer tiles even out the waves' scanned groups), on
+// Ragged CRC32 / CRC32C lists: crc32_list_stream_kernel (0 keeps crc32_braid_kernel<POLY, true>), on
 // two 512-thread workgroups per CU once a list holds kListTwoPerCuBytes of main bytes
 #ifndef AMDCRC_LIST_STREAM  // compile-time only (A/B builds)
 #define AMDCRC_LIST_STREAM 1
-#endif
-#ifndef AMDCRC_LIST_TILES_PER_SLOT
-#define AMDCRC_LIST_TILES_PER_SLOT 1
 #endif
 #ifndef AMDCRC_LIST_TWO_PER_CU
 #define AMDCRC_LIST_TWO_PER_CU (64ull << 20)
 #endif
 constexpr bool kListStream = AMDCRC_LIST_STREAM != 0;
-constexpr uint64_t kListStreamTilesPerSlot = AMDCRC_LIST_TILES_PER_SLOT;
 constexpr uint64_t kListTwoPerCuBytes = AMDCRC_LIST_TWO_PER_CU;
-uint64_t list_stream_blocks(const Device *d, uint64_t ntiles, uint64_t total_main) {
+// workgroups of a list launch: 8 waves each, at most one wave per 8 groups (4 KiB each)
+uint64_t list_stream_blocks(const Device *d, uint64_t ngroups, uint64_t total_main) {
     const uint64_t per_cu = total_main >= kListTwoPerCuBytes ? 2 : 1;
-    return std::max<uint64_t>(1, std::min<uint64_t>((ntiles + 7) / 8, (uint64_t)d->cus * per_cu));
+    return std::max<uint64_t>(1, std::min<uint64_t>((ngroups + 63) / 64, (uint64_t)d->cus * per_cu));
 }
 
 struct ScanGeometry {
@@ -777,33 +783,20 @@ int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
 }
 
 // Ragged CRC32 / CRC32C lists on crc32_list_stream_kernel.  Every buffer's main
-// region is T = ceil(main / TILE) tiles, front-padded to whole tiles; tile 0 scans its groups from the
-// one holding the pad's end.  The waves' tile ranges are cut at the tile boundaries nearest to an even
-// split of the scanned groups.  Descriptor block: ptrs[count] lens[count] tile prefix[count + 1], then
-// per wave its start buffer [nw], start tile [nw + 1] and group prefix [nw + 1].
+// region is front-padded to whole 4 KiB groups; the list is one sequence of groups, split evenly over
+// the waves (cut anywhere, also inside a buffer).  Wave w walks buffers [wbuf[w], wbuf[w + 1]) from
+// group woff[w] of the first, scans groups [wq[w], wq[w + 1]) of the sequence and folds the buffers
+// without a main region whose place in the sequence falls in its range.  Descriptor block:
+// ptrs[count] lens[count] wbuf[nw + 1] woff[nw + 1] wq[nw + 1].
 int list_stream(Device *d, int alg, const void *const *ptrs, const size_t *lens, size_t count,
-                const std::vector<uint64_t> &mains, uint64_t total, uint32_t seg, const void *d_seeds, void *d_out,
-                hipStream_t s) {
-    const uint64_t tile = (uint64_t)seg * kWave, G = seg / kGroupBytes, gbytes = tile / G;
-    std::vector<uint64_t> prefix(count + 1, 0), gp(count + 1, 0), gs(count, 0);
-    uint64_t tmax = 1;
-    for (size_t i = 0; i < count; ++i) {
-        const uint64_t T = mains[i] ? (mains[i] + tile - 1) / tile : 1;
-        gs[i] = mains[i] ? (T * tile - mains[i]) / gbytes : G;  // first scanned group of tile 0
-        tmax = std::max(tmax, T);
-        prefix[i + 1] = prefix[i] + T;
-        gp[i + 1] = gp[i] + (mains[i] ? T * G - gs[i] : 0);
-    }
-    const uint64_t ntiles = prefix[count], ng = gp[count];
-    const uint64_t blocks = list_stream_blocks(d, ntiles, total), nw = blocks * 8;
-    // group prefix at tile t (t < ntiles), and the tile holding group q (q < ng)
-    auto tile_buf = [&](uint64_t t) { return (uint64_t)(std::upper_bound(prefix.begin(), prefix.end(), t) - prefix.begin()) - 1; };
-    auto gstart = [&](uint64_t t) {
-        if (t >= ntiles) return ng;
-        const uint64_t b = tile_buf(t), k = t - prefix[b];
-        return mains[b] == 0 || k == 0 ? gp[b] : gp[b] + (G - gs[b]) + (k - 1) * G;
-    };
-    const size_t words = count * 2 + (count + 1) + nw + 2 * (nw + 1);
+                const std::vector<uint64_t> &mains, uint64_t total, const void *d_seeds, void *d_out, hipStream_t s) {
+    constexpr uint64_t gb = 4096;  // bytes per wave group
+    std::vector<uint64_t> gp(count + 1, 0);
+    bool split = false;
+    for (size_t i = 0; i < count; ++i) gp[i + 1] = gp[i] + (mains[i] + gb - 1) / gb;
+    const uint64_t ng = gp[count];
+    const uint64_t blocks = list_stream_blocks(d, ng, total), nw = blocks * 8;
+    const size_t words = count * 2 + 3 * (nw + 1);
     uint64_t *h;
     int rc = stage_begin(d, s, words * 8, (void **)&h);
     if (rc) return rc;
@@ -811,43 +804,40 @@ int list_stream(Device *d, int alg, const void *const *ptrs, const size_t *lens,
         h[i] = (uint64_t)(uintptr_t)ptrs[i];
         h[count + i] = lens[i];
     }
-    std::memcpy(h + 2 * count, prefix.data(), (count + 1) * 8);
-    uint64_t *wbuf = h + 3 * count + 1, *wtile = wbuf + nw, *wq = wtile + nw + 1;
+    uint64_t *wbuf = h + 2 * count, *woff = wbuf + nw + 1, *wq = woff + nw + 1;
+    // wave w starts at the first buffer that ends past q0 = w * ng / nw, or at a buffer without a main
+    // region whose place is q0 (those come first in index order); both cursors only move forward
+    size_t b = 0;
     for (uint64_t w = 0; w <= nw; ++w) {
-        uint64_t t;
-        if (w == 0) {
-            t = 0;
-        } else if (w == nw || ng == 0) {
-            t = ntiles;
+        const uint64_t q0 = w == nw ? ng : w * ng / nw;
+        if (w == nw) {
+            b = count;
         } else {
-            const uint64_t q = w * ng / nw;
-            const uint64_t b = (uint64_t)(std::upper_bound(gp.begin(), gp.end(), q) - gp.begin()) - 1;  // main > 0
-            const uint64_t qq = q - gp[b], g0 = G - gs[b];
-            const uint64_t k = qq < g0 ? 0 : 1 + (qq - g0) / G;
-            const uint64_t gt = k == 0 ? g0 : G, at = k == 0 ? 0 : g0 + (k - 1) * G;
-            t = prefix[b] + k + (2 * (qq - at) > gt ? 1 : 0);  // the nearer boundary of that tile
+            while (b < count && gp[b + 1] <= q0 && !(gp[b + 1] == gp[b] && gp[b] >= q0)) ++b;
         }
-        wtile[w] = std::max<uint64_t>(t, w ? wtile[w - 1] : 0);
-        wq[w] = gstart(wtile[w]);
-        if (w < nw) wbuf[w] = wtile[w] < ntiles ? tile_buf(wtile[w]) : count - 1;
+        wbuf[w] = b;
+        wq[w] = q0;
+        woff[w] = b < count && gp[b + 1] > gp[b] ? q0 - gp[b] : 0;
+        if (woff[w]) split = true;
     }
     const uint64_t *dd;
     if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;
     ScanParams p{};
-    p.seg = seg;
+    p.seg = kGroupBytes;
     p.list_mode = 1;
     p.stream = 4;
     p.nbatch = 1;
     p.bcount = count;
     p.d_ptrs = dd;
     p.d_lens = dd + count;
-    p.d_tile_prefix = dd + 2 * count;
-    p.d_wave_buf = dd + 3 * count + 1;
+    p.d_wave_buf = dd + 2 * count;
+    p.d_tile_prefix = dd + 2 * count + nw + 1;
     p.nbuf = count;
-    p.ntiles = ntiles;
+    p.ntiles = ng;
     p.d_seeds = d_seeds;
     p.d_out = d_out;
-    return launch_scan(d, alg, p, count, tmax, total, s);
+    // a buffer cut between waves combines through the per-buffer accumulator and count (workspace)
+    return launch_scan(d, alg, p, count, split ? 2 : 1, total, s);
 }
 
 int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, size_t count, const void *d_seeds,
@@ -884,17 +874,16 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     }
     uint32_t seg = kGroupBytes;
     uint64_t tile = 0;
-    const bool lstream = kListStream && !xxh && width_of(alg) == 32;
+    if (kListStream && !xxh && width_of(alg) == 32) return list_stream(d, alg, ptrs, lens, count, mains, total, d_seeds, d_out, s);
     if (!xxh) {
         std::vector<uint64_t> sorted(mains);
         std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
-        seg = choose_seg(d, total, sorted[count / 2], lstream ? kListStreamTilesPerSlot : 1);
+        seg = choose_seg(d, total, sorted[count / 2]);
 #ifdef AMDCRC_XP_LIST_SEG_DIV  // experiment builds only: smaller list tiles (balance vs finishes)
         seg = std::max<uint32_t>(kGroupBytes, seg / AMDCRC_XP_LIST_SEG_DIV);
 #endif
         tile = (uint64_t)seg * kWave;
     }
-    if (lstream) return list_stream(d, alg, ptrs, lens, count, mains, total, seg, d_seeds, d_out, s);
     // descriptor block: ptrs[count] lens[count] prefix[count+1] wavebuf[nwaves]
     std::vector<uint64_t> prefix(count + 1, 0);
     uint64_t tmax = 1;

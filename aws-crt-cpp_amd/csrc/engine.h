@@ -45,8 +45,9 @@ struct ScanParams {
     const uint64_t *d_ptrs;        // list: device addresses
     const uint64_t *d_lens;        // list: lengths
     const uint64_t *d_tile_prefix; // list: exclusive prefix of T_b (nbuf + 1 entries)
-    const uint64_t *d_wave_buf;    // list: buffer index holding each wave's first tile (stream 4: then the
-                                   // waves' first tiles, nw + 1, and their group prefix, nw + 1)
+    const uint64_t *d_wave_buf;    // list: buffer index holding each wave's first tile (stream 4: each
+                                   // wave's first buffer, nw + 1 entries; d_tile_prefix then holds its
+                                   // first group in that buffer, nw + 1, and the group prefix, nw + 1)
     uint64_t nbuf;
     uint64_t ntiles;
     // ---- seeds (previous CRC, finalised) and results
@@ -92,11 +93,13 @@ struct ScanParams {
 //   [5376, 7424)  K-matrix image of x^(-128 l) (the streaming scan's 16-byte words), same layout
 //   [7424, 7936)  columns (u64) of X^(-j), X = x^(8*512), j < 8: the list streaming scan's head-state
 //                 entry (crc32_list_stream_kernel)
+//   [7936, 9984)  columns (u64) of x^(8*4096*2^i), i < 32: the list streaming scan's part shifts
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 7936;
-constexpr int kBraidXinvWord = 7424;  // first word of the X^(-j) columns
+constexpr int kBraidConstWords = 9984;
+constexpr int kBraidXinvWord = 7424;    // first word of the X^(-j) columns
+constexpr int kBraidGshiftWord = 7936;  // first word of the x^(8*4096*2^i) columns
 constexpr int kBraidK64Word = 3328;   // first word of the x^(-64 l) K image
 constexpr int kBraidK128Word = 5376;  // first word of the x^(-128 l) K image
 
