@@ -86,6 +86,14 @@ __device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
     return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
                       __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
 }
+__device__ __forceinline__ uint32_t wave_add_s(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) + __builtin_amdgcn_readlane((int)v, 16) +
+                      __builtin_amdgcn_readlane((int)v, 32) + __builtin_amdgcn_readlane((int)v, 48));
+}
 __device__ __forceinline__ uint64_t wave_xor64_s(uint64_t v) {
     const uint32_t lo = wave_xor_s((uint32_t)v), hi = wave_xor_s((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
@@ -1084,6 +1092,8 @@ template <int R>
 __device__ __forceinline__ uint64_t gld_w8(uint32_t voff, uint64_t sbase) {
     return __builtin_nontemporal_load((gu64 *)(sbase + voff + R * kW8Row));
 }
+template <int R>
+__device__ __forceinline__ void stream_issue(W8Group &g, uint32_t voff, uint64_t s);
 
 // 8-byte rows: x = u ^ lo(w_r) is the chained value; the hi lookups of row r are issued with row
 // r - 1's chain step and XORed in at row r (h = row r - 1's hi part).  One row ahead measured 0.4-1 %
@@ -1092,7 +1102,11 @@ template <int R, class B>
 __device__ __forceinline__ uint32_t stream_rows_w8(uint32_t x, typename B::Hi h, W8Group &cur, W8Group &nxt, uint32_t voff,
                                                    uint64_t snext, const B &eng) {
     if constexpr (R < kW8RowsPerGroup) {
+#ifdef AMDCRC_XP_ISSUE_AHEAD  // experiment builds only: the next slot's eight loads all issued at row 0
+        if constexpr (R == 0) stream_issue<0>(nxt, voff, snext);
+#else
         nxt.w[R] = gld_w8<R>(voff, snext);
+#endif
         typename B::Hi hn;
         if constexpr (R == 0) {
             x ^= (uint32_t)cur.w[0];
@@ -1356,6 +1370,13 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
+#ifdef AMDCRC_XP_V4ORDER  // experiment builds only (timing; results wrong): XCD-window 16 KiB chunk order
+        if (fq < nq) {
+            const uint64_t xcd = blockIdx.x & 7, j = (blockIdx.x >> 3) * WAVES + wv, nwx = nw / 8;
+            const uint64_t ngt = p.ntiles << gsh, grp = xcd * (ngt / 8) + (j + (fq / 4) * nwx) * 4 + fq % 4;
+            return rfl64(p.base + hoff + grp * 4096);
+        }
+#endif
         uint64_t a = fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
         if (!AMDCRC_GUARD_OK(fq >= nq || p.nbatch > 1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
                                                                  p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
@@ -1504,6 +1525,29 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // pass reached the loop header with a merged state in which the slot about to be loaded still had
     // loads in flight, and drained most of the ring at the top of every rotation (vmcnt 7..2 before the
     // first step's row loads); without the breaks every row waits exactly vmcnt(16).
+#ifdef AMDCRC_XP_RING4  // experiment builds only: a four-slot ring (three groups ahead)
+    Grp rd;
+    stream_issue<0>(rc, voff, f_addr());
+    f_next();
+    step(ra, rd, true);
+    while (q + 4 <= nq) {
+        step(rb, ra, false);
+        step(rc, rb, false);
+        step(rd, rc, false);
+        step(ra, rd, false);
+    }
+    if (q < nq) {
+        step(rb, ra, false);
+        if (q < nq) step(rc, rb, false);
+        if (q < nq) step(rd, rc, false);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R8W(ra)::"memory");
+    asm volatile("" : AMDCRC_R8W(rb));
+    asm volatile("" : AMDCRC_R8W(rc));
+    asm volatile("" : AMDCRC_R8W(rd));
+    stream_publish(p, acc, eng, lane);
+    return;
+#endif
     step(ra, rc, true);
 #ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
     while (q < nq) {
@@ -2264,7 +2308,14 @@ template <int R, class B>
 __device__ __forceinline__ uint64_t stream64_rows(uint64_t x, B64Group &cur, B64Group &nxt, uint32_t voff, uint64_t snext,
                                                   const B &eng) {
     if constexpr (R < kB64RowsPerGroup) {
+#ifdef AMDCRC_XP_ISSUE_AHEAD  // experiment builds only: the next slot's eight loads all issued at row 0
+        if constexpr (R == 0) {
+#pragma unroll
+            for (int k = 0; k < kB64RowsPerGroup; ++k) nxt.w[k] = __builtin_nontemporal_load((gu64 *)(snext + voff + k * kB64Row));
+        }
+#else
         nxt.w[R] = gld_row64<R>(voff, snext);
+#endif
         x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
         __builtin_amdgcn_sched_barrier(0);
         return stream64_rows<R + 1>(x, cur, nxt, voff, snext, eng);
@@ -2357,6 +2408,13 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
+#ifdef AMDCRC_XP_V4ORDER  // experiment builds only (timing; results wrong): XCD-window 16 KiB chunk order
+        if (fq < nq) {
+            const uint64_t xcd = blockIdx.x & 7, j = (blockIdx.x >> 3) * kBraidWaves + (threadIdx.x >> 6), nwx = nw / 8;
+            const uint64_t ngt = p.ntiles << gsh, grp = xcd * (ngt / 8) + (j + (fq / 4) * nwx) * 4 + fq % 4;
+            return rfl64(p.base + hoff + grp * 4096);
+        }
+#endif
         return rfl64(fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup) : dummy);
     };
     auto f_next = [&]() {
@@ -2437,6 +2495,248 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
 #endif
 }
 
+
+// ------------------------------------------------------------------------------------------
+// W = 64 scan of long uniform buffers in XCD windows (crc64_xcd_kernel, round 3).  Streaming reads
+// ran 4-10 % faster when the waves of one XCD read neighbouring 4-16 KiB pieces of one window than
+// when every wave streams its own contiguous range (aws-crt-cpp_amd/tools/readpattern.hip; with the
+// CRC64 scan's slower waves the gap was 6 %: profiles/r03/order).  So the launch's main bytes, all
+// buffers' main regions in order, are cut into chunks of kXcdChunkGroups 4 KiB groups; XCD x
+// (blockIdx mod 8 under round-robin dispatch) takes the x-th eighth of the chunks, and its nwx waves
+// take chunks j, j + nwx, j + 2 nwx, ... of that eighth (j = the wave's index in the XCD).
+//  * Inside a chunk a wave runs crc64_stream4_kernel's rows (8-byte lane words, 512-byte rows, the
+//    4-copy tables, the three-slot ring).
+//  * A wave's next chunk in the same buffer starts (nwx - 1) chunks past the end of the last one; every
+//    lane's braid jumps there with u <- u * J, J = x^(8 * chunk * (nwx - 1)), from nibble tables of J in
+//    LDS (16 broadcast-friendly reads; ScanParams::d_pcols holds them and the shift columns).
+//  * A part (the wave's chunks of one buffer) ends with the stream kernel's tile finish (lane shares
+//    K_l, wave XOR), moved to the buffer end by x^(8 * chunk * m), m = chunks after its last one (one
+//    column product per set bit of m), then XORed into the buffer's accumulator; the part adds its
+//    chunk count, and the part completing the buffer's count finalises it.
+// Taken by strided CRC64NVME launches whose main regions are whole chunks of at least kXcdMinChunks.
+constexpr int kXcdChunkGroups = AMDCRC_XCD_CHUNK_GROUPS;
+constexpr uint32_t kXcdChunk = kXcdChunkGroups * kB64Row * kB64RowsPerGroup;
+constexpr uint32_t kXcdJumpOff = kB64x4Lds;               // 16 nibbles x 16 x u64: v << 4n times J
+constexpr uint32_t kXcdSlotOff = kXcdJumpOff + 16 * 16 * 8;  // two held parts per wave (b, value, chunks)
+constexpr uint32_t kXcdLds = kXcdSlotOff + 16 * 32;
+static_assert(2 * kXcdLds <= 160 * 1024, "two crc64_xcd_kernel workgroups per CU");
+
+__device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u) {
+    const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    uint64_t v[16];
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+        v[n] = lds64(lds, kXcdJumpOff + 128u * n + 8u * ((lo >> (4 * n)) & 15u));
+        v[8 + n] = lds64(lds, kXcdJumpOff + 128u * (8 + n) + 8u * ((hi >> (4 * n)) & 15u));
+    }
+    uint32_t rl = 0, rh = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n += 2) {
+        rl = xor3(rl, (uint32_t)v[n], (uint32_t)v[n + 1]);
+        rh = xor3(rh, (uint32_t)(v[n] >> 32), (uint32_t)(v[n + 1] >> 32));
+    }
+    return ((uint64_t)rh << 32) | rl;
+}
+
+// a wave-uniform walk over the chunks j, j + nwx, ... of [lo, hi): chunk k of buffer b
+struct XcdCursor {
+    uint64_t b, k;      // buffer, chunk in buffer
+    uint64_t main;      // main-region address of buffer b
+};
+
+template <uint64_t POLY>
+__global__ __launch_bounds__(512, 4) void crc64_xcd_kernel(const ScanParams p) {
+    using B = Braid64<POLY, 4>;
+    __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
+    constexpr int kWaves = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwx = (uint64_t)gridDim.x * kWaves / 8;  // waves per XCD (gridDim % 8 == 0)
+    const uint64_t xcd = blockIdx.x & 7u;
+    const uint64_t j = rfl64((uint64_t)(blockIdx.x >> 3) * kWaves + (threadIdx.x >> 6));
+    const uint64_t NC = p.ntiles, CPB = p.tiles_per_buf;
+    const uint64_t xlo = xcd * NC / 8, xhi = (xcd + 1) * NC / 8;
+    const uint64_t c0 = xlo + j;
+    const uint32_t nchunks = c0 < xhi ? (uint32_t)((xhi - c0 + nwx - 1) / nwx) : 0u;
+    const uint32_t nq = nchunks * kXcdChunkGroups;  // groups of this wave
+    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
+    const uint32_t voff = 8u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
+    const uint64_t dq = nwx / CPB, dr = nwx - dq * CPB;   // chunk step as (buffers, chunks)
+    auto cur_at = [&](uint64_t c) -> XcdCursor {
+        const uint64_t b = c / CPB;
+        const BatchPos bp = batch_pos(p, b);
+        return XcdCursor{b, c - b * CPB, karg64(p.bbase, bp.j) + bp.i * p.stride + hoff};
+    };
+    auto cur_next = [&](XcdCursor &x) {
+        uint64_t b = x.b + dq, k = x.k + dr;
+        if (k >= CPB) k -= CPB, ++b;
+        if (b != x.b) {
+            const BatchPos bp = batch_pos(p, b);
+            x.main = karg64(p.bbase, bp.j) + bp.i * p.stride + hoff;
+        }
+        x.b = b, x.k = k;
+    };
+    // prefetch cursor: chunk fc, group fg; fq groups issued
+    XcdCursor fc = nq ? cur_at(c0) : XcdCursor{0, 0, 0};
+    uint32_t fq = 0, fg = 0;
+    auto f_addr = [&]() -> uint64_t {
+        return rfl64(fq < nq ? fc.main + fc.k * kXcdChunk + (uint64_t)fg * (kB64Row * kB64RowsPerGroup) : dummy);
+    };
+    auto f_next = [&]() {
+        ++fq;
+        if (++fg == (uint32_t)kXcdChunkGroups) {
+            fg = 0;
+            if (fq < nq) cur_next(fc);
+        }
+    };
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
+    const uint64_t jt = threadIdx.x < 256 ? *(gu64 *)(p.d_pcols + threadIdx.x) : 0ull;
+    B64Group ra, rb, rc;
+    if (nq) {
+        stream64_issue<0>(ra, voff, f_addr());
+        f_next();
+    }
+    b64x4_build_tables<POLY>(lds);
+    b64x4_build_nib<POLY>(lds, kl);
+    if (threadIdx.x < 256) *(uint64_t *)(lds + kXcdJumpOff + 8u * threadIdx.x) = jt;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    const uint64_t *shcols = p.d_pcols + 256;        // columns of x^(8 * chunk * 2^i), i < 40
+    const uint64_t *bytecols = p.d_pcols + 256 + 40 * 64;  // [level][v][j]: x^(8 * chunk * v * 256^level) * x^j
+    uint64_t pb = ~0ull, pk = 0;  // the open part: buffer, last chunk
+    uint32_t pn = 0;              // chunks in the part
+    uint64_t u = 0;
+    // the open part's register (lane shares joined), at the end of its last chunk
+    auto part_raw = [&]() -> uint64_t { return wave_xor64_s(eng.mulK(u)); };
+    // r * x^(8 * chunk * m): one 64-column product per nonzero byte of m, the columns spread over the
+    // lanes (lane c holds column c, a coalesced 512-byte load; the four loads issue together) and the
+    // selected columns XORed across the wave.  Only where the payload ring is drained.
+    auto shift_lanes = [&](uint64_t r, uint64_t m) -> uint64_t {
+        uint64_t col[4];
+#pragma unroll
+        for (int L = 0; L < 4; ++L) {
+            const uint64_t v = (m >> (8 * L)) & 255u;
+            col[L] = v ? *(gu64 *)(bytecols + (256u * L + v) * 64 + lane) : 0ull;
+        }
+#pragma unroll
+        for (int L = 0; L < 4; ++L) {
+            if (((m >> (8 * L)) & 255u) == 0) continue;
+            const uint64_t sel = (r >> (63 - lane)) & 1u;
+            r = wave_xor64_s(sel ? col[L] : 0ull);
+        }
+        return r;
+    };
+    // the same product on the scalar unit (columns by SMEM): inside the scan, rarely
+    auto shift_scalar = [&](uint64_t r, uint64_t m) -> uint64_t {
+        for (int i = 0; m; ++i, m >>= 1)
+            if (m & 1) r = mul_pcols<uint64_t, 64>(r, shcols + 64 * i);
+        return r;
+    };
+    // value r of n chunks of buffer b into the buffer's accumulator; the part completing the count
+    // finalises the buffer (lane 0)
+    auto publish = [&](uint64_t b, uint64_t r, uint32_t n) {
+        (void)sx_xor64_ret(&p.d_acc[b], (unsigned long long)r);  // performed before it is counted
+        const unsigned int c = sx_add32_ret(&p.d_cnt[b], n);
+        if (c + n == (unsigned int)CPB) {
+            const uint64_t fin = sx_swap64_ret(&p.d_acc[b], 0ull);
+            sx_store32(&p.d_cnt[b], 0u);
+            finalize<false>(p, b, fin, eng);
+        }
+    };
+    // A part that ends inside the scan is held (one per wave) and published with the wave's last part:
+    // the waves of an XCD cross a buffer boundary at about the same step, and 512 returning atomics on
+    // one address at once would stall every one of them (with its payload ring drained).  An older held
+    // part is published at once.
+    uint64_t hb = ~0ull, hr = 0, hk = 0;  // the held part: buffer, raw register, last chunk, chunks
+    uint32_t hn = 0;
+    auto part_finish = [&]() {
+        const uint64_t r = part_raw();
+        if (hb != ~0ull) {
+            const uint64_t v = shift_scalar(hr, CPB - 1 - hk);
+            if (lane == 0) publish(hb, v, hn);
+        }
+        hb = pb, hr = r, hk = pk, hn = pn;
+    };
+    // every wave's held and last parts go through LDS: wave 0 joins the parts of one buffer, so the
+    // workgroup's eight waves (neighbouring chunks at every step) meet its accumulator once
+    auto final_parts = [&](bool have) {
+        const uint64_t r = have ? shift_lanes(part_raw(), CPB - 1 - pk) : 0ull;
+        const uint64_t h = hb != ~0ull ? shift_lanes(hr, CPB - 1 - hk) : 0ull;
+        if (lane == 0) {
+            uint64_t *slot = (uint64_t *)(lds + kXcdSlotOff) + 8 * (threadIdx.x >> 6);
+            slot[0] = have ? pb : ~0ull;
+            slot[1] = r;
+            slot[2] = have ? pn : 0u;
+            slot[4] = hb;
+            slot[5] = h;
+            slot[6] = hn;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (threadIdx.x >= 64) return;
+        // wave 0: entry e in lane e (< 16); one publication per distinct buffer
+        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane & 15);
+        uint64_t eb = lane < 16 ? slot[0] : ~0ull;
+        const uint64_t er = slot[1];
+        const uint32_t en = (uint32_t)slot[2];
+        for (int e = 0; e < 16; ++e) {
+            const uint64_t b = rfl64((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, e) |
+                                     ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), e) << 32));
+            if (b == ~0ull) continue;
+            const bool mine = eb == b;
+            const uint64_t r = wave_xor64_s(mine ? er : 0ull);
+            const uint32_t n = wave_add_s(mine ? en : 0u);
+            if (mine) eb = ~0ull;
+            if (lane == 0) publish(b, r, n);
+        }
+    };
+    if (!nq) {
+        final_parts(false);
+        return;
+    }
+    stream64_issue<0>(rb, voff, f_addr());
+    f_next();
+
+    XcdCursor sc = cur_at(c0);
+    uint32_t g = 0, q = 0;
+    auto step = [&](B64Group &cur, B64Group &nxt) {
+        if (g == 0) {
+            if (pn && sc.b == pb) {
+                u = xcd_jump(lds, u);
+            } else {
+                if (pn) part_finish();
+                pb = sc.b, pn = 0;
+                u = sc.k == 0 && lane == 0 ? head_state<false>(p, sc.b, eng) : 0ull;
+            }
+            ++pn, pk = sc.k;
+        }
+        const uint64_t sn = f_addr();
+        f_next();
+        u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
+        ++q;
+        if (++g == (uint32_t)kXcdChunkGroups) {
+            g = 0;
+            if (q < nq) cur_next(sc);
+        }
+    };
+    // whole rotations of three steps, then the rest (see crc32_stream_kernel)
+    while (q + 3 <= nq) {
+        step(ra, rc);
+        step(rb, ra);
+        step(rc, rb);
+    }
+    if (q < nq) {
+        step(ra, rc);
+        if (q < nq) step(rb, ra);
+    }
+    // the trailing placeholder rows land before the finish reuses registers
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]), "+v"(ra.w[5]),
+                 "+v"(ra.w[6]), "+v"(ra.w[7])::"memory");
+    asm volatile("" : "+v"(rb.w[0]), "+v"(rb.w[1]), "+v"(rb.w[2]), "+v"(rb.w[3]), "+v"(rb.w[4]), "+v"(rb.w[5]), "+v"(rb.w[6]), "+v"(rb.w[7]));
+    asm volatile("" : "+v"(rc.w[0]), "+v"(rc.w[1]), "+v"(rc.w[2]), "+v"(rc.w[3]), "+v"(rc.w[4]), "+v"(rc.w[5]), "+v"(rc.w[6]), "+v"(rc.w[7]));
+    final_parts(true);
+}
 
 // ------------------------------------------------------------------------------------------
 // W = 64 scan of many short uniform buffers (the C4 per-GPU shard: 131,072 x 8 KiB), 16 lanes per
@@ -3136,6 +3436,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
         case ALG_CRC64NVME:
             if (p->stream == 3 && !list)  // many short buffers: 16 lanes per buffer
                 launch(crc64_rows16_kernel<kPoly64Nvme>, nblocks, kR16Block, s, p, ev);
+            else if (p->stream == 5 && !list)  // long buffers: XCD-window chunks
+                launch(crc64_xcd_kernel<kPoly64Nvme>, nblocks, 512, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list)

@@ -94,6 +94,7 @@ struct Device {
     std::map<int, DevBuf> braid64;                     // alg -> W=64 braided-scan constants
     std::map<std::pair<int, uint64_t>, DevBuf> pcols;  // (alg, tile) -> tmax x W x u64
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
+    std::map<std::pair<int, uint64_t>, DevBuf> xcd;    // (alg, waves per XCD) -> crc64_xcd_kernel constants
     std::vector<DevBuf> retired;                       // outgrown buffers queued kernels may still read
     std::map<hipStream_t, Workspace> ws;
     std::map<hipStream_t, DevBuf> xsums;  // split XXH3 long path: per-block accumulator sums
@@ -258,6 +259,51 @@ int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
     return 0;
 }
 
+// crc64_xcd_kernel constants for nwx waves per XCD (u64): [0, 256) the nibble tables of the chunk
+// jump J = x^(8 * chunk * (nwx - 1)), entry 16 n + v = (v << 4n) * J; then 40 x 64 columns of
+// x^(8 * chunk * 2^i) * x^j; then [level < 4][v < 256] x 64 columns of x^(8 * chunk * v * 256^level) * x^j
+// (a part's shift to its buffer end: bit by bit on the scalar unit, or a byte of the distance per
+// lane-parallel product)
+int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
+    const auto key = std::make_pair(alg, nwx);
+    auto it = d->xcd.find(key);
+    if (it == d->xcd.end()) {
+        const uint64_t poly = alg_poly(alg);
+        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64, 0);
+        const uint64_t J = gf2_xpow8n((uint64_t)kXcdChunkBytes * (nwx - 1), poly, 64);
+        for (int n = 0; n < 16; ++n)
+            for (uint64_t v = 0; v < 16; ++v) c[16 * n + v] = gf2_mulmod(v << (4 * n), J, poly, 64);
+        uint64_t sq = gf2_xpow8n(kXcdChunkBytes, poly, 64);
+        for (int i = 0; i < 40; ++i) {
+            uint64_t col = sq;
+            for (int j = 0; j < 64; ++j) {
+                c[256 + 64 * i + j] = col;
+                col = gf2_mulx(col, poly);
+            }
+            sq = gf2_mulmod(sq, sq, poly, 64);
+        }
+        uint64_t base = gf2_xpow8n(kXcdChunkBytes, poly, 64);  // x^(8 * chunk * 256^level)
+        for (int L = 0; L < 4; ++L) {
+            uint64_t pv = 1ull << 63;  // x^0, then base^v
+            for (int v = 0; v < 256; ++v) {
+                uint64_t col = pv;
+                for (int j = 0; j < 64; ++j) {
+                    c[256 + 40 * 64 + (256 * L + v) * 64 + j] = col;
+                    col = gf2_mulx(col, poly);
+                }
+                pv = gf2_mulmod(pv, base, poly, 64);
+            }
+            base = pv;  // base^256
+        }
+        DevBuf b;
+        int rc = upload_new(b, c.data(), c.size() * 8);
+        if (rc) return rc;
+        it = d->xcd.emplace(key, b).first;
+    }
+    *out = (const uint64_t *)it->second.p;
+    return 0;
+}
+
 // column j of P_k = x^(8*tile*k) * x^j, k < tmax : moves tile k's partial to its buffer end
 int get_pcols(Device *d, int alg, uint64_t tile, uint64_t tmax, hipStream_t s, const uint64_t **out) {
     auto key = std::make_pair(alg, tile);
@@ -362,6 +408,13 @@ constexpr bool kStreamW16 = AMDCRC_STREAM_W16 != 0;
 #define AMDCRC_ROWS16 1
 #endif
 constexpr bool kRows16 = AMDCRC_ROWS16 != 0;
+// Strided CRC64NVME batches whose main regions are whole chunks, at least kXcdMinChunks of them, take
+// crc64_xcd_kernel (XCD-window chunk order)
+#ifndef AMDCRC_XCD  // compile-time only (A/B builds)
+#define AMDCRC_XCD 1
+#endif
+constexpr bool kXcd = AMDCRC_XCD != 0;
+constexpr uint64_t kXcdMinChunks = 256;
 constexpr uint64_t kRows16MinBuffers = 4 * 4096;
 constexpr uint64_t kRows16MaxBytes = 256u << 10;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
@@ -734,6 +787,26 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
         p.ntiles = count;
         p.seed_all = seed_all;
         return launch_scan(d, alg, p, count, 1, ml * count, s);
+    }
+    // long CRC64NVME buffers of whole chunks: XCD-window chunk order (crc64_xcd_kernel)
+    if (!w32 && kXcd && ml % kXcdChunkBytes == 0 && ml / kXcdChunkBytes >= kXcdMinChunks) {
+        const uint64_t blocks = (2 * (uint64_t)d->cus) & ~7ull, nwx = blocks;  // 8 waves per block, 8 XCDs
+        if (blocks >= 8) {
+            p.stream = 5;
+            p.tiles_per_buf = ml / kXcdChunkBytes;
+            p.ntiles = p.tiles_per_buf * count;
+            int rc = get_braid64_consts(d, alg, &p.d_kvals);
+            if (!rc) rc = get_xcd_consts(d, alg, nwx, &p.d_pcols);
+            Workspace *w;
+            if (!rc) rc = get_workspace(d, s, count, 1, &w);
+            if (rc) return rc;
+            p.d_acc = w->acc;
+            p.d_cnt = w->cnt;
+            int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
+            g_time_events[0] = g_time_events[1] = nullptr;
+            if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString((hipError_t)e));
+            return 0;
+        }
     }
     // large W=32 launches: 16-byte lane words in one 1024-thread workgroup per CU (the same waves per
     // CU as two 512-thread workgroups; the tiles hold 4 KiB groups either way)

@@ -26,6 +26,11 @@ constexpr int kVecPerGroup = kGroupBytes / 16;
 #define AMDCRC_W64_BLOCK 512
 #endif
 constexpr int kW64StreamBlock = AMDCRC_W64_BLOCK;
+// crc64_xcd_kernel: 4 KiB groups per chunk (a wave's contiguous piece of an XCD window)
+#ifndef AMDCRC_XCD_CHUNK_GROUPS  // compile-time only (A/B builds)
+#define AMDCRC_XCD_CHUNK_GROUPS 4
+#endif
+constexpr uint64_t kXcdChunkBytes = (uint64_t)AMDCRC_XCD_CHUNK_GROUPS * 4096;
 constexpr int kMaxBatches = 32;  // batches per strided launch (kernel arguments, 768 bytes)
 
 // The 16-byte-word CRC32 streaming scan (crc_kernels.hip Braid32W16: slice-by-16 rows, one
@@ -60,7 +65,9 @@ struct ScanParams {
     uint32_t stream;               // strided batch with main % TILE == 0: the streaming scan (crc32_stream_kernel /
                                    // crc64_stream4_kernel); W=32: 1 = 8-byte lane words (512-thread workgroups),
                                    // 2 = 16-byte lane words (one 1024-thread workgroup per CU); 3 = CRC64NVME
-                                   // rows of 16 lanes (crc64_rows16_kernel); lists: 4 = crc32_list_stream_kernel
+                                   // rows of 16 lanes (crc64_rows16_kernel); lists: 4 = crc32_list_stream_kernel;
+                                   // 5 = CRC64NVME XCD-window chunks (crc64_xcd_kernel: tiles_per_buf = chunks
+                                   // per buffer, ntiles = chunks, d_pcols = engine.cpp get_xcd_consts)
     const uint64_t *d_kvals;       // 64 x K_l = x^(8*seg*(63-l)) mod P
     const uint64_t *d_pcols;       // [tmax][W]: column j of x^(8*TILE*k) = x^(8*TILE*k) * x^j
     uint64_t pcols_tmax;

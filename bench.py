@@ -276,7 +276,13 @@ def kernel_name(alg, nbuf, L):
     if alg in ("crc32", "crc32c"):
         return "crc32_stream_kernel"
     if alg == "crc64nvme":
-        return "crc_lanes_kernel" if L <= 4096 and nbuf >= 65536 else "crc64_stream4_kernel"
+        if L <= 4096 and nbuf >= 65536:
+            return "crc_lanes_kernel"
+        if nbuf >= 16384 and L % 1024 == 0 and 1024 <= L <= 256 << 10:
+            return "crc64_rows16_kernel"
+        if L % 16384 == 0 and L // 16384 >= 256:
+            return "crc64_xcd_kernel"
+        return "crc64_stream4_kernel"
     if alg == "xxh64":
         if nbuf <= 16 and L >= 1 << 20:
             return "xxh64 host route (D2H slices + host threads, stream-ordered; DESIGN.md §3.4)"

@@ -255,6 +255,55 @@ def test_crc64_rows16_short_buffers(engine, count, L, stride, off, seeded):
             assert got[i] == oracle.crc("crc64nvme", h[off + i * stride: off + i * stride + L], seeds[i]), i
 
 
+@pytest.mark.parametrize("count,chunks,head,tail,seeded", [
+    (3, 300, 13, 7, True),     # unaligned heads and tails, seeds; XCD eighths cut inside buffers
+    (5, 256, 0, 0, False),     # the fewest chunks taken: a wave's next chunk is two buffers on
+    (2, 4099, 11, 5, True),    # 64 MiB + 3 chunks: parts of 8-9 chunks per wave, ragged eighths
+    (9, 1024, 0, 9, False),    # nine 16 MiB buffers over eight XCDs
+])
+def test_crc64_xcd_long_buffers(engine, count, chunks, head, tail, seeded):
+    """Strided CRC64NVME batches whose main regions are whole 16 KiB chunks (at least 256) take
+    crc64_xcd_kernel: XCD-window chunk order, the chunk jump from nibble tables, parts moved to the
+    buffer end and joined by chunk count."""
+    import torch
+
+    off = (16 - head) % 16
+    L = head + chunks * 16384 + tail
+    stride = (L + 15) // 16 * 16
+    d = dev_random(stride * count + off + 64, 0x5CD + count)
+    rng = random.Random(chunks)
+    seeds = [rng.getrandbits(64) for _ in range(count)] if seeded else None
+    out = engine.checksum_strided(ALG["crc64nvme"], d, stride, L, count,
+                                  seeds=seeds_tensor("crc64nvme", seeds) if seeded else None, base_offset=off)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    got = engine.as_unsigned(out)
+    for i in range(count):
+        want = oracle.crc("crc64nvme", h[off + i * stride: off + i * stride + L], seeds[i] if seeded else 0)
+        assert got[i] == want, i
+
+
+def test_crc64_xcd_multi_batch(engine):
+    """Three queued batches of 2 x 16 MiB through aws_crt_amd_checksum_batches (one crc64_xcd_kernel
+    launch over six buffers), seeds on one batch."""
+    import torch
+
+    L, count, nb = 16 << 20, 2, 3
+    d = dev_random(nb * L * count, 0x5CE)
+    rng = random.Random(0x5CE)
+    seeds = [[rng.getrandbits(64) for _ in range(count)] if j == 1 else None for j in range(nb)]
+    outs = [torch.empty(count, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    engine.checksum_batches(ALG["crc64nvme"], [(d.data_ptr() + j * L * count, seeds_tensor("crc64nvme", seeds[j]) if seeds[j] else None,
+                                                outs[j]) for j in range(nb)], L, L, count)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    for j in range(nb):
+        got = engine.as_unsigned(outs[j])
+        for i in range(count):
+            o = (j * count + i) * L
+            assert got[i] == oracle.crc("crc64nvme", h[o:o + L], seeds[j][i] if seeds[j] else 0), (j, i)
+
+
 def test_crc64_rows16_multi_batch(engine):
     """Three queued batches of 16384 x 8 KiB through aws_crt_amd_checksum_batches (one rows16 launch
     over 49152 buffers, sets crossing batch boundaries), seeds on one batch."""
