@@ -1092,8 +1092,6 @@ template <int R>
 __device__ __forceinline__ uint64_t gld_w8(uint32_t voff, uint64_t sbase) {
     return __builtin_nontemporal_load((gu64 *)(sbase + voff + R * kW8Row));
 }
-template <int R>
-__device__ __forceinline__ void stream_issue(W8Group &g, uint32_t voff, uint64_t s);
 
 // 8-byte rows: x = u ^ lo(w_r) is the chained value; the hi lookups of row r are issued with row
 // r - 1's chain step and XORed in at row r (h = row r - 1's hi part).  One row ahead measured 0.4-1 %
@@ -1102,11 +1100,7 @@ template <int R, class B>
 __device__ __forceinline__ uint32_t stream_rows_w8(uint32_t x, typename B::Hi h, W8Group &cur, W8Group &nxt, uint32_t voff,
                                                    uint64_t snext, const B &eng) {
     if constexpr (R < kW8RowsPerGroup) {
-#ifdef AMDCRC_XP_ISSUE_AHEAD  // experiment builds only: the next slot's eight loads all issued at row 0
-        if constexpr (R == 0) stream_issue<0>(nxt, voff, snext);
-#else
         nxt.w[R] = gld_w8<R>(voff, snext);
-#endif
         typename B::Hi hn;
         if constexpr (R == 0) {
             x ^= (uint32_t)cur.w[0];
@@ -1370,13 +1364,6 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
-#ifdef AMDCRC_XP_V4ORDER  // experiment builds only (timing; results wrong): XCD-window 16 KiB chunk order
-        if (fq < nq) {
-            const uint64_t xcd = blockIdx.x & 7, j = (blockIdx.x >> 3) * WAVES + wv, nwx = nw / 8;
-            const uint64_t ngt = p.ntiles << gsh, grp = xcd * (ngt / 8) + (j + (fq / 4) * nwx) * 4 + fq % 4;
-            return rfl64(p.base + hoff + grp * 4096);
-        }
-#endif
         uint64_t a = fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
         if (!AMDCRC_GUARD_OK(fq >= nq || p.nbatch > 1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
                                                                  p.base + (p.nbuf - 1) * p.stride + hoff + T * tile_bytes),
@@ -1525,29 +1512,6 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // pass reached the loop header with a merged state in which the slot about to be loaded still had
     // loads in flight, and drained most of the ring at the top of every rotation (vmcnt 7..2 before the
     // first step's row loads); without the breaks every row waits exactly vmcnt(16).
-#ifdef AMDCRC_XP_RING4  // experiment builds only: a four-slot ring (three groups ahead)
-    Grp rd;
-    stream_issue<0>(rc, voff, f_addr());
-    f_next();
-    step(ra, rd, true);
-    while (q + 4 <= nq) {
-        step(rb, ra, false);
-        step(rc, rb, false);
-        step(rd, rc, false);
-        step(ra, rd, false);
-    }
-    if (q < nq) {
-        step(rb, ra, false);
-        if (q < nq) step(rc, rb, false);
-        if (q < nq) step(rd, rc, false);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : AMDCRC_R8W(ra)::"memory");
-    asm volatile("" : AMDCRC_R8W(rb));
-    asm volatile("" : AMDCRC_R8W(rc));
-    asm volatile("" : AMDCRC_R8W(rd));
-    stream_publish(p, acc, eng, lane);
-    return;
-#endif
     step(ra, rc, true);
 #ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
     while (q < nq) {
@@ -2308,14 +2272,7 @@ template <int R, class B>
 __device__ __forceinline__ uint64_t stream64_rows(uint64_t x, B64Group &cur, B64Group &nxt, uint32_t voff, uint64_t snext,
                                                   const B &eng) {
     if constexpr (R < kB64RowsPerGroup) {
-#ifdef AMDCRC_XP_ISSUE_AHEAD  // experiment builds only: the next slot's eight loads all issued at row 0
-        if constexpr (R == 0) {
-#pragma unroll
-            for (int k = 0; k < kB64RowsPerGroup; ++k) nxt.w[k] = __builtin_nontemporal_load((gu64 *)(snext + voff + k * kB64Row));
-        }
-#else
         nxt.w[R] = gld_row64<R>(voff, snext);
-#endif
         x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
         __builtin_amdgcn_sched_barrier(0);
         return stream64_rows<R + 1>(x, cur, nxt, voff, snext, eng);
@@ -2408,13 +2365,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
     auto f_addr = [&]() -> uint64_t {
-#ifdef AMDCRC_XP_V4ORDER  // experiment builds only (timing; results wrong): XCD-window 16 KiB chunk order
-        if (fq < nq) {
-            const uint64_t xcd = blockIdx.x & 7, j = (blockIdx.x >> 3) * kBraidWaves + (threadIdx.x >> 6), nwx = nw / 8;
-            const uint64_t ngt = p.ntiles << gsh, grp = xcd * (ngt / 8) + (j + (fq / 4) * nwx) * 4 + fq % 4;
-            return rfl64(p.base + hoff + grp * 4096);
-        }
-#endif
         return rfl64(fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kB64Row * kB64RowsPerGroup) : dummy);
     };
     auto f_next = [&]() {
