@@ -23,6 +23,9 @@
 
 #include <type_traits>
 
+#ifndef AMDCRC_R16_XCD  // compile-time only: crc64_rows16_kernel's sets in XCD-window order (1) or contiguous (0)
+#define AMDCRC_R16_XCD 1
+#endif
 #ifndef AMDCRC_STREAM_W8  // compile-time only: the W=32 streaming scan on 8-byte words (1) or 4-byte words (0)
 #define AMDCRC_STREAM_W8 1
 #endif
@@ -2744,12 +2747,25 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
     const uint64_t nsets = (p.nbuf + 3) / 4;
     const uint64_t nw = (uint64_t)gridDim.x * kWaves;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6));
-    const uint64_t s0 = rfl64(gw * nsets / nw), s1 = rfl64((gw + 1) * nsets / nw);
+    // the wave's sets: s0, s0 + sstep, ... (nsw of them).  With a grid of whole XCD rows (gridDim % 8
+    // == 0) the waves of XCD x = blockIdx mod 8 take sets j, j + nwx, ... of the x-th eighth
+    // (neighbouring sets at every step: crc64_xcd_kernel's read order); otherwise contiguous ranges.
+    uint64_t s0, sstep, nsw;
+#if AMDCRC_R16_XCD
+    if ((gridDim.x & 7u) == 0) {
+        const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * nsets / 8, xhi = (xcd + 1) * nsets / 8;
+        const uint64_t j = rfl64((uint64_t)(blockIdx.x >> 3) * kWaves + (threadIdx.x >> 6));
+        s0 = xlo + j, sstep = nwx, nsw = s0 < xhi ? (xhi - s0 + nwx - 1) / nwx : 0;
+    } else
+#endif
+    {
+        s0 = rfl64(gw * nsets / nw), sstep = 1, nsw = rfl64((gw + 1) * nsets / nw) - s0;
+    }
     const Edges e0 = buffer_edges<false>(p, 0);
     const uint64_t hoff = e0.headend - p.base, ml = e0.tail - e0.headend;
     const uint32_t G = (uint32_t)(ml / kR16Group);  // groups per buffer (the host checks ml % kR16Group == 0)
-    const uint32_t nq = (uint32_t)((s1 - s0) * G);  // groups of this wave
-    const bool work = s0 < s1;
+    const uint32_t nq = (uint32_t)(nsw * G);  // groups of this wave
+    const bool work = nsw > 0;
     const uint64_t dummy = (uint64_t)p.d_kvals + 8u * t;  // placeholder rows: the 16 KiB constant block
     // this lane's buffer of set s: main-region address + 8 t (rows past the batch read the constants)
     // (the four row bases are wave-uniform: computed on the scalar unit, so a multi-batch launch reads
@@ -2777,7 +2793,8 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
         ++fq;
         if (++fg == G) {
             fg = 0;
-            if (++fs < s1) fbase = lane_base(fs);
+            fs += sstep;
+            if (fq < nq) fbase = lane_base(fs);
         }
     };
     const uint64_t kl = *(gu64 *)(p.d_kvals + t);  // K_t = x^(-64 t)
@@ -2823,7 +2840,7 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
                                      (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
                 if (b < p.nbuf && lane == 0) finalize<false>(p, b, fin, eng);
             }
-            ++s;
+            s += sstep;
         }
     };
 #ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
