@@ -260,6 +260,7 @@ def test_crc64_rows16_short_buffers(engine, count, L, stride, off, seeded):
     (5, 256, 0, 0, False),     # the fewest chunks taken: a wave's next chunk is two buffers on
     (2, 4099, 11, 5, True),    # 64 MiB + 3 chunks: parts of 8-9 chunks per wave, ragged eighths
     (9, 1024, 0, 9, False),    # nine 16 MiB buffers over eight XCDs
+    (1, 4101, 3, 9, True),     # one buffer over all eight XCDs: every eighth a part, shifts up to 3.6 K chunks
 ])
 def test_crc64_xcd_long_buffers(engine, count, chunks, head, tail, seeded):
     """Strided CRC64NVME batches whose main regions are whole 16 KiB chunks (at least 256) take
