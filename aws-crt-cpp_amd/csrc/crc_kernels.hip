@@ -2471,7 +2471,7 @@ constexpr int kXcdChunkGroups = AMDCRC_XCD_CHUNK_GROUPS;
 constexpr uint32_t kXcdChunk = kXcdChunkGroups * kB64Row * kB64RowsPerGroup;
 constexpr uint32_t kXcdJumpOff = kB64x4Lds;               // 16 nibbles x 16 x u64: v << 4n times J
 constexpr uint32_t kXcdSlotOff = kXcdJumpOff + 16 * 16 * 8;  // two held parts per wave (b, value, chunks)
-constexpr uint32_t kXcdLds = kXcdSlotOff + 16 * 32;
+constexpr uint32_t kXcdLds = kXcdSlotOff + 32 * 32;           // up to 16 waves
 static_assert(2 * kXcdLds <= 160 * 1024, "two crc64_xcd_kernel workgroups per CU");
 
 __device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u) {
@@ -2497,11 +2497,12 @@ struct XcdCursor {
     uint64_t main;      // main-region address of buffer b
 };
 
-template <uint64_t POLY>
-__global__ __launch_bounds__(512, 4) void crc64_xcd_kernel(const ScanParams p) {
+template <uint64_t POLY, int BLOCK>
+__global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p) {
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
-    constexpr int kWaves = 8;
+    constexpr int kWaves = BLOCK / 64;
+    static_assert(kWaves <= 16, "two held-part slots per wave, 32 entries");
     const int lane = threadIdx.x & 63;
     const uint64_t nwx = (uint64_t)gridDim.x * kWaves / 8;  // waves per XCD (gridDim % 8 == 0)
     const uint64_t xcd = blockIdx.x & 7u;
@@ -2628,12 +2629,13 @@ __global__ __launch_bounds__(512, 4) void crc64_xcd_kernel(const ScanParams p) {
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (threadIdx.x >= 64) return;
-        // wave 0: entry e in lane e (< 16); one publication per distinct buffer
-        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane & 15);
-        uint64_t eb = lane < 16 ? slot[0] : ~0ull;
+        // wave 0: entry e in lane e (< 2 per wave); one publication per distinct buffer
+        constexpr int kEntries = 2 * kWaves;
+        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane & (kEntries - 1));
+        uint64_t eb = lane < kEntries ? slot[0] : ~0ull;
         const uint64_t er = slot[1];
         const uint32_t en = (uint32_t)slot[2];
-        for (int e = 0; e < 16; ++e) {
+        for (int e = 0; e < kEntries; ++e) {
             const uint64_t b = rfl64((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, e) |
                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), e) << 32));
             if (b == ~0ull) continue;
@@ -3404,7 +3406,7 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             if (p->stream == 3 && !list)  // many short buffers: 16 lanes per buffer
                 launch(crc64_rows16_kernel<kPoly64Nvme>, nblocks, kR16Block, s, p, ev);
             else if (p->stream == 5 && !list)  // long buffers: XCD-window chunks
-                launch(crc64_xcd_kernel<kPoly64Nvme>, nblocks, 512, s, p, ev);
+                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list)
