@@ -655,23 +655,25 @@ def test_config5_crc64_xxh64_8x64mib(engine):
     assert x3 == [oracle.xxh3_64(h[i * L:(i + 1) * L]) for i in range(n)]
 
 
-def test_graph_capture_replay(engine):
+@pytest.mark.parametrize("alg,n,L", [
+    ("crc32c", 24, (3 << 20) + 16),   # multi-tile buffers: the cross-tile combine inside the graph
+    ("crc64nvme", 4, 8 << 20),        # crc64_xcd_kernel: parts joined by chunk count inside the graph
+])
+def test_graph_capture_replay(engine, alg, n, L):
     """A scan captured into a HIP graph (torch.cuda.graph) after one eager warm-up on the capture
     stream replays correctly on that stream, also after the input bytes change (the captured launch
-    keeps the capture stream's self-cleaning workspace); multi-tile buffers exercise
-    the cross-tile combine inside the graph."""
+    keeps the capture stream's self-cleaning workspace)."""
     import torch
 
-    n, L = 24, (3 << 20) + 16
     d = dev_random(n * L, 51)
     s = torch.cuda.Stream()
-    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    out = torch.empty(n, dtype=torch.int64 if alg in W64 else torch.int32, device="cuda")
     with torch.cuda.stream(s):
-        engine.checksum_strided(ALG["crc32c"], d, L, L, n, out=out, stream=s)  # warm-up: tables, workspace
+        engine.checksum_strided(ALG[alg], d, L, L, n, out=out, stream=s)  # warm-up: tables, workspace
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        engine.checksum_strided(ALG["crc32c"], d, L, L, n, out=out, stream=s)
+        engine.checksum_strided(ALG[alg], d, L, L, n, out=out, stream=s)
     for it in range(3):
         if it:
             d.copy_(dev_random(n * L, 60 + it))
@@ -680,4 +682,4 @@ def test_graph_capture_replay(engine):
             g.replay()
         torch.cuda.synchronize()
         h = host_bytes(d)
-        assert engine.as_unsigned(out) == [oracle.crc("crc32c", h[i * L:(i + 1) * L]) for i in range(n)], it
+        assert engine.as_unsigned(out) == [oracle.crc(alg, h[i * L:(i + 1) * L]) for i in range(n)], it
