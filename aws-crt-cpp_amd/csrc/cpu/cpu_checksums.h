@@ -17,6 +17,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
+
 namespace amdcrc {
 namespace cpu {
 
@@ -84,6 +86,10 @@ void xxh3_128_digest(const Xxh3State *s, uint64_t out_hi_lo[2]);
 // buffer (XXH3-128: two words, high then low).  alg as aws_crt_amd_algorithm.  seeds may be null.
 void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64_t *seeds, uint64_t *out, size_t count,
            int threads);
+
+// fn(0) .. fn(n - 1) on the host batch's persistent worker threads (fn(0) on the calling thread), or
+// on threads of their own when the pool is busy
+void parallel(size_t n, const std::function<void(size_t)> &fn);
 
 }  // namespace cpu
 }  // namespace amdcrc

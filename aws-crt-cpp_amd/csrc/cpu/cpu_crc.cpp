@@ -327,6 +327,23 @@ Pool &pool() {
 
 }  // namespace
 
+void parallel(size_t n, const std::function<void(size_t)> &fn) {
+    if (n == 0) return;
+    if (n == 1 || pool().try_run(n, fn)) {
+        if (n == 1) fn(0);
+        return;
+    }
+    std::vector<std::thread> ts;
+    size_t spawned = 1;
+    try {
+        for (; spawned < n; ++spawned) ts.emplace_back(fn, spawned);
+    } catch (...) {
+    }
+    fn(0);
+    for (auto &t : ts) t.join();
+    for (size_t i = spawned; i < n; ++i) fn(i);  // threads that could not be started
+}
+
 // Host batch (aws_crt_amd_cpu_batch).  Work items are claimed dynamically by `threads` threads.  A
 // CRC buffer longer than the piece size is cut into pieces, each checksummed from seed 0 (the first
 // from the caller's seed) and folded in order with Combine (CRC.h:41-51) -- so a batch of fewer

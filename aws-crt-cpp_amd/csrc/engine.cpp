@@ -572,16 +572,9 @@ void x64_chunk_fn(void *u) noexcept {
         cpu::xxh64_update(&j->xs[i], c->rows + i * c->rowbytes, c->rowbytes);
         if (c->last) j->h_res[i] = cpu::xxh64_digest(&j->xs[i]);
     };
-    // one host thread per buffer (the calling runtime thread takes buffer 0)
-    std::vector<std::thread> ts;
-    size_t spawned = 1;
-    try {
-        for (; spawned < j->count; ++spawned) ts.emplace_back(row, spawned);
-    } catch (...) {
-    }
-    row(0);
-    for (auto &t : ts) t.join();
-    for (size_t i = spawned; i < j->count; ++i) row(i);  // threads that could not be started
+    // one host thread per buffer on the host path's persistent workers (the calling runtime thread
+    // takes buffer 0): a std::thread per buffer per slice cost its creation on every slice
+    cpu::parallel(j->count, row);
 }
 void x64_free_fn(void *u) noexcept {
     X64Job *j = (X64Job *)u;
