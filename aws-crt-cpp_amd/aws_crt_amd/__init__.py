@@ -231,6 +231,61 @@ def checksum_batches(alg: int, batches, stride: int, length: int, count: int, st
     BatchSet(alg, batches, stride, length, count).run(stream)
 
 
+class Queue:
+    """A submission queue (aws_crt_amd_queue_*): batches of one shape pushed one at a time are launched
+    together, when 32 are queued and at flush() / close().  Keeps the pushed tensors referenced until
+    their launch is on the stream."""
+
+    def __init__(self, alg: int, stride: int, length: int, count: int, stream=None):
+        L = lib()
+        L.aws_crt_amd_queue_create.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        L.aws_crt_amd_queue_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.aws_crt_amd_queue_flush.argtypes = [ctypes.c_void_p]
+        L.aws_crt_amd_queue_pending.argtypes = [ctypes.c_void_p]
+        L.aws_crt_amd_queue_pending.restype = ctypes.c_size_t
+        L.aws_crt_amd_queue_destroy.argtypes = [ctypes.c_void_p]
+        self._L = L
+        self._stream = stream
+        self._keep = []
+        h = ctypes.c_void_p()
+        _check(L.aws_crt_amd_queue_create(alg, stride, length, count, _stream_handle(stream), ctypes.byref(h)))
+        self._h = h
+        self._n = 0  # pushed since the last launch (the engine launches at 32 queued batches)
+
+    def _launched(self):
+        self._n = 0
+        if self._stream is not None and hasattr(self._stream, "cuda_stream"):
+            for t in self._keep:
+                if getattr(t, "is_cuda", False):
+                    t.record_stream(self._stream)
+        self._keep = []
+
+    def push(self, base, out, seeds=None) -> None:
+        for t in (base, out, seeds):
+            if hasattr(t, "data_ptr"):
+                self._keep.append(t)
+        b = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+        _check(self._L.aws_crt_amd_queue_push(self._h, b, seeds.data_ptr() if seeds is not None else None, out.data_ptr()))
+        self._n += 1
+        if self._n == 32:
+            self._launched()
+
+    def pending(self) -> int:
+        return int(self._L.aws_crt_amd_queue_pending(self._h))
+
+    def flush(self) -> None:
+        _check(self._L.aws_crt_amd_queue_flush(self._h))
+        self._launched()
+
+    def close(self) -> None:
+        if self._h:
+            rc = self._L.aws_crt_amd_queue_destroy(self._h)
+            self._h = None
+            self._launched()
+            _check(rc)
+
+
 class HostJob:
     """A prepared host-ingest job (aws_crt_amd_host_submit / aws_crt_amd_job_wait) over host buffers
     given by raw addresses: the argument arrays are built once; `run()` submits and waits (the C

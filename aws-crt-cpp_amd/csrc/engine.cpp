@@ -1279,6 +1279,77 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(int alg, const struct aws_crt_a
     });
 }
 
+// Submission queue (checksums_batch.h): pushes collect batches of one shape; a full queue (kMaxBatches)
+// or a flush hands them to aws_crt_amd_checksum_batches, one launch per run of batches.
+struct aws_crt_amd_queue {
+    int alg;
+    size_t stride, len, count;
+    void *stream;
+    std::mutex mu;
+    std::vector<aws_crt_amd_batch> pending;
+};
+
+namespace {
+int queue_flush_locked(aws_crt_amd_queue *q) {
+    if (q->pending.empty()) return 0;
+    const int rc = aws_crt_amd_checksum_batches(q->alg, q->pending.data(), q->pending.size(), q->stride, q->len, q->count,
+                                                q->stream);
+    q->pending.clear();  // launched, or refused with its error recorded: not retried
+    return rc;
+}
+}  // namespace
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_create(int alg, size_t stride, size_t len, size_t count, void *hip_stream,
+                                             aws_crt_amd_queue **out) {
+    return guarded(err_sink, [&]() -> int {
+        if (!out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue pointer");
+        *out = nullptr;
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        if (count > 1 && stride % 16 != 0 && !is_hash(alg))
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
+        std::unique_ptr<aws_crt_amd_queue> q(new aws_crt_amd_queue);
+        q->alg = alg, q->stride = stride, q->len = len, q->count = count, q->stream = hip_stream;
+        q->pending.reserve(kMaxBatches);
+        *out = q.release();
+        return 0;
+    });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_push(aws_crt_amd_queue *q, const void *d_base, const void *d_seeds, void *d_out) {
+    return guarded(err_sink, [&]() -> int {
+        if (!q) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue");
+        if (!d_out || (q->len && !d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
+        std::lock_guard<std::mutex> g(q->mu);
+        q->pending.push_back({d_base, d_seeds, d_out});
+        return q->pending.size() >= (size_t)kMaxBatches ? queue_flush_locked(q) : 0;
+    });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_flush(aws_crt_amd_queue *q) {
+    return guarded(err_sink, [&]() -> int {
+        if (!q) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue");
+        std::lock_guard<std::mutex> g(q->mu);
+        return queue_flush_locked(q);
+    });
+}
+
+AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const aws_crt_amd_queue *q) {
+    if (!q) return 0;
+    std::lock_guard<std::mutex> g(const_cast<aws_crt_amd_queue *>(q)->mu);
+    return q->pending.size();
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(aws_crt_amd_queue *q) {
+    if (!q) return 0;
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(q->mu);
+        rc = guarded(err_sink, [&]() -> int { return queue_flush_locked(q); });
+    }
+    delete q;
+    return rc;
+}
+
 AWS_CRT_AMD_API int aws_crt_amd_checksum_list(int alg, const void *const *d_ptrs, const size_t *lens, size_t count,
                                               const void *d_seeds, void *d_out, void *hip_stream) {
     return guarded(err_sink, [&]() -> int {

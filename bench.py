@@ -584,6 +584,30 @@ def main():
                           "ms_per_step": round(el1 / args.steps * 1e3, 4),
                           "launch": f"one launch per batch, {args.steps} launches over {len(streams)} streams"}
 
+    # the same K steps pushed one at a time into a submission queue (aws_crt_amd_queue_*), which
+    # launches at 32 queued batches and at the flush: what a producer of one batch at a time gets
+    queued = None
+    if G > 1 and args.steps > 0:
+        q = eng.Queue(ALG[alg], L, L, count, stream=streams[0])
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            b = batch(i)
+            q.push(b[0], b[2])
+        q.flush()
+        torch.cuda.synchronize()
+        elq = time.perf_counter() - t0
+        q.close()
+        if world > 1:
+            t = torch.tensor([elq], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elq = float(t.item())
+        queued = {"value": round(world * args.steps * step_bytes / max(elq, 1e-9) / 2**30, 2), "unit": "GiB/s",
+                  "ms_per_step": round(elq / args.steps * 1e3, 4),
+                  "launch": f"{args.steps} pushes of one batch into aws_crt_amd_queue (launch at 32 queued and at flush)"}
+
     # every rank checks a sample of its own results against the engine's host path (the first 64
     # buffers of the first resident batch, which the timed region and the warm-up both wrote)
     torch.cuda.synchronize()
@@ -690,6 +714,7 @@ def main():
             "parity": parity_all,
             "ranks": ranks,
             "one_batch_per_launch": one_per_launch,
+            "queued_one_at_a_time": queued,
             "roofline": roof,
             "cpu_baseline": cpu,
             "e2e_pinned": e2e,

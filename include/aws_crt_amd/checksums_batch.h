@@ -133,6 +133,30 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(
     void *hip_stream);
 
 /*
+ * Submission queue: a producer that gets one uniform batch at a time (aws-c-s3 checksumming parts as
+ * they arrive, source/s3/S3.cpp:1133-1149) pushes each batch and the engine launches them together:
+ * a push queues (base, seeds, out) without launching; the queue launches on its stream when it holds
+ * 32 batches (one launch, as aws_crt_amd_checksum_batches), and at aws_crt_amd_queue_flush or
+ * aws_crt_amd_queue_destroy.  Work is on the stream only after the launch that holds it: a caller
+ * that synchronises the stream, records an event on it or reads a result flushes first.  Every
+ * batch of a queue has the queue's algorithm and shape (stride, len, count).  Thread-safe.
+ */
+struct aws_crt_amd_queue;
+AWS_CRT_AMD_API int aws_crt_amd_queue_create(
+    int algorithm,
+    size_t stride,
+    size_t len,
+    size_t count,
+    void *hip_stream,
+    struct aws_crt_amd_queue **out_queue);
+AWS_CRT_AMD_API int aws_crt_amd_queue_push(struct aws_crt_amd_queue *queue, const void *d_base, const void *d_seeds, void *d_out);
+AWS_CRT_AMD_API int aws_crt_amd_queue_flush(struct aws_crt_amd_queue *queue);
+/* batches pushed and not yet launched */
+AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const struct aws_crt_amd_queue *queue);
+/* flushes, then frees the queue; returns the flush's status */
+AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
+
+/*
  * Ragged batch: buffer i = [d_ptrs[i], + lens[i]).  d_ptrs and lens are HOST arrays describing
  * device buffers (any alignment, any length including 0).  The engine uploads a compact
  * descriptor (16 B per buffer + tile prefix) per call.  d_seeds as above.
