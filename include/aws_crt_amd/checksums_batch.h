@@ -139,7 +139,8 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(
  * 32 batches (one launch, as aws_crt_amd_checksum_batches), and at aws_crt_amd_queue_flush or
  * aws_crt_amd_queue_destroy.  Work is on the stream only after the launch that holds it: a caller
  * that synchronises the stream, records an event on it or reads a result flushes first.  Every
- * batch of a queue has the queue's algorithm and shape (stride, len, count).  Thread-safe.
+ * batch of a queue has the queue's algorithm and shape (stride, len, count).  Push, flush and pending
+ * may be called from several threads; destroy must not overlap any other call on the same queue.
  */
 struct aws_crt_amd_queue;
 AWS_CRT_AMD_API int aws_crt_amd_queue_create(
