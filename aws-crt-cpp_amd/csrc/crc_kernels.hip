@@ -2494,10 +2494,40 @@ __device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u) {
 // a wave-uniform walk over the chunks j, j + nwx, ... of [lo, hi): chunk k of buffer b
 struct XcdCursor {
     uint64_t b, k;      // buffer, chunk in buffer
-    uint64_t main;      // main-region address of buffer b
+    uint64_t main;      // virtual start of buffer b's chunk 0 (main-region start - front pad)
 };
 
-template <uint64_t POLY, int BLOCK>
+// rows through a raw buffer resource (crc32_list_stream_kernel's loads): offsets at or past `lim`
+// read zeros, so a chunk's front pad costs no masking and no traffic
+template <int R>
+__device__ __forceinline__ uint64_t xcd_bld(__amdgpu_buffer_rsrc_t rs, uint32_t o0, uint32_t lim) {
+    const uint32_t o = __builtin_elementwise_min(o0 + (uint32_t)(R * kB64Row), lim);
+    const v2u v = __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 2);  // aux 2: non-temporal
+    return ((uint64_t)v.y << 32) | v.x;
+}
+template <int R, class B>
+__device__ __forceinline__ uint64_t xcd_rows(uint64_t x, B64Group &cur, B64Group &nxt, __amdgpu_buffer_rsrc_t rs, uint32_t o0,
+                                             uint32_t lim, const B &eng) {
+    if constexpr (R < kB64RowsPerGroup) {
+        nxt.w[R] = xcd_bld<R>(rs, o0, lim);
+        x = R == 0 ? x ^ cur.w[0] : eng.step_x(x, cur.w[R]);
+        __builtin_amdgcn_sched_barrier(0);
+        return xcd_rows<R + 1>(x, cur, nxt, rs, o0, lim, eng);
+    } else {
+        return eng.step(x);
+    }
+}
+template <int R>
+__device__ __forceinline__ void xcd_issue(B64Group &g, __amdgpu_buffer_rsrc_t rs, uint32_t o0, uint32_t lim) {
+    if constexpr (R < kB64RowsPerGroup) {
+        g.w[R] = xcd_bld<R>(rs, o0, lim);
+        xcd_issue<R + 1>(g, rs, o0, lim);
+    }
+}
+
+// PADDED: some main regions hold no whole number of chunks (ScanParams::xcd_pad != 0): every group
+// reads through a buffer resource.  Otherwise plain global loads (1-2 % shorter C5 launches).
+template <uint64_t POLY, int BLOCK, bool PADDED>
 __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p) {
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
@@ -2516,25 +2546,45 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint32_t voff = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
     const uint64_t dq = nwx / CPB, dr = nwx - dq * CPB;   // chunk step as (buffers, chunks)
+    // every buffer's main region is front-padded with virtual zeros to CPB whole chunks (pad < chunk)
+    const uint32_t pad = p.xcd_pad;
     auto cur_at = [&](uint64_t c) -> XcdCursor {
         const uint64_t b = c / CPB;
         const BatchPos bp = batch_pos(p, b);
-        return XcdCursor{b, c - b * CPB, karg64(p.bbase, bp.j) + bp.i * p.stride + hoff};
+        return XcdCursor{b, c - b * CPB, karg64(p.bbase, bp.j) + bp.i * p.stride + hoff - pad};
     };
     auto cur_next = [&](XcdCursor &x) {
         uint64_t b = x.b + dq, k = x.k + dr;
         if (k >= CPB) k -= CPB, ++b;
         if (b != x.b) {
             const BatchPos bp = batch_pos(p, b);
-            x.main = karg64(p.bbase, bp.j) + bp.i * p.stride + hoff;
+            x.main = karg64(p.bbase, bp.j) + bp.i * p.stride + hoff - pad;
         }
         x.b = b, x.k = k;
     };
-    // prefetch cursor: chunk fc, group fg; fq groups issued
+    // prefetch cursor: chunk fc, group fg; fq groups issued.  A group reads through a buffer resource
+    // based at its first real byte with its real bytes as records; a lane's offset into the pad comes
+    // out negative (wrapped), is clamped to the record count and reads zero.
     XcdCursor fc = nq ? cur_at(c0) : XcdCursor{0, 0, 0};
     uint32_t fq = 0, fg = 0;
-    auto f_addr = [&]() -> uint64_t {
-        return rfl64(fq < nq ? fc.main + fc.k * kXcdChunk + (uint64_t)fg * (kB64Row * kB64RowsPerGroup) : dummy);
+    constexpr uint32_t kGB = kB64Row * kB64RowsPerGroup;
+    auto f_adj = [&]() -> uint32_t {  // pad bytes at the front of group fg of chunk fc.k
+        if (fc.k != 0 || pad <= fg * kGB) return 0u;
+        const uint32_t a = pad - fg * kGB;
+        return a < kGB ? a : kGB;
+    };
+    auto f_rsrc = [&]() {
+        return fq < nq ? list_rsrc(fc.main + fc.k * kXcdChunk + (uint64_t)fg * kGB + f_adj(), kGB - f_adj())
+                       : list_rsrc(dummy, 0u);
+    };
+    auto f_off = [&]() { return fq < nq ? voff - f_adj() : voff; };
+    auto f_lim = [&]() { return fq < nq ? kGB - f_adj() : 0u; };
+    auto f_addr = [&]() -> uint64_t { return rfl64(fq < nq ? fc.main + fc.k * kXcdChunk + (uint64_t)fg * kGB : dummy); };
+    auto issue = [&](B64Group &g) {
+        if constexpr (PADDED)
+            xcd_issue<0>(g, f_rsrc(), f_off(), f_lim());
+        else
+            stream64_issue<0>(g, voff, f_addr());
     };
     auto f_next = [&]() {
         ++fq;
@@ -2547,7 +2597,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint64_t jt = threadIdx.x < 256 ? *(gu64 *)(p.d_pcols + threadIdx.x) : 0ull;
     B64Group ra, rb, rc;
     if (nq) {
-        stream64_issue<0>(ra, voff, f_addr());
+        issue(ra);
         f_next();
     }
     b64x4_build_tables<POLY>(lds);
@@ -2650,9 +2700,14 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
         final_parts(false);
         return;
     }
-    stream64_issue<0>(rb, voff, f_addr());
+    issue(rb);
     f_next();
 
+    // the head state enters lane (pad mod 512) / 8 at the start of chunk 0 divided by X^jr (X = x^(8*512),
+    // jr = the pad's row): that lane's words before the pad are zero, so jr row steps bring it to the head
+    // state exactly where the first real word joins (crc32_list_stream_kernel's head entry)
+    const uint64_t *xinv = p.d_pcols + 256 + 40 * 64 + 4 * 256 * 64;  // [jr < 32][j]: X^(-jr) * x^j
+    const uint32_t jr = pad / kB64Row, l0 = (pad % kB64Row) / 8u;
     XcdCursor sc = cur_at(c0);
     uint32_t g = 0, q = 0;
     auto step = [&](B64Group &cur, B64Group &nxt) {
@@ -2662,13 +2717,25 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
             } else {
                 if (pn) part_finish();
                 pb = sc.b, pn = 0;
-                u = sc.k == 0 && lane == 0 ? head_state<false>(p, sc.b, eng) : 0ull;
+                u = 0ull;
+                if (sc.k == 0) {
+                    uint64_t s_h = head_state<false>(p, sc.b, eng);
+                    if (jr) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * jr);
+                    if ((uint32_t)lane == l0) u = s_h;
+                }
             }
             ++pn, pk = sc.k;
         }
-        const uint64_t sn = f_addr();
-        f_next();
-        u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
+        if constexpr (PADDED) {
+            const __amdgpu_buffer_rsrc_t rs = f_rsrc();
+            const uint32_t fo = f_off(), fl = f_lim();
+            f_next();
+            u = xcd_rows<0>(u, cur, nxt, rs, fo, fl, eng);
+        } else {
+            const uint64_t sn = f_addr();
+            f_next();
+            u = stream64_rows<0>(u, cur, nxt, voff, sn, eng);
+        }
         ++q;
         if (++g == (uint32_t)kXcdChunkGroups) {
             g = 0;
@@ -3405,8 +3472,10 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
         case ALG_CRC64NVME:
             if (p->stream == 3 && !list)  // many short buffers: 16 lanes per buffer
                 launch(crc64_rows16_kernel<kPoly64Nvme>, nblocks, kR16Block, s, p, ev);
-            else if (p->stream == 5 && !list)  // long buffers: XCD-window chunks
-                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock>, nblocks, kXcdBlock, s, p, ev);
+            else if (p->stream == 5 && !list && p->xcd_pad)  // long buffers: XCD-window chunks, front pads
+                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, true>, nblocks, kXcdBlock, s, p, ev);
+            else if (p->stream == 5 && !list)  // long buffers of whole chunks
+                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list)

@@ -269,7 +269,7 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
     auto it = d->xcd.find(key);
     if (it == d->xcd.end()) {
         const uint64_t poly = alg_poly(alg);
-        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64, 0);
+        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64, 0);
         const uint64_t J = gf2_xpow8n((uint64_t)kXcdChunkBytes * (nwx - 1), poly, 64);
         for (int n = 0; n < 16; ++n)
             for (uint64_t v = 0; v < 16; ++v) c[16 * n + v] = gf2_mulmod(v << (4 * n), J, poly, 64);
@@ -294,6 +294,16 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
                 pv = gf2_mulmod(pv, base, poly, 64);
             }
             base = pv;  // base^256
+        }
+        // X^(-jr) columns, X = x^(8*512), jr < 32: the head state's entry behind a front pad
+        uint64_t xj = 1ull << 63;  // x^0
+        for (int jr = 0; jr < 32; ++jr) {
+            uint64_t col = xj;
+            for (int j = 0; j < 64; ++j) {
+                c[256 + 40 * 64 + 4 * 256 * 64 + 64 * jr + j] = col;
+                col = gf2_mulx(col, poly);
+            }
+            for (int i = 0; i < 8 * 512; ++i) xj = inv_mulx64(xj, poly);
         }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 8);
@@ -782,11 +792,12 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
         return launch_scan(d, alg, p, count, 1, ml * count, s);
     }
     // long CRC64NVME buffers of whole chunks: XCD-window chunk order (crc64_xcd_kernel)
-    if (!w32 && kXcd && ml % kXcdChunkBytes == 0 && ml / kXcdChunkBytes >= kXcdMinChunks) {
+    if (!w32 && kXcd && ml >= kXcdMinChunks * kXcdChunkBytes) {
         const uint64_t blocks = ((uint64_t)d->cus * (1024 / kXcdBlock)) & ~7ull, nwx = blocks * (kXcdBlock / 64) / 8;
         if (blocks >= 8) {
             p.stream = 5;
-            p.tiles_per_buf = ml / kXcdChunkBytes;
+            p.tiles_per_buf = (ml + kXcdChunkBytes - 1) / kXcdChunkBytes;
+            p.xcd_pad = (uint32_t)(p.tiles_per_buf * kXcdChunkBytes - ml);
             p.ntiles = p.tiles_per_buf * count;
             int rc = get_braid64_consts(d, alg, &p.d_kvals);
             if (!rc) rc = get_xcd_consts(d, alg, nwx, &p.d_pcols);

@@ -85,6 +85,7 @@ struct ScanParams {
     // seed_all), result bout[j][i].  A plain strided launch is nbatch = 1.  All bases share their
     // alignment mod 16 (the host splits the launch otherwise).
     uint32_t nbatch;
+    uint32_t xcd_pad;               // crc64_xcd_kernel: virtual zero bytes in front of every main region (< chunk)
     uint64_t bcount;
     uint64_t bbase[kMaxBatches], bout[kMaxBatches], bseed[kMaxBatches];
     // ---- dynamic tile pool (W=32 braided scan, strided batches): tiles [0, nstatic) are split

@@ -280,7 +280,7 @@ def kernel_name(alg, nbuf, L):
             return "crc_lanes_kernel"
         if nbuf >= 16384 and L % 1024 == 0 and 1024 <= L <= 256 << 10:
             return "crc64_rows16_kernel"
-        if L % 16384 == 0 and L // 16384 >= 256:
+        if L >= 256 * 16384:
             return "crc64_xcd_kernel"
         return "crc64_stream4_kernel"
     if alg == "xxh64":

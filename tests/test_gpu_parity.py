@@ -255,21 +255,26 @@ def test_crc64_rows16_short_buffers(engine, count, L, stride, off, seeded):
             assert got[i] == oracle.crc("crc64nvme", h[off + i * stride: off + i * stride + L], seeds[i]), i
 
 
-@pytest.mark.parametrize("count,chunks,head,tail,seeded", [
-    (3, 300, 13, 7, True),     # unaligned heads and tails, seeds; XCD eighths cut inside buffers
-    (5, 256, 0, 0, False),     # the fewest chunks taken: a wave's next chunk is two buffers on
-    (2, 4099, 11, 5, True),    # 64 MiB + 3 chunks: parts of 8-9 chunks per wave, ragged eighths
-    (9, 1024, 0, 9, False),    # nine 16 MiB buffers over eight XCDs
-    (1, 4101, 3, 9, True),     # one buffer over all eight XCDs: every eighth a part, shifts up to 3.6 K chunks
+@pytest.mark.parametrize("count,chunks,head,tail,seeded,extra", [
+    (3, 300, 13, 7, True, 0),     # unaligned heads and tails, seeds; XCD eighths cut inside buffers
+    (5, 256, 0, 0, False, 0),     # the fewest chunks taken: a wave's next chunk is two buffers on
+    (2, 4099, 11, 5, True, 0),    # 64 MiB + 3 chunks: parts of 8-9 chunks per wave, ragged eighths
+    (9, 1024, 0, 9, False, 0),    # nine 16 MiB buffers over eight XCDs
+    (1, 4101, 3, 9, True, 0),     # one buffer over all eight XCDs: every eighth a part, shifts up to 3.6 K chunks
+    (3, 300, 13, 7, True, 16),    # front pad 16368: the head enters lane 62 at row 31
+    (2, 260, 0, 0, False, 2608),  # front pad 13776: lane 58, row 26
+    (1, 4096, 5, 3, True, 8192),  # front pad 8192: lane 0, row 16 (two whole groups of zeros)
+    (4, 256, 11, 0, False, 4080), # front pad 12304: lane 2, row 24
 ])
-def test_crc64_xcd_long_buffers(engine, count, chunks, head, tail, seeded):
-    """Strided CRC64NVME batches whose main regions are whole 16 KiB chunks (at least 256) take
+def test_crc64_xcd_long_buffers(engine, count, chunks, head, tail, seeded, extra):
+    """Strided CRC64NVME batches with main regions of at least 256 chunks of 16 KiB take
     crc64_xcd_kernel: XCD-window chunk order, the chunk jump from nibble tables, parts moved to the
-    buffer end and joined by chunk count."""
+    buffer end and joined by chunk count; a main region of no whole number of chunks is front-padded
+    with virtual zeros (buffer-resource loads) and the head state enters behind the pad."""
     import torch
 
     off = (16 - head) % 16
-    L = head + chunks * 16384 + tail
+    L = head + chunks * 16384 + extra + tail
     stride = (L + 15) // 16 * 16
     d = dev_random(stride * count + off + 64, 0x5CD + count)
     rng = random.Random(chunks)

@@ -10,7 +10,10 @@ shares and the byte tables are test_braid64_model's:
   * a part (a wave's chunks of one buffer) ends with the lane shares sum_l u_l K_l, moved to the
     buffer end by x^(8 * chunk * m) as one product per nonzero byte v of m (the host's byte-level
     columns of x^(8 * chunk * v * 256^L)), XORed into the buffer's accumulator with its chunk count;
-    the part that completes the count finalises the buffer (tail bytes, complement).
+    the part that completes the count finalises the buffer (tail bytes, complement);
+  * a main region of no whole number of chunks is front-padded with virtual zeros (the kernel's
+    buffer-resource loads return zeros there) and the head state enters lane (pad mod 512) / 8 of
+    chunk 0 divided by X^(pad / 512), X = x^(8 * 512).
 
 The kernel's chunk is 32 rows (16 KiB); the model takes a few rows per chunk (the algebra does not
 depend on it) and small XCD / wave counts, so the cuts fall at every kind of place.
@@ -20,7 +23,7 @@ import random
 import pytest
 
 from oracle import oracle
-from tests.test_braid64_model import M64, ROW, Braid64, mulmod, xpow8n
+from tests.test_braid64_model import M64, ROW, Braid64, inv_mulx, mulmod, xpow8n
 
 
 @pytest.fixture(scope="module")
@@ -56,11 +59,16 @@ def xcd_model(br, data, ptrs, L, seeds, rows_per_chunk, nx, nwx):
     heads, mains = [], []
     for p in ptrs:
         H, E = (p + 15) & ~15, (p + L) & ~15
-        assert (E - H) % chunk == 0 and E > H
+        assert E > H
         heads.append(H)
         mains.append(E - H)
-    cpb = mains[0] // chunk
     assert all(m == mains[0] for m in mains)
+    cpb = -(-mains[0] // chunk)
+    pad = cpb * chunk - mains[0]  # virtual zeros in front of every main region
+    jr, l0 = pad // ROW, (pad % ROW) // 8
+    xinv = 1 << 63  # X^(-jr), X = x^(8 * ROW)
+    for _ in range(8 * ROW * jr):
+        xinv = inv_mulx(xinv)
     nc = cpb * len(ptrs)
     J = xpow8n(chunk * (nwx - 1))
     jt = jump_tables(J)
@@ -99,14 +107,15 @@ def xcd_model(br, data, ptrs, L, seeds, rows_per_chunk, nx, nwx):
                     pb, pn = b, 0
                     u = [0] * 64
                     if k == 0:
-                        u[0] = head_state(b)
+                        u[l0] = mulmod(head_state(b), xinv)
                 pn += 1
                 pk = k
-                base = heads[b] + k * chunk
+                base = heads[b] - pad + k * chunk
                 for row in range(rows_per_chunk):
                     for lane in range(64):
                         a = base + ROW * row + 8 * lane
-                        u[lane] = br.step(u[lane] ^ int.from_bytes(data[a: a + 8], "little"))
+                        w = int.from_bytes(data[a: a + 8], "little") if a >= heads[b] else 0
+                        u[lane] = br.step(u[lane] ^ w)
                 c += nwx
             if pn:
                 r = 0
@@ -129,15 +138,18 @@ def test_jump_tables_and_byte_shifts():
         assert shift_bytes(r, m, 16384) == mulmod(r, xpow8n(16384 * m)), m
 
 
-@pytest.mark.parametrize("count,cpb,head,tail,nx,nwx", [
-    (3, 5, 13, 7, 2, 3),    # eighths (here halves) cut inside buffers; a wave's chunks span buffers
-    (2, 7, 0, 0, 3, 2),     # jumps inside buffers; three "XCDs"
-    (5, 2, 5, 11, 2, 4),    # more waves than a buffer's chunks: a wave's next chunk two buffers on
+@pytest.mark.parametrize("count,cpb,head,tail,nx,nwx,extra", [
+    (3, 5, 13, 7, 2, 3, 0),     # eighths (here halves) cut inside buffers; a wave's chunks span buffers
+    (2, 7, 0, 0, 3, 2, 0),      # jumps inside buffers; three "XCDs"
+    (5, 2, 5, 11, 2, 4, 0),     # more waves than a buffer's chunks: a wave's next chunk two buffers on
+    (3, 4, 13, 7, 2, 3, 16),    # front pad of a chunk less 16 bytes: the head enters the last row's lane 62
+    (2, 5, 0, 9, 3, 2, 528),    # front pad 496: row 0, lane 62
+    (4, 3, 5, 0, 2, 3, 512),    # front pad 512: row 1, lane 0
 ])
-def test_xcd_walk_matches_oracle(br, count, cpb, head, tail, nx, nwx):
+def test_xcd_walk_matches_oracle(br, count, cpb, head, tail, nx, nwx, extra):
     rows = 2
     chunk = ROW * rows
-    L = head + cpb * chunk + tail
+    L = head + cpb * chunk + extra + tail
     stride = (L + 15) // 16 * 16
     off = (16 - head) % 16
     rng = random.Random(count * 131 + cpb)
