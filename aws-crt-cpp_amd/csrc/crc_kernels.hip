@@ -2761,6 +2761,163 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
 }
 
 // ------------------------------------------------------------------------------------------
+// Ragged CRC64NVME lists on the streaming scan (crc64_list_stream_kernel, round 3):
+// crc32_list_stream_kernel's walk at W = 64.  Every buffer's main region is front-padded to whole
+// 4 KiB groups and the list is one sequence of groups, split evenly over the waves (cut anywhere, also
+// inside buffers); groups read through buffer resources whose range check supplies the pad's zeros; the
+// head state enters lane (pad mod 512)/8 of group 0 divided by X^j (X = x^(8*512), j = the pad's row);
+// a part of a buffer ends with the lane shares (nibble-table K_l product, wave XOR), is moved to the
+// buffer end by x^(8*4096*m) for the m groups after it, and finishes the buffer or joins it through the
+// per-buffer accumulator and group count.  The tables, the nibble-table finish and the row step are
+// crc64_stream4_kernel's (4 copies, two 512-thread workgroups per CU).  Constants: ScanParams::d_pcols
+// = engine.cpp get_xcd_consts (the X^(-j) and x^(8*4096*2^i) columns).
+constexpr uint32_t kXcdXinvU64 = 256 + 40 * 64 + 4 * 256 * 64;  // get_xcd_consts: X^(-j) columns, j < 32
+constexpr uint32_t kXcdGshiftU64 = kXcdXinvU64 + 32 * 64;        // x^(8*4096*2^i) columns, i < 40
+
+template <uint64_t POLY>
+__global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanParams p) {
+    using B = Braid64<POLY, 4>;
+    __shared__ __attribute__((aligned(16))) char lds[kB64x4Lds];
+    constexpr int WAVES = 8;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6));
+    const uint64_t *wbuf = p.d_wave_buf, *woff = p.d_tile_prefix, *wq = p.d_tile_prefix + nw + 1;
+    const uint64_t b0 = sload64(wbuf + gw), b_end = sload64(wbuf + gw + 1);
+    const uint32_t g0 = (uint32_t)sload64(woff + gw);
+    const uint32_t nq = (uint32_t)(sload64(wq + gw + 1) - sload64(wq + gw));  // groups of this wave
+    const uint32_t lo8 = 8u * (uint32_t)lane;
+    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
+    const uint64_t *xinv = p.d_pcols + kXcdXinvU64;
+    const uint64_t *gsh = p.d_pcols + kXcdGshiftU64;
+
+    // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
+    const bool owns = b0 < b_end || nq;
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0};
+    uint32_t fq = 0, fg = g0;
+    if (nq)
+        while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
+    auto f_adj = [&]() -> uint32_t { return fg == 0 ? fc.pad : 0u; };
+    auto f_rsrc = [&]() {
+        return fq < nq ? list_rsrc(fc.vb + (uint64_t)fg * kWaveGroupBytes + f_adj(), kWaveGroupBytes - f_adj())
+                       : list_rsrc(dummy, 0u);
+    };
+    auto f_off = [&]() { return fq < nq ? lo8 - f_adj() : lo8; };
+    auto f_lim = [&]() { return fq < nq ? kWaveGroupBytes - f_adj() : 0u; };
+    auto f_next = [&]() {
+        if (++fq >= nq) return;
+        if (++fg == fc.vg) {
+            do fc = lbuf_at(p, fc.b + 1);
+            while (fc.vg == 0);
+            fg = 0;
+        }
+    };
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
+    // the two primed slots are issued unconditionally (zero-record placeholders for a wave without
+    // groups), so the compiler's wait-count pass sees one prologue shape
+    B64Group ra, rb, rc;
+    xcd_issue<0>(ra, f_rsrc(), f_off(), f_lim());
+    f_next();
+    b64x4_build_tables<POLY>(lds);
+    b64x4_build_nib<POLY>(lds, kl);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B eng;
+    eng.init(lds, lane);
+    eng.kl = kl;
+    xcd_issue<0>(rb, f_rsrc(), f_off(), f_lim());
+    f_next();
+    auto drain = [&]() {  // the placeholder rows land before anything reuses their registers
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]),
+                     "+v"(ra.w[5]), "+v"(ra.w[6]), "+v"(ra.w[7])::"memory");
+        asm volatile("" : "+v"(rb.w[0]), "+v"(rb.w[1]), "+v"(rb.w[2]), "+v"(rb.w[3]), "+v"(rb.w[4]), "+v"(rb.w[5]), "+v"(rb.w[6]),
+                     "+v"(rb.w[7]));
+        asm volatile("" : "+v"(rc.w[0]), "+v"(rc.w[1]), "+v"(rc.w[2]), "+v"(rc.w[3]), "+v"(rc.w[4]), "+v"(rc.w[5]), "+v"(rc.w[6]),
+                     "+v"(rc.w[7]));
+    };
+    // scan cursor: buffer sc, group g, the part's first group ga
+    LBuf sc = fc;
+    if (owns) sc = lbuf_at(p, b0);
+    auto finish_empty = [&]() {  // a buffer without a main region: its head fold is the whole CRC
+        const uint64_t s_h = head_state<true>(p, sc.b, eng);
+        if (lane == 0) finalize<true>(p, sc.b, s_h, eng);
+    };
+    if (owns)
+        while (sc.vg == 0) {
+            finish_empty();
+            if (!nq && sc.b + 1 >= b_end) break;
+            sc = lbuf_at(p, sc.b + 1);
+        }
+    if (!nq) {
+        drain();
+        return;
+    }
+    uint32_t g = g0, ga = g0, q = 0;
+    uint64_t u = 0;
+    auto part_begin = [&]() {
+        ga = g;
+        u = 0;
+        if (g == 0) {
+            uint64_t s_h = head_state<true>(p, sc.b, eng);
+            const uint32_t j = (sc.pad >> 9) & 7u;
+            if (j) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * j);
+            if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
+        }
+    };
+    auto part_finish = [&]() {
+        uint64_t r = wave_xor64_s(eng.mulK(u));
+        for (uint32_t m = sc.vg - g, i = 0; m; m >>= 1, ++i)
+            if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
+        if (lane != 0) return;
+        if (ga == 0 && g == sc.vg) {
+            finalize<true>(p, sc.b, r, eng);
+            return;
+        }
+        (void)sx_xor64_ret(&p.d_acc[sc.b], (unsigned long long)r);  // performed before it is counted
+        const uint32_t n = g - ga, c = sx_add32_ret(&p.d_cnt[sc.b], n);
+        if (c + n == sc.vg) {
+            const uint64_t fin = sx_swap64_ret(&p.d_acc[sc.b], 0ull);
+            sx_store32(&p.d_cnt[sc.b], 0u);
+            finalize<true>(p, sc.b, fin, eng);
+        }
+    };
+    part_begin();
+    auto step = [&](B64Group &cur, B64Group &nxt) {
+        const __amdgpu_buffer_rsrc_t rs = f_rsrc();
+        const uint32_t fo = f_off(), fl = f_lim();
+        f_next();
+        u = xcd_rows<0>(u, cur, nxt, rs, fo, fl, eng);
+        ++q;
+        if (++g == sc.vg || q == nq) {
+            part_finish();
+            if (q < nq) {
+                for (;;) {  // the next buffer with a main region, finishing the empty ones on the way
+                    sc = lbuf_at(p, sc.b + 1);
+                    if (sc.vg) break;
+                    finish_empty();
+                }
+                g = 0;
+                part_begin();
+            }
+        }
+    };
+    step(ra, rc);
+    while (q + 3 <= nq) {  // whole rotations, then the rest (see crc32_stream_kernel)
+        step(rb, ra);
+        step(rc, rb);
+        step(ra, rc);
+    }
+    if (q < nq) {
+        step(rb, ra);
+        if (q < nq) step(rc, rb);
+    }
+    drain();
+    while (sc.b + 1 < b_end) {  // trailing buffers without a main region
+        sc = lbuf_at(p, sc.b + 1);
+        finish_empty();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // W = 64 scan of many short uniform buffers (the C4 per-GPU shard: 131,072 x 8 KiB), 16 lanes per
 // buffer.  A wave scans four buffers at once, one per 16-lane row: lane t of row r owns the 8-byte
 // word at 8t of every 128-byte row of buffer 4s + r, so the braid step's tables fold in the skip over
@@ -3478,6 +3635,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
                 launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
+            else if (list && p->stream == 4)  // ragged lists: the list streaming scan
+                launch(crc64_list_stream_kernel<kPoly64Nvme>, nblocks, 512, s, p, ev);
             else if (list)
                 launch(crc64_braid_kernel<kPoly64Nvme, true>, nblocks, kBlock, s, p, ev);
             else
