@@ -434,7 +434,13 @@ constexpr bool kRows16 = AMDCRC_ROWS16 != 0;
 #define AMDCRC_XCD 1
 #endif
 constexpr bool kXcd = AMDCRC_XCD != 0;
-constexpr uint64_t kXcdMinChunks = 256;
+#ifndef AMDCRC_XCD_MIN_CHUNKS  // compile-time only (A/B builds)
+#define AMDCRC_XCD_MIN_CHUNKS 256
+#endif
+constexpr uint64_t kXcdMinChunks = AMDCRC_XCD_MIN_CHUNKS;
+#ifndef AMDCRC_XP_STREAM64  // experiment: 0 sends aligned strided CRC64NVME batches to crc64_braid_kernel
+#define AMDCRC_XP_STREAM64 1
+#endif
 constexpr uint64_t kRows16MinBuffers = 4 * 4096;
 constexpr uint64_t kRows16MaxBytes = 256u << 10;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
@@ -778,7 +784,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     const bool small = ml * count < kSmallBatchBytes;
     const uint64_t wpc = w32 ? 8 * (small ? 1 : 2) : small ? 4 : (uint64_t)kWavesPerBlock;
     const uint32_t seg_stream = choose_seg(d, ml * count, ml, 1, wpc);
-    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0;
+    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0 && (w32 || AMDCRC_XP_STREAM64);
     if (stream) p.seg = seg_stream;
     // W=32 braided scan: every wave scans one static tile, then claims tiles from its workgroup's
     // pool, where the pool does not shrink the tiles (smaller tiles cost a tile finish per 8 KiB and

@@ -376,6 +376,29 @@ def test_ragged_list_random(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ["crc32c", "crc64nvme"])
+def test_list_long_buffers_cut_over_all_waves(engine, alg):
+    """list streaming scans (crc32_list_stream_kernel, crc64_list_stream_kernel): a 300 MiB buffer cut
+    into parts on thousands of waves (part shifts of up to 2^16 groups, accumulator and count joins)
+    beside empty, short and 64 MiB buffers, at every kind of front pad; seeds on all."""
+    import torch
+
+    lens = [(300 << 20) + 13, 0, 17, (64 << 20) - 8, (5 << 20) + 4095, 4096, 1]
+    offs, pos = [], 3
+    for ln in lens:
+        offs.append(pos)
+        pos += ln + 7
+    d = dev_random(pos + 64, 0x1A)
+    rng = random.Random(0x1A + ALG[alg])
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.checksum(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_fuzz_lengths_alignments_seeds(engine, alg):
     """GPU-vs-oracle differential fuzzing: 2000 buffers of uniformly random length
