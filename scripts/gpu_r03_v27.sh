@@ -6,6 +6,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; T=${TAG:-r03v27}; O=$R/gpurun_out/$T; mkdir -p $O; export TMPDIR=/tmp
 Q="--no-configs --no-cpu-baseline --e2e-batches 0 --no-read-ceiling"
+cp ab/libA.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so || exit 1
+bash scripts/gpu_step.sh 200 $O/pytest_lists_A.log python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "long_buffers_cut or ragged_list or front_pads" --timeout 120 --timeout-method thread -p no:cacheprovider &&
+tail -1 $O/pytest_lists_A.log && grep -q " passed" $O/pytest_lists_A.log && ! grep -q "failed" $O/pytest_lists_A.log || exit 1
 for v in X B; do
   cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so || exit 1
   bash scripts/gpu_step.sh 300 $O/pytest_$v.log python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "crc64 or C5 or c5 or strided" --timeout 120 --timeout-method thread -p no:cacheprovider &&
