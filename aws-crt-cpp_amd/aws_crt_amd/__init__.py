@@ -187,14 +187,34 @@ def checksum_strided(alg: int, base, stride: int, length: int, count: int, seeds
     return out
 
 
+def stream_release(stream) -> None:
+    """aws_crt_amd_stream_release: the stream's engine state goes back for reuse (call before the
+    stream is dropped, if it was used with the engine)."""
+    L = lib()
+    L.aws_crt_amd_stream_release.argtypes = [ctypes.c_void_p]
+    _check(L.aws_crt_amd_stream_release(_stream_handle(stream)))
+
+
+def stream_states() -> dict:
+    """live / spare / ever-created per-stream engine states of the current device"""
+    L = lib()
+    sz = ctypes.c_size_t
+    L.aws_crt_amd_stream_states.argtypes = [ctypes.POINTER(sz)] * 3
+    a, b, c = sz(), sz(), sz()
+    _check(L.aws_crt_amd_stream_states(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return {"live": a.value, "spare": b.value, "created": c.value}
+
+
 class _Batch(ctypes.Structure):
     _fields_ = [("d_base", ctypes.c_void_p), ("d_seeds", ctypes.c_void_p), ("d_out", ctypes.c_void_p)]
 
 
 class BatchSet:
-    """A prepared submission of several uniform batches of one shape (aws_crt_amd_checksum_batches):
-    the descriptor array is built once, like a producer filling a submission queue, and `run()` only
-    submits it.  `batches`: (base address / tensor, seeds tensor or None, out tensor) per batch."""
+    """A prepared submission of several uniform batches of one shape (aws_crt_amd_plan_create over
+    the batches of aws_crt_amd_checksum_batches): the planning -- runs of batches, kernel, tile size,
+    geometry, constants -- is done once, like a producer filling a submission queue, and `run()` only
+    launches the plan (aws_crt_amd_plan_launch).  `batches`: (base address / tensor, seeds tensor or
+    None, out tensor) per batch."""
 
     def __init__(self, alg: int, batches, stride: int, length: int, count: int):
         self.n = len(batches)
@@ -202,120 +222,200 @@ class BatchSet:
         # temporary freed (and reused by the caching allocator) under a queued launch would be read or
         # written by it
         self._keep = [t for b in batches for t in b if hasattr(t, "data_ptr")]
-        self.arr = (_Batch * max(self.n, 1))()
+        self._cuda = [t for t in self._keep if getattr(t, "is_cuda", False)]
+        arr = (_Batch * max(self.n, 1))()
         for i, (base, seeds, out) in enumerate(batches):
-            self.arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
-            self.arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
-            self.arr[i].d_out = out.data_ptr()
-        self.args = (alg, self.arr, self.n, stride, length, count)
+            arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+            arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
+            arr[i].d_out = out.data_ptr()
         L = lib()
-        self.fn = L.aws_crt_amd_checksum_batches
-        self.fn.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
-                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+        L.aws_crt_amd_plan_create.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
+                                              ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+        L.aws_crt_amd_plan_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.aws_crt_amd_plan_launches.argtypes = [ctypes.c_void_p]
+        L.aws_crt_amd_plan_launches.restype = ctypes.c_size_t
+        L.aws_crt_amd_plan_destroy.argtypes = [ctypes.c_void_p]
+        self._destroy = L.aws_crt_amd_plan_destroy
+        h = ctypes.c_void_p()
+        _check(L.aws_crt_amd_plan_create(alg, arr, self.n, stride, length, count, ctypes.byref(h)))
+        self._plan = h
+        self.fn = L.aws_crt_amd_plan_launch
+        self.launches = int(L.aws_crt_amd_plan_launches(h))
 
     def run(self, stream=None) -> None:
-        rc = self.fn(*self.args, _stream_handle(stream))
+        rc = self.fn(self._plan, _stream_handle(stream))
         if rc != 0:
             _check(rc)
-        if stream is not None and hasattr(stream, "cuda_stream"):
+        if self._cuda and stream is not None and hasattr(stream, "cuda_stream"):
             # a launch on a side stream: the caching allocator must not hand these blocks out again
             # before that stream has finished with them
-            for t in self._keep:
-                if getattr(t, "is_cuda", False):
-                    t.record_stream(stream)
+            for t in self._cuda:
+                t.record_stream(stream)
+
+    def __del__(self):
+        if getattr(self, "_plan", None):
+            self._destroy(self._plan)
+            self._plan = None
 
 
 def checksum_batches(alg: int, batches, stride: int, length: int, count: int, stream=None) -> None:
     """Several uniform batches of one shape, each (base address, seeds tensor or None, out tensor),
     coalesced into as few launches as the engine allows (aws_crt_amd_checksum_batches)."""
-    BatchSet(alg, batches, stride, length, count).run(stream)
+    n = len(batches)
+    arr = (_Batch * max(n, 1))()
+    for i, (base, seeds, out) in enumerate(batches):
+        arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
+        arr[i].d_seeds = seeds.data_ptr() if seeds is not None else None
+        arr[i].d_out = out.data_ptr()
+    L = lib()
+    L.aws_crt_amd_checksum_batches.argtypes = [ctypes.c_int, ctypes.POINTER(_Batch), ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p]
+    _check(L.aws_crt_amd_checksum_batches(alg, arr, n, stride, length, count, _stream_handle(stream)))
+    if stream is not None and hasattr(stream, "cuda_stream"):
+        for b in batches:
+            for t in b:
+                if getattr(t, "is_cuda", False):
+                    t.record_stream(stream)
+
+
+class _QueueOptions(ctypes.Structure):
+    _fields_ = [("max_batches", ctypes.c_size_t), ("max_age_us", ctypes.c_uint64)]
+
+
+TICKET_QUEUED, TICKET_LAUNCHED = 1, 2
 
 
 class Queue:
     """A submission queue (aws_crt_amd_queue_*): batches of one shape pushed one at a time are launched
-    together, when 32 are queued and at flush() / close().  Keeps the pushed tensors referenced until
-    their launch is on the stream."""
+    together, at max_batches queued (32 by default), once the oldest has waited max_age_us (0: no age
+    bound), and at flush() / wait() / close().  push() returns the batch's ticket; status(ticket) /
+    wait(ticket) give its completion (0) or the error of the launch that dropped it.  The pushed tensors
+    stay referenced until the engine has launched them (every ticket below first_pending()); thread-safe."""
 
-    def __init__(self, alg: int, stride: int, length: int, count: int, stream=None):
+    def __init__(self, alg: int, stride: int, length: int, count: int, stream=None, max_batches: int = 0,
+                 max_age_us: int = 0):
+        import threading
+
         L = lib()
-        L.aws_crt_amd_queue_create.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
-                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
-        L.aws_crt_amd_queue_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-        L.aws_crt_amd_queue_flush.argtypes = [ctypes.c_void_p]
-        L.aws_crt_amd_queue_pending.argtypes = [ctypes.c_void_p]
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        L.aws_crt_amd_queue_create_ex.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                                  vp, ctypes.POINTER(_QueueOptions), ctypes.POINTER(vp)]
+        L.aws_crt_amd_queue_push_ex.argtypes = [vp, vp, vp, vp, ctypes.POINTER(u64)]
+        L.aws_crt_amd_queue_flush.argtypes = [vp]
+        L.aws_crt_amd_queue_pending.argtypes = [vp]
         L.aws_crt_amd_queue_pending.restype = ctypes.c_size_t
-        L.aws_crt_amd_queue_destroy.argtypes = [ctypes.c_void_p]
+        L.aws_crt_amd_queue_first_pending.argtypes = [vp]
+        L.aws_crt_amd_queue_first_pending.restype = u64
+        L.aws_crt_amd_queue_status.argtypes = [vp, u64]
+        L.aws_crt_amd_queue_wait.argtypes = [vp, u64]
+        L.aws_crt_amd_queue_destroy.argtypes = [vp]
         self._L = L
         self._stream = stream
-        self._keep = []
-        h = ctypes.c_void_p()
-        _check(L.aws_crt_amd_queue_create(alg, stride, length, count, _stream_handle(stream), ctypes.byref(h)))
+        self._keep = {}  # ticket -> tensors, until the ticket is launched
+        self._lock = threading.Lock()
+        h = vp()
+        opt = _QueueOptions(max_batches, max_age_us)
+        _check(L.aws_crt_amd_queue_create_ex(alg, stride, length, count, _stream_handle(stream), ctypes.byref(opt),
+                                             ctypes.byref(h)))
         self._h = h
-        self._n = 0  # pushed since the last launch (the engine launches at 32 queued batches)
 
-    def _launched(self):
-        self._n = 0
-        if self._stream is not None and hasattr(self._stream, "cuda_stream"):
-            for t in self._keep:
-                if getattr(t, "is_cuda", False):
-                    t.record_stream(self._stream)
-        self._keep = []
+    def _release_launched(self):
+        """drop the references of every launched ticket (after record_stream on a side stream)"""
+        first = int(self._L.aws_crt_amd_queue_first_pending(self._h)) if self._h else 1 << 64
+        done = [t for t in self._keep if t < first]
+        side = self._stream is not None and hasattr(self._stream, "cuda_stream")
+        for t in done:
+            for x in self._keep.pop(t):
+                if side and getattr(x, "is_cuda", False):
+                    x.record_stream(self._stream)
 
-    def push(self, base, out, seeds=None) -> None:
-        for t in (base, out, seeds):
-            if hasattr(t, "data_ptr"):
-                self._keep.append(t)
+    def push(self, base, out, seeds=None) -> int:
         b = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
-        _check(self._L.aws_crt_amd_queue_push(self._h, b, seeds.data_ptr() if seeds is not None else None, out.data_ptr()))
-        self._n += 1
-        if self._n == 32:
-            self._launched()
+        tk = ctypes.c_uint64(0)
+        with self._lock:
+            rc = self._L.aws_crt_amd_queue_push_ex(self._h, b, seeds.data_ptr() if seeds is not None else None,
+                                                   out.data_ptr(), ctypes.byref(tk))
+            if tk.value:
+                self._keep[tk.value] = [t for t in (base, out, seeds) if hasattr(t, "data_ptr")]
+            self._release_launched()
+        _check(rc)
+        return int(tk.value)
 
     def pending(self) -> int:
         return int(self._L.aws_crt_amd_queue_pending(self._h))
 
+    def first_pending(self) -> int:
+        return int(self._L.aws_crt_amd_queue_first_pending(self._h))
+
+    def status(self, ticket: int) -> int:
+        return int(self._L.aws_crt_amd_queue_status(self._h, ticket))
+
+    def wait(self, ticket: int) -> int:
+        """0 once the ticket's batch is complete, or the (negative) status of the launch that dropped it"""
+        rc = int(self._L.aws_crt_amd_queue_wait(self._h, ticket))
+        with self._lock:
+            self._release_launched()
+        return rc
+
     def flush(self) -> None:
-        _check(self._L.aws_crt_amd_queue_flush(self._h))
-        self._launched()
+        with self._lock:
+            rc = self._L.aws_crt_amd_queue_flush(self._h)
+            self._release_launched()
+        _check(rc)
 
     def close(self) -> None:
-        if self._h:
+        with self._lock:
+            if not self._h:
+                return
             rc = self._L.aws_crt_amd_queue_destroy(self._h)
             self._h = None
-            self._launched()
-            _check(rc)
+            self._release_launched()
+        _check(rc)
+
+
+class _IngestOptions(ctypes.Structure):
+    _fields_ = [("ndevices", ctypes.c_int), ("host_threads", ctypes.c_int), ("device_bytes", ctypes.POINTER(ctypes.c_uint64))]
 
 
 class HostJob:
-    """A prepared host-ingest job (aws_crt_amd_host_submit / aws_crt_amd_job_wait) over host buffers
+    """A prepared host-ingest job (aws_crt_amd_host_submit_ex / aws_crt_amd_job_wait) over host buffers
     given by raw addresses: the argument arrays are built once; `run()` submits and waits (the C
-    calls only); `results()` reads them back (XXH3_128: 128-bit ints)."""
+    calls only); `results()` reads them back (XXH3_128: 128-bit ints).  host_threads: -1 = hybrid
+    (the CPU share beside the device lanes, the default), 0 = devices only, n = n host threads.
+    `device_bytes` after run(): the bytes the devices checksummed."""
 
-    def __init__(self, alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):
+    def __init__(self, alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0,
+                 host_threads: int = -1):
         L = lib()
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
-        L.aws_crt_amd_host_submit.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp,
-                                              ctypes.c_int, ctypes.POINTER(vp)]
+        L.aws_crt_amd_host_submit_ex.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz, vp, vp,
+                                                 ctypes.POINTER(_IngestOptions), ctypes.POINTER(vp)]
         L.aws_crt_amd_job_wait.argtypes = [vp]
         L.aws_crt_amd_job_last_error.restype = ctypes.c_char_p
-        self.L, self.alg, self.n, self.ndevices = L, alg, len(ptrs), ndevices
+        self.L, self.alg, self.n = L, alg, len(ptrs)
         n = self.n
         self.P = (vp * max(n, 1))(*ptrs)
         self.S = (sz * max(n, 1))(*lens)
         T = ctypes.c_uint64 if alg in WIDE else ctypes.c_uint32
         self.out = (T * max(n * (2 if alg == XXH3_128 else 1), 1))()
         self.sd = (T * max(n, 1))(*seeds) if seeds is not None else None
+        self._dev_bytes = ctypes.c_uint64(0)
+        self.opt = _IngestOptions(ndevices, host_threads, ctypes.pointer(self._dev_bytes))
 
     def run(self) -> None:
         vp = ctypes.c_void_p
         job = vp()
-        rc = self.L.aws_crt_amd_host_submit(self.alg, self.P, self.S, self.n,
-                                            ctypes.cast(self.sd, vp) if self.sd is not None else None,
-                                            ctypes.cast(self.out, vp), self.ndevices, ctypes.byref(job))
+        rc = self.L.aws_crt_amd_host_submit_ex(self.alg, self.P, self.S, self.n,
+                                               ctypes.cast(self.sd, vp) if self.sd is not None else None,
+                                               ctypes.cast(self.out, vp), ctypes.byref(self.opt), ctypes.byref(job))
         if rc == 0:
             rc = self.L.aws_crt_amd_job_wait(job)
         if rc != 0:
             raise EngineError(f"host job failed ({rc}): {self.L.aws_crt_amd_job_last_error().decode()}")
+
+    @property
+    def device_bytes(self) -> int:
+        return int(self._dev_bytes.value)
 
     def results(self) -> list:
         out, n = self.out, self.n
@@ -324,10 +424,10 @@ class HostJob:
         return list(out[:n]) if n else []
 
 
-def host_job(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0):
-    """aws_crt_amd_host_submit + aws_crt_amd_job_wait over host buffers given by raw addresses; returns
-    the results (XXH3_128: 128-bit ints).  Synchronous from Python's point of view."""
-    job = HostJob(alg, ptrs, lens, seeds, ndevices)
+def host_job(alg: int, ptrs: Sequence[int], lens: Sequence[int], seeds=None, ndevices: int = 0, host_threads: int = -1):
+    """aws_crt_amd_host_submit_ex + aws_crt_amd_job_wait over host buffers given by raw addresses;
+    returns the results (XXH3_128: 128-bit ints).  Synchronous from Python's point of view."""
+    job = HostJob(alg, ptrs, lens, seeds, ndevices, host_threads)
     job.run()
     return job.results()
 

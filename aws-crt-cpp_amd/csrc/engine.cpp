@@ -13,9 +13,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -30,6 +33,7 @@
 #include "cpu/cpu_checksums.h"
 #include "engine.h"
 #include "gf2.h"
+#include "stream_states.h"
 
 #define AWS_CRT_AMD_BUILD 1
 #include <aws_crt_amd/checksums_batch.h>
@@ -41,6 +45,20 @@ namespace {
 thread_local std::string g_last_error;
 // measurement hook (aws_crt_amd_debug_time_next_launch): events stamped by the next scan dispatch
 thread_local void *g_time_events[2] = {nullptr, nullptr};
+
+// Prepared launches (aws_crt_amd_plan_*): while a plan is being built, the strided scan planner
+// records each launch it would make instead of making it.  A launch that needs the per-stream
+// cross-tile workspace records its size; the workspace is looked up on the stream at launch time.
+struct PlannedLaunch {
+    int alg = 0;
+    int kind = 0;  // 0: amdcrc_launch_scan(ScanParams), 1: amdcrc_launch_lanes(LaneParams)
+    amdcrc::ScanParams p{};
+    amdcrc::LaneParams lp{};
+    uint64_t blocks = 0;
+    bool ws = false;  // patch d_acc / d_cnt (/ acc1, cnt1, claim) from the stream's workspace
+    uint64_t ws_nbuf = 0, ws_tiles = 0;
+};
+thread_local std::vector<PlannedLaunch> *t_plan = nullptr;
 
 int fail(int code, const std::string &msg) {
     g_last_error = msg;
@@ -86,9 +104,42 @@ struct Stage {
     int next = 0, cur = 0;
 };
 
+// Everything the engine keeps per caller stream (stream_states.h): scratch that launches on one stream
+// share in stream order, and the fence recorded after the last launch that read it.
+struct StreamState {
+    Workspace ws;
+    Stage st;
+    DevBuf xsums;   // split XXH3 long path: per-block accumulator sums
+    DevBuf mp_out;  // multipart part results
+    // held by a multipart call on the stream from its list launch until its results are on the host:
+    // two calls on one stream would otherwise queue launch A, launch B, then A's copy of B's results
+    std::mutex mp_mu;
+    hipEvent_t fence = nullptr;  // recorded after the last launch that read this state
+    bool fenced = false;
+    bool pinned = false;         // read by a launch captured into a graph: never handed to another stream
+    uint64_t tick = 0;
+};
+struct StatePolicy {
+    static bool idle(StreamState &s) {
+        if (s.pinned) return false;
+        if (!s.mp_mu.try_lock()) return false;
+        s.mp_mu.unlock();
+        if (!s.fenced) return true;
+        const hipError_t e = hipEventQuery(s.fence);
+        if (e == hipSuccess) {
+            s.fenced = false;
+            return true;
+        }
+        (void)hipGetLastError();
+        return false;
+    }
+};
+constexpr size_t kMaxStreamStates = 64;
+
 struct Device {
     int id = -1;
     int cus = 0;
+    uint64_t max_pitch = 0;  // hipDeviceProp_t::memPitch: the largest pitch a 2D copy accepts
     std::mutex mu;
     std::map<int, DevBuf> braid;                       // alg -> W=32 braided-scan constants
     std::map<int, DevBuf> braid64;                     // alg -> W=64 braided-scan constants
@@ -96,13 +147,7 @@ struct Device {
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
     std::map<std::pair<int, uint64_t>, DevBuf> xcd;    // (alg, waves per XCD) -> crc64_xcd_kernel constants
     std::vector<DevBuf> retired;                       // outgrown buffers queued kernels may still read
-    std::map<hipStream_t, Workspace> ws;
-    std::map<hipStream_t, DevBuf> xsums;  // split XXH3 long path: per-block accumulator sums
-    std::map<hipStream_t, Stage> stage;
-    std::map<hipStream_t, DevBuf> mp_out;  // multipart part results
-    // held by a multipart call on that stream from its list launch until its results are on the host:
-    // two calls on one stream would otherwise queue launch A, launch B, then A's copy of B's results
-    std::map<hipStream_t, std::unique_ptr<std::mutex>> mp_mu;
+    StreamStates<hipStream_t, StreamState, StatePolicy> states{kMaxStreamStates};  // under mu
     // single path (GPU-dispatched host buffers, device buffers through the aws-checksums ABI)
     hipStream_t own_stream = nullptr;
     void *pin[2] = {nullptr, nullptr};
@@ -146,6 +191,7 @@ int get_device(Device **out) {
         auto d = std::make_unique<Device>();
         d->id = id;
         d->cus = prop.multiProcessorCount;
+        d->max_pitch = prop.memPitch ? (uint64_t)prop.memPitch : (1ull << 31) - 1;
         slot = std::move(d);
     }
     *out = slot.get();
@@ -163,6 +209,27 @@ bool capturing(hipStream_t s) {
         return false;
     }
     return st != hipStreamCaptureStatusNone;
+}
+
+// The per-stream state the launch about to be made reads (set by get_workspace / stage_begin / the
+// XXH3 sums, under the device mutex); fence_after records the state's fence behind that launch.
+thread_local StreamState *t_used = nullptr;
+
+void fence_after(hipStream_t s) {
+    StreamState *u = t_used;
+    t_used = nullptr;
+    if (!u) return;
+    if (capturing(s)) {
+        u->pinned = true;  // a graph may replay it at any time
+        return;
+    }
+    if ((!u->fence && hipEventCreateWithFlags(&u->fence, hipEventDisableTiming) != hipSuccess) ||
+        hipEventRecord(u->fence, s) != hipSuccess) {
+        (void)hipGetLastError();
+        u->pinned = true;  // unknown completion: never handed over
+        return;
+    }
+    u->fenced = true;
 }
 
 int upload_new(DevBuf &b, const void *host, size_t bytes) {
@@ -366,7 +433,9 @@ int alloc_zero(T **p, size_t n, hipStream_t s) {
 }
 
 int get_workspace(Device *d, hipStream_t s, size_t nbuf, size_t ntiles, Workspace **out) {
-    Workspace &w = d->ws[s];
+    StreamState *ss = d->states.get(s);
+    t_used = ss;
+    Workspace &w = ss->ws;
     const bool grow = w.cap_tiles < ntiles || !w.claim || w.cap < nbuf;
     if (grow && capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "engine workspace must be warmed up before stream capture");
     int rc;
@@ -516,16 +585,20 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     p.d_acc1 = nullptr;
     p.d_cnt1 = nullptr;
     p.d_claim = nullptr;
+    bool ws = false;
     if (tmax > 1 || p.nstatic) {
         if ((rc = get_pcols(d, alg, tile, tmax, s, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
-        Workspace *w;
-        if ((rc = get_workspace(d, s, nbuf, p.ntiles, &w))) return rc;
-        p.d_acc = w->acc;
-        p.d_cnt = w->cnt;
-        p.d_acc1 = w->acc1;
-        p.d_cnt1 = w->cnt1;
-        p.d_claim = w->claim;
+        ws = true;
+        if (!t_plan) {
+            Workspace *w;
+            if ((rc = get_workspace(d, s, nbuf, p.ntiles, &w))) return rc;
+            p.d_acc = w->acc;
+            p.d_cnt = w->cnt;
+            p.d_acc1 = w->acc1;
+            p.d_cnt1 = w->cnt1;
+            p.d_claim = w->claim;
+        }
     }
     const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
     uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
@@ -534,9 +607,16 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     if (blocks == 0) return 0;
     // crc64_list_stream_kernel: the head-entry and part-shift columns
     if (p.list_mode && p.stream == 4 && width_of(alg) == 64 && (rc = get_xcd_consts(d, alg, 512, &p.d_pcols))) return rc;
+    if (t_plan) {
+        PlannedLaunch pl;
+        pl.alg = alg, pl.p = p, pl.blocks = blocks, pl.ws = ws, pl.ws_nbuf = nbuf, pl.ws_tiles = p.ntiles;
+        t_plan->push_back(pl);
+        return 0;
+    }
     int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
     g_time_events[0] = g_time_events[1] = nullptr;
     if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString((hipError_t)e));
+    fence_after(s);
     return 0;
 }
 
@@ -705,8 +785,12 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         const Batch b{base, d_seeds, d_out};
         return scan_batches(d, alg, &b, 1, stride, len, count, seed_all, s);
     }
-    if (alg == AWS_CRT_AMD_XXH64 && count <= kX64HostMaxBuffers && len >= kX64HostMinBytes && !capturing(s))
-        return xxh64_host_route(d->id, base, stride, len, count, d_seeds, seed_all, d_out, s);
+    // the route copies rows with hipMemcpy2DAsync (source pitch = stride): overlapping or repeated
+    // buffers (stride < len, e.g. stride 0 = one buffer under several seeds) and pitches past the
+    // device's 2D-copy limit stay on the kernels
+    if (alg == AWS_CRT_AMD_XXH64 && count <= kX64HostMaxBuffers && len >= kX64HostMinBytes && (count == 1 || stride >= len) &&
+        (count == 1 || stride <= d->max_pitch) && !capturing(s))
+        return xxh64_host_route(d->id, base, count == 1 ? len : stride, len, count, d_seeds, seed_all, d_out, s);
     {
         XxhParams xp{};
         xp.base = base;
@@ -720,8 +804,12 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
         // scrambles the 64-byte sums (xxh3_kernels.hip)
         const uint64_t nb = len > 240 ? (len - 1) / 1024 : 0;
         if (alg != AWS_CRT_AMD_XXH64 && nb >= kXxh3SplitBlocks) {
+            // the sums are the stream's state: held from their sizing until the fence behind the
+            // scramble pass that reads them
             std::lock_guard<std::mutex> g(d->mu);
-            DevBuf &xs = d->xsums[s];
+            StreamState *ss = d->states.get(s);
+            t_used = ss;
+            DevBuf &xs = ss->xsums;
             const size_t need = count * nb * 64;
             if (xs.bytes < need) {
                 if (capturing(s)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "engine workspace must be warmed up before stream capture");
@@ -733,7 +821,14 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
             xp.d_sums = (uint64_t *)xs.p;
             int e = amdcrc_launch_xxh3_blocksum(&xp, s, g_time_events[0]);
             g_time_events[0] = nullptr;
-            if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh3 block-sum launch: ") + hipGetErrorString((hipError_t)e));
+            if (e) {
+                t_used = nullptr;
+                return fail(AWS_CRT_AMD_ERR_HIP, std::string("xxh3 block-sum launch: ") + hipGetErrorString((hipError_t)e));
+            }
+            const int rc = launch_hash(alg, xp, s);
+            if (rc) t_used = nullptr;
+            fence_after(s);
+            return rc;
         }
         return launch_hash(alg, xp, s);
     }
@@ -747,6 +842,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
         return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
     if (nb == 0 || nb > (size_t)kMaxBatches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad batch count");
     std::lock_guard<std::mutex> g(d->mu);
+    t_used = nullptr;
     const uint64_t base = bs[0].base;
     const uint64_t ml = main_len(base, len);
     ScanParams p{};
@@ -768,6 +864,12 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
         lp.len = len;
         lp.bcount = p.bcount;
         for (size_t j = 0; j < nb; ++j) lp.bbase[j] = p.bbase[j], lp.bout[j] = p.bout[j], lp.bseed[j] = p.bseed[j];
+        if (t_plan) {
+            PlannedLaunch pl;
+            pl.alg = alg, pl.kind = 1, pl.lp = lp;
+            t_plan->push_back(pl);
+            return 0;
+        }
         int e = amdcrc_launch_lanes(alg, &lp, s, g_time_events);
         g_time_events[0] = g_time_events[1] = nullptr;
         return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
@@ -824,14 +926,21 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
             p.ntiles = p.tiles_per_buf * count;
             int rc = get_braid64_consts(d, alg, &p.d_kvals);
             if (!rc) rc = get_xcd_consts(d, alg, nwx, &p.d_pcols);
-            Workspace *w;
-            if (!rc) rc = get_workspace(d, s, count, 1, &w);
             if (rc) return rc;
+            if (t_plan) {
+                PlannedLaunch pl;
+                pl.alg = alg, pl.p = p, pl.blocks = blocks, pl.ws = true, pl.ws_nbuf = count, pl.ws_tiles = 1;
+                t_plan->push_back(pl);
+                return 0;
+            }
+            Workspace *w;
+            if ((rc = get_workspace(d, s, count, 1, &w))) return rc;
             p.d_acc = w->acc;
             p.d_cnt = w->cnt;
             int e = amdcrc_launch_scan(alg, &p, (int)blocks, s, g_time_events);
             g_time_events[0] = g_time_events[1] = nullptr;
             if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString((hipError_t)e));
+            fence_after(s);
             return 0;
         }
     }
@@ -849,7 +958,9 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
 // Descriptor staging: returns pinned host memory to fill (slot `cur`); stage_end queues its upload
 // on the stream and returns the device copy.  The slot reused is the one three calls old.
 int stage_begin(Device *d, hipStream_t s, size_t bytes, void **host) {
-    Stage &st = d->stage[s];
+    StreamState *ss = d->states.get(s);
+    t_used = ss;
+    Stage &st = ss->st;
     const int k = st.next;
     st.cur = k;
     st.next = (k + 1) % kStageSlots;
@@ -874,7 +985,7 @@ int stage_begin(Device *d, hipStream_t s, size_t bytes, void **host) {
 }
 
 int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
-    Stage &st = d->stage[s];
+    Stage &st = d->states.get(s)->st;
     const int k = st.cur;
     HIP_TRY(hipMemcpyAsync(st.dev[k].p, st.host[k].p, bytes, hipMemcpyHostToDevice, s));
     HIP_TRY(hipEventRecord(st.done[k], s));
@@ -945,6 +1056,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     if (count == 0) return 0;
     if (!ptrs || !lens || !d_out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null argument");
     std::lock_guard<std::mutex> g(d->mu);
+    t_used = nullptr;
     // plan: seg from the median main length, tiles per buffer, per-wave starting buffer
     std::vector<uint64_t> mains(count);
     uint64_t total = 0, maxlen = 0;
@@ -970,7 +1082,9 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         lp.d_ptrs = dl, lp.d_lens = dl + count, lp.nbuf = count, lp.d_seeds = d_seeds, lp.d_out = d_out;
         int e = amdcrc_launch_lanes(alg, &lp, s, g_time_events);
         g_time_events[0] = g_time_events[1] = nullptr;
-        return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
+        if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("lane kernel launch: ") + hipGetErrorString((hipError_t)e));
+        fence_after(s);
+        return 0;
     }
     uint32_t seg = kGroupBytes;
     uint64_t tile = 0;
@@ -1028,7 +1142,9 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         xp.nbuf = count;
         xp.d_seeds = (const uint64_t *)d_seeds;
         xp.d_out = (uint64_t *)d_out;
-        return launch_hash(alg, xp, s);
+        const int rc = launch_hash(alg, xp, s);
+        if (!rc) fence_after(s);
+        return rc;
     }
     ScanParams p{};
     p.seg = seg;
@@ -1076,6 +1192,7 @@ bool is_device_ptr(const void *p) {
 }
 
 constexpr size_t kStageChunk = 16u << 20;
+constexpr size_t kHashStageMax = 256u << 20;  // cached device copy of a GPU-dispatched host hash
 
 // One buffer (host or device memory) on the GPU, synchronous.  Host data streams through two pinned
 // slots; chunk i+1 is seeded on the device with chunk i's result, so no host round trip sits
@@ -1099,16 +1216,25 @@ int single_impl(int alg, const void *input, size_t len, uint64_t seed, uint64_t 
         // that is freed once the call has synchronised, so a large hash never stays pinned in HBM.
         const void *dp = input;
         void *temp = nullptr;
-        if (len && !is_device_ptr(input)) {
-            if (len > kStageChunk) {
+        const bool host_in = len && !is_device_ptr(input);
+        // a long XXH64 buffer takes the host route on the device too (strided_impl): one that is
+        // already in host memory is hashed where it is, without crossing PCIe twice
+        if (host_in && alg == AWS_CRT_AMD_XXH64 && len >= kX64HostMinBytes) {
+            result[0] = cpu::xxh64((const uint8_t *)input, len, seed);
+            return 0;
+        }
+        if (host_in) {
+            if (len > kHashStageMax) {
                 HIP_TRY(hipMalloc(&temp, len));
                 dp = temp;
             } else {
                 if (d->hash_stage.bytes < len) {
+                    // geometric growth up to kHashStageMax: repeated large hashes reuse one buffer
+                    const size_t cap = std::min(kHashStageMax, std::max(std::max(len, kStageChunk), d->hash_stage.bytes * 2));
                     if (d->hash_stage.p) (void)hipFree(d->hash_stage.p);  // own stream synchronised after every call
                     d->hash_stage = DevBuf{};
-                    HIP_TRY(hipMalloc(&d->hash_stage.p, kStageChunk));
-                    d->hash_stage.bytes = kStageChunk;
+                    HIP_TRY(hipMalloc(&d->hash_stage.p, cap));
+                    d->hash_stage.bytes = cap;
                 }
                 dp = d->hash_stage.p;
             }
@@ -1273,6 +1399,34 @@ AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t by
     });
 }
 
+// Per-stream state (stream_states.h): hand a stream's state back (before destroying the stream, or
+// when it will not be used with the engine for a while); at most kMaxStreamStates streams per device
+// hold state otherwise, the least recently used idle one handing its state to a new stream.
+AWS_CRT_AMD_API int aws_crt_amd_stream_release(void *hip_stream) {
+    return guarded(err_sink, [&]() -> int {
+        std::lock_guard<std::mutex> g(g_mu);
+        for (auto &kv : g_devices) {
+            Device *d = kv.second.get();
+            std::lock_guard<std::mutex> gd(d->mu);
+            d->states.release((hipStream_t)hip_stream);
+        }
+        return 0;
+    });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_stream_states(size_t *live, size_t *spare, size_t *created) {
+    return guarded(err_sink, [&]() -> int {
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> g(d->mu);
+        if (live) *live = d->states.live();
+        if (spare) *spare = d->states.spares();
+        if (created) *created = d->states.created();
+        return 0;
+    });
+}
+
 AWS_CRT_AMD_API int aws_crt_amd_checksum_strided(int alg, const void *d_base, size_t stride, size_t len, size_t count,
                                                  const void *d_seeds, void *d_out, void *hip_stream) {
     return guarded(err_sink, [&]() -> int {
@@ -1319,50 +1473,263 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(int alg, const struct aws_crt_a
     });
 }
 
-// Submission queue (checksums_batch.h): pushes collect batches of one shape; a full queue (kMaxBatches)
-// or a flush hands them to aws_crt_amd_checksum_batches, one launch per run of batches.
+// Prepared submissions (checksums_batch.h aws_crt_amd_plan_*): the planning of
+// aws_crt_amd_checksum_batches (runs of batches, kernel, tile size, geometry, constants) done once;
+// a launch of the plan only looks up the stream's workspace where a kernel needs one and launches.
+struct aws_crt_amd_plan {
+    Device *dev = nullptr;
+    int alg = 0;
+    std::vector<PlannedLaunch> launches;
+    // hashes: the batch call itself, made at launch (their launches depend on the stream)
+    std::vector<aws_crt_amd_batch> batches;
+    size_t stride = 0, len = 0, count = 0;
+};
+
+AWS_CRT_AMD_API int aws_crt_amd_plan_create(int alg, const struct aws_crt_amd_batch *batches, size_t nbatches, size_t stride,
+                                            size_t len, size_t count, aws_crt_amd_plan **out) {
+    return guarded(err_sink, [&]() -> int {
+        if (!out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null plan pointer");
+        *out = nullptr;
+        if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
+        if (nbatches && !batches) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null batches");
+        Device *d;
+        int rc = get_device(&d);
+        if (rc) return rc;
+        if (count == 1) stride = len;
+        for (size_t j = 0; j < nbatches; ++j)
+            if (!batches[j].d_out || (len && !batches[j].d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
+        if (count > 1 && (stride % 16) != 0 && !is_hash(alg))
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
+        std::unique_ptr<aws_crt_amd_plan> pl(new aws_crt_amd_plan);
+        pl->dev = d, pl->alg = alg, pl->stride = stride, pl->len = len, pl->count = count;
+        if (is_hash(alg) || count == 0) {
+            pl->batches.assign(batches, batches + nbatches);
+        } else {
+            struct Rec {
+                explicit Rec(std::vector<PlannedLaunch> *v) { t_plan = v; }
+                ~Rec() { t_plan = nullptr; }
+            } rec(&pl->launches);
+            std::vector<Batch> run;
+            for (size_t j = 0; j <= nbatches && !rc; ++j) {
+                const bool flush = j == nbatches || run.size() == (size_t)kMaxBatches ||
+                                   (!run.empty() && ((uint64_t)(uintptr_t)batches[j].d_base & 15) != (run[0].base & 15));
+                if (flush && !run.empty()) {
+                    rc = scan_batches(d, alg, run.data(), run.size(), stride, len, count, 0, nullptr);
+                    run.clear();
+                }
+                if (j < nbatches) run.push_back({(uint64_t)(uintptr_t)batches[j].d_base, batches[j].d_seeds, batches[j].d_out});
+            }
+            if (rc) return rc;
+        }
+        *out = pl.release();
+        return 0;
+    });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_plan_launch(aws_crt_amd_plan *pl, void *hip_stream) {
+    return guarded(err_sink, [&]() -> int {
+        if (!pl) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null plan");
+        hipStream_t s = (hipStream_t)hip_stream;
+        if (!pl->batches.empty())
+            return aws_crt_amd_checksum_batches(pl->alg, pl->batches.data(), pl->batches.size(), pl->stride, pl->len, pl->count,
+                                                hip_stream);
+        for (const PlannedLaunch &L : pl->launches) {
+            int e;
+            if (L.kind == 1) {
+                e = amdcrc_launch_lanes(L.alg, &L.lp, s, g_time_events);
+            } else if (L.ws) {
+                ScanParams p = L.p;
+                std::lock_guard<std::mutex> g(pl->dev->mu);
+                t_used = nullptr;
+                Workspace *w;
+                const int rc = get_workspace(pl->dev, s, L.ws_nbuf, L.ws_tiles, &w);
+                if (rc) {
+                    t_used = nullptr;
+                    return rc;
+                }
+                p.d_acc = w->acc, p.d_cnt = w->cnt, p.d_acc1 = w->acc1, p.d_cnt1 = w->cnt1, p.d_claim = w->claim;
+                e = amdcrc_launch_scan(L.alg, &p, (int)L.blocks, s, g_time_events);
+                if (!e) fence_after(s);
+                t_used = nullptr;
+            } else {
+                e = amdcrc_launch_scan(L.alg, &L.p, (int)L.blocks, s, g_time_events);
+            }
+            g_time_events[0] = g_time_events[1] = nullptr;
+            if (e) return fail(AWS_CRT_AMD_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString((hipError_t)e));
+        }
+        return 0;
+    });
+}
+
+AWS_CRT_AMD_API size_t aws_crt_amd_plan_launches(const aws_crt_amd_plan *pl) {
+    return pl ? (pl->batches.empty() ? pl->launches.size() : pl->batches.size()) : 0;
+}
+
+AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(aws_crt_amd_plan *pl) { delete pl; }
+
+// Submission queue (checksums_batch.h): pushes collect batches of one shape; a full queue
+// (max_batches, at most kMaxBatches), an age bound (a flusher thread), a flush or a wait hand them to
+// aws_crt_amd_checksum_batches, one launch per run of batches.  Every push gets a ticket; each launch
+// records an event after it on the queue's stream, so a ticket's completion (or the error of the
+// launch that dropped it) can be asked for and waited on.
 struct aws_crt_amd_queue {
-    int alg;
-    size_t stride, len, count;
-    void *stream;
+    int alg = 0;
+    int device = 0;
+    size_t stride = 0, len = 0, count = 0;
+    void *stream = nullptr;
+    size_t max_batches = kMaxBatches;
+    uint64_t max_age_us = 0;
     std::mutex mu;
+    std::condition_variable cv;
     std::vector<aws_crt_amd_batch> pending;
+    uint64_t next_ticket = 1;                                  // ticket of the next push
+    std::chrono::steady_clock::time_point oldest;              // push time of pending[0]
+    struct Launch {
+        uint64_t first, end;  // tickets [first, end)
+        hipEvent_t ev;        // recorded after the launch (nullptr when it was refused)
+        int rc;
+    };
+    std::deque<Launch> launches;                               // recent launches, oldest first
+    std::vector<Launch> failed;                                // pruned refused launches (bounded)
+    std::vector<hipEvent_t> spare;                             // events of completed, pruned launches
+    std::thread flusher;
+    bool stop = false;
 };
 
 namespace {
+constexpr size_t kQueueKeepLaunches = 64;
+constexpr size_t kQueueKeepFailures = 1024;
+
+void queue_prune_locked(aws_crt_amd_queue *q) {
+    while (q->launches.size() > kQueueKeepLaunches) {
+        aws_crt_amd_queue::Launch &L = q->launches.front();
+        if (L.rc) {
+            if (q->failed.size() >= kQueueKeepFailures) q->failed.erase(q->failed.begin());
+            q->failed.push_back(L);
+        } else if (hipEventQuery(L.ev) != hipSuccess) {
+            (void)hipGetLastError();
+            return;  // still running: keep it (and every later one)
+        } else {
+            q->spare.push_back(L.ev);
+        }
+        q->launches.pop_front();
+    }
+}
+
 int queue_flush_locked(aws_crt_amd_queue *q) {
     if (q->pending.empty()) return 0;
-    const int rc = aws_crt_amd_checksum_batches(q->alg, q->pending.data(), q->pending.size(), q->stride, q->len, q->count,
-                                                q->stream);
-    q->pending.clear();  // launched, or refused with its error recorded: not retried
+    const uint64_t first = q->next_ticket - q->pending.size();
+    int rc = aws_crt_amd_checksum_batches(q->alg, q->pending.data(), q->pending.size(), q->stride, q->len, q->count,
+                                          q->stream);
+    hipEvent_t ev = nullptr;
+    if (!rc) {
+        if (!q->spare.empty()) {
+            ev = q->spare.back();
+            q->spare.pop_back();
+        } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            ev = nullptr;
+        }
+        if (!ev || hipEventRecord(ev, (hipStream_t)q->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            if (ev) q->spare.push_back(ev);
+            ev = nullptr;
+            rc = fail(AWS_CRT_AMD_ERR_HIP, "queue: completion event");
+        }
+    }
+    // launched (with its completion event), or refused: its tickets carry the error; not retried
+    q->launches.push_back({first, q->next_ticket, ev, rc});
+    q->pending.clear();
+    queue_prune_locked(q);
     return rc;
+}
+
+// The age bound: launch what is queued once the oldest push is max_age_us old
+void queue_flusher(aws_crt_amd_queue *q) noexcept {
+    (void)hipSetDevice(q->device);
+    std::unique_lock<std::mutex> g(q->mu);
+    while (!q->stop) {
+        if (q->pending.empty()) {
+            q->cv.wait(g);
+            continue;
+        }
+        const auto due = q->oldest + std::chrono::microseconds(q->max_age_us);
+        if (std::chrono::steady_clock::now() >= due) {
+            (void)guarded(err_sink, [&]() -> int { return queue_flush_locked(q); });
+        } else {
+            q->cv.wait_until(g, due);
+        }
+    }
+}
+
+int queue_status_locked(aws_crt_amd_queue *q, uint64_t ticket, hipEvent_t *ev) {
+    *ev = nullptr;
+    if (ticket == 0 || ticket >= q->next_ticket) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: no such ticket");
+    if (ticket >= q->next_ticket - q->pending.size()) return AWS_CRT_AMD_TICKET_QUEUED;
+    for (auto it = q->launches.rbegin(); it != q->launches.rend(); ++it) {
+        if (ticket < it->first || ticket >= it->end) continue;
+        if (it->rc) return it->rc;
+        const hipError_t e = hipEventQuery(it->ev);
+        if (e == hipSuccess) return 0;
+        (void)hipGetLastError();
+        *ev = it->ev;
+        return e == hipErrorNotReady ? AWS_CRT_AMD_TICKET_LAUNCHED : AWS_CRT_AMD_ERR_HIP;
+    }
+    for (const auto &L : q->failed)
+        if (ticket >= L.first && ticket < L.end) return L.rc;
+    return 0;  // pruned: completed
 }
 }  // namespace
 
-AWS_CRT_AMD_API int aws_crt_amd_queue_create(int alg, size_t stride, size_t len, size_t count, void *hip_stream,
-                                             aws_crt_amd_queue **out) {
+AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(int alg, size_t stride, size_t len, size_t count, void *hip_stream,
+                                                const struct aws_crt_amd_queue_options *opt, aws_crt_amd_queue **out) {
     return guarded(err_sink, [&]() -> int {
         if (!out) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue pointer");
         *out = nullptr;
         if (alg < 0 || alg > 5) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "bad algorithm");
         if (count > 1 && stride % 16 != 0 && !is_hash(alg))
             return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
+        if (opt && opt->max_batches > (size_t)kMaxBatches)
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: max_batches above 32");
         std::unique_ptr<aws_crt_amd_queue> q(new aws_crt_amd_queue);
         q->alg = alg, q->stride = stride, q->len = len, q->count = count, q->stream = hip_stream;
+        if (opt && opt->max_batches) q->max_batches = opt->max_batches;
+        if (opt) q->max_age_us = opt->max_age_us;
+        if (hipGetDevice(&q->device) != hipSuccess) {
+            (void)hipGetLastError();
+            q->device = 0;
+        }
         q->pending.reserve(kMaxBatches);
+        if (q->max_age_us) q->flusher = std::thread(queue_flusher, q.get());
         *out = q.release();
         return 0;
     });
 }
 
-AWS_CRT_AMD_API int aws_crt_amd_queue_push(aws_crt_amd_queue *q, const void *d_base, const void *d_seeds, void *d_out) {
+AWS_CRT_AMD_API int aws_crt_amd_queue_create(int alg, size_t stride, size_t len, size_t count, void *hip_stream,
+                                             aws_crt_amd_queue **out) {
+    return aws_crt_amd_queue_create_ex(alg, stride, len, count, hip_stream, nullptr, out);
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_push_ex(aws_crt_amd_queue *q, const void *d_base, const void *d_seeds, void *d_out,
+                                              uint64_t *ticket) {
     return guarded(err_sink, [&]() -> int {
+        if (ticket) *ticket = 0;
         if (!q) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue");
         if (!d_out || (q->len && !d_base)) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null buffer");
         std::lock_guard<std::mutex> g(q->mu);
+        if (q->pending.empty()) {
+            q->oldest = std::chrono::steady_clock::now();
+            if (q->max_age_us) q->cv.notify_one();
+        }
         q->pending.push_back({d_base, d_seeds, d_out});
-        return q->pending.size() >= (size_t)kMaxBatches ? queue_flush_locked(q) : 0;
+        if (ticket) *ticket = q->next_ticket;
+        ++q->next_ticket;
+        return q->pending.size() >= q->max_batches ? queue_flush_locked(q) : 0;
     });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_push(aws_crt_amd_queue *q, const void *d_base, const void *d_seeds, void *d_out) {
+    return aws_crt_amd_queue_push_ex(q, d_base, d_seeds, d_out, nullptr);
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_queue_flush(aws_crt_amd_queue *q) {
@@ -1379,12 +1746,61 @@ AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const aws_crt_amd_queue *q) {
     return q->pending.size();
 }
 
+AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_first_pending(const aws_crt_amd_queue *q) {
+    if (!q) return 0;
+    std::lock_guard<std::mutex> g(const_cast<aws_crt_amd_queue *>(q)->mu);
+    return q->next_ticket - q->pending.size();
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_status(aws_crt_amd_queue *q, uint64_t ticket) {
+    return guarded(err_sink, [&]() -> int {
+        if (!q) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue");
+        std::lock_guard<std::mutex> g(q->mu);
+        hipEvent_t ev;
+        return queue_status_locked(q, ticket, &ev);
+    });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_queue_wait(aws_crt_amd_queue *q, uint64_t ticket) {
+    return guarded(err_sink, [&]() -> int {
+        if (!q) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "null queue");
+        hipEvent_t ev;
+        {
+            std::lock_guard<std::mutex> g(q->mu);
+            int st = queue_status_locked(q, ticket, &ev);
+            if (st == AWS_CRT_AMD_TICKET_QUEUED) {
+                const int rc = queue_flush_locked(q);
+                if (rc) return rc;
+                st = queue_status_locked(q, ticket, &ev);
+            }
+            if (st != AWS_CRT_AMD_TICKET_LAUNCHED) return st;
+        }
+        // the event is never destroyed while the queue lives (pruned events are kept as spares, and a
+        // spare is re-recorded only after its launch completed -- waiting on it then returns at once)
+        HIP_TRY(hipEventSynchronize(ev));
+        std::lock_guard<std::mutex> g(q->mu);
+        hipEvent_t ev2;
+        const int st = queue_status_locked(q, ticket, &ev2);
+        return st == AWS_CRT_AMD_TICKET_LAUNCHED ? 0 : st;
+    });
+}
+
 AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(aws_crt_amd_queue *q) {
     if (!q) return 0;
     int rc;
     {
         std::lock_guard<std::mutex> g(q->mu);
+        q->stop = true;
+        q->cv.notify_all();
+    }
+    if (q->flusher.joinable()) q->flusher.join();
+    {
+        std::lock_guard<std::mutex> g(q->mu);
         rc = guarded(err_sink, [&]() -> int { return queue_flush_locked(q); });
+        // the events may be destroyed while their launches run (HIP releases them after completion)
+        for (auto &L : q->launches)
+            if (L.ev) (void)hipEventDestroy(L.ev);
+        for (hipEvent_t e : q->spare) (void)hipEventDestroy(e);
     }
     delete q;
     return rc;
@@ -1457,6 +1873,7 @@ AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(int alg, const void *d_crc1, c
         if (rc) return rc;
         hipStream_t s = (hipStream_t)hip_stream;
         std::lock_guard<std::mutex> g(d->mu);
+        t_used = nullptr;
         // staging: [x^(8*2^i), i < 64][len2[count]]
         uint64_t *h;
         const size_t words = 64 + count;
@@ -1473,7 +1890,12 @@ AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(int alg, const void *d_crc1, c
         if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;
         CombineParams cp{d_crc1, d_crc2, dd + 64, count, d_out, dd};
         int e = amdcrc_launch_combine(alg, &cp, s);
-        return e ? fail(AWS_CRT_AMD_ERR_HIP, "combine launch failed") : 0;
+        if (e) {
+            t_used = nullptr;
+            return fail(AWS_CRT_AMD_ERR_HIP, "combine launch failed");
+        }
+        fence_after(s);
+        return 0;
     });
 }
 
@@ -1494,17 +1916,23 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
             const size_t osz = w / 8;
             hipStream_t s = (hipStream_t)hip_stream;
             void *d_out;
-            std::mutex *smu;
-            {
+            std::unique_lock<std::mutex> call;
+            for (;;) {
+                StreamState *ss;
+                {
+                    std::lock_guard<std::mutex> g(d->mu);
+                    ss = d->states.get(s);
+                }
+                // per stream, taken before d->mu (list_impl takes d->mu); a held state is never handed
+                // to another stream (StatePolicy::idle), so re-check that it is still this stream's
+                call = std::unique_lock<std::mutex>(ss->mp_mu);
                 std::lock_guard<std::mutex> g(d->mu);
-                auto &m = d->mp_mu[s];
-                if (!m) m.reset(new std::mutex);
-                smu = m.get();
+                if (d->states.get(s) == ss) break;
+                call.unlock();
             }
-            std::lock_guard<std::mutex> call(*smu);  // per stream, taken before d->mu (list_impl takes d->mu)
             {
                 std::lock_guard<std::mutex> g(d->mu);
-                DevBuf &ob = d->mp_out[s];
+                DevBuf &ob = d->states.get(s)->mp_out;
                 if (ob.bytes < count * osz) {
                     if (ob.p) d->retired.push_back(ob);
                     ob = DevBuf{};

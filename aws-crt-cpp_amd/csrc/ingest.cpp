@@ -10,11 +10,17 @@
 //     compute stream  scan slot k    (one ragged list launch over the pieces packed into the slot)
 //                     D2H piece results
 //
-// Buffers longer than a slot are cut into pieces; every piece is scanned from seed 0 (the caller's
+// Buffers longer than a piece are cut into pieces; every piece is scanned from seed 0 (the caller's
 // seed for a buffer's first piece) and the pieces of a buffer are folded on the host with Combine
 // (CRC.h:41-51), O(log n) scalar algebra per piece.  xxHash cannot be split that way and is a serial
-// chain per buffer, so a job's xxHash buffers run on the engine's host path (one std::thread per
-// device slot of the job) while the CRCs run on the GPUs.
+// chain per buffer, so a job's xxHash buffers run on the engine's host path.
+//
+// Hybrid jobs (round 4, the default): the data starts in host memory, where the host path checksums
+// it at 20-45 GiB/s per core while one device lane is bound by PCIe (~50 GiB/s).  So the CPU share's
+// threads and the device lanes both take pieces from one cursor over the job (work stealing by
+// claims of contiguous pieces): a device claims about its share of what is left (its PCIe rate
+// against the host threads'), a host thread a run of about 1 MiB.  Offloading is then never slower
+// than the host path alone, and the devices add their PCIe rate on top.
 //
 // Device-resident lists spanning several devices (aws_crt_amd_checksum_list_devices) are grouped by
 // the device that owns each buffer; one host thread per device stages and launches that device's
@@ -95,7 +101,13 @@ struct JobImpl {
     std::vector<uint64_t> seeds;  // per buffer (0 when none)
     void *h_out = nullptr;
     std::vector<Piece> pieces;
-    std::vector<uint64_t> piece_val;  // per piece (CRC jobs)
+    std::vector<uint64_t> piece_val;    // per piece (CRC jobs)
+    std::vector<uint64_t> piece_start;  // byte offset of each piece in the job (pieces.size() + 1)
+    std::atomic<size_t> cursor{0};      // the next unclaimed piece
+    int ndev = 0;                       // device lanes of the job
+    size_t hthreads = 0;                // host threads taking pieces beside them
+    std::atomic<uint64_t> dev_bytes{0};
+    uint64_t *dev_bytes_out = nullptr;  // options: bytes the devices scanned, set by job_wait
     std::vector<std::thread> workers;
     std::atomic<int> rc{0};
     std::string err;
@@ -177,18 +189,52 @@ void lane_free(Lane &L) {
     if (L.comp) (void)hipStreamDestroy(L.comp);
 }
 
-// Worker for one device: pieces `mine` (indices into job->pieces, in order) through the 3-slot ring
-void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine);
-void device_worker(JobImpl *job, int dev, std::vector<size_t> mine) noexcept {
+constexpr size_t kHybridPiece = 8u << 20;  // piece size of hybrid jobs (host threads claim whole pieces)
+constexpr uint64_t kMinDevClaim = 1u << 20;
+constexpr uint64_t kHostClaim = 1u << 20;
+
+// Claim the next run of pieces [*a, *b): at least one, at most max_pieces, at most `budget` bytes
+// past the first.  false when the job has no unclaimed piece left.
+bool claim(JobImpl *job, uint64_t budget, size_t max_pieces, size_t *a, size_t *b) {
+    const size_t n = job->pieces.size();
+    size_t cur = job->cursor.load(std::memory_order_relaxed);
+    for (;;) {
+        if (cur >= n) return false;
+        const uint64_t lim = job->piece_start[cur] + std::max<uint64_t>(budget, 1);
+        size_t e = (size_t)(std::upper_bound(job->piece_start.begin() + (long)cur + 1, job->piece_start.end(), lim) -
+                            job->piece_start.begin()) - 1;
+        e = std::min(std::max(e, cur + 1), std::min(n, cur + max_pieces));
+        if (job->cursor.compare_exchange_weak(cur, e, std::memory_order_relaxed)) {
+            *a = cur;
+            *b = e;
+            return true;
+        }
+    }
+}
+
+// A device lane's claim: about its share of the unclaimed bytes, at one lane's PCIe rate (~50 GiB/s)
+// against a host thread's CRC rate (~20 GiB/s and up): 5 : 2 per lane and thread.  Devices alone: a
+// whole slot.
+uint64_t dev_budget(const JobImpl *job) {
+    if (!job->hthreads) return kSlotBytes;
+    const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
+    const uint64_t rem = job->piece_start.back() - job->piece_start[c];
+    const uint64_t share = rem * 5 / (5 * (uint64_t)job->ndev + 2 * (uint64_t)job->hthreads);
+    return std::min<uint64_t>(kSlotBytes, std::max(kMinDevClaim, share));
+}
+
+// Worker for one device: claimed runs of pieces through the 3-slot ring
+void device_worker_body(JobImpl *job, int dev);
+void device_worker(JobImpl *job, int dev) noexcept {
     try {
-        device_worker_body(job, dev, mine);
+        device_worker_body(job, dev);
     } catch (const std::bad_alloc &) {
         job->set_error(AWS_CRT_AMD_ERR_OOM, "out of host memory");
     } catch (...) {
         job->set_error(AWS_CRT_AMD_ERR_HIP, "internal error in a device worker");
     }
 }
-void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine) {
+void device_worker_body(JobImpl *job, int dev) {
     Lane *lp = lane_take(dev);
     Lane &L = *lp;
     struct Guard {
@@ -225,24 +271,19 @@ void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine) 
         L.used[k] = false;
         return true;
     };
-    size_t next = 0;
     int k = 0;
-    while (next < mine.size() && job->rc.load() == 0) {
+    while (job->rc.load() == 0) {
         if (!harvest(k)) {
             job->set_error(AWS_CRT_AMD_ERR_HIP, "slot results");
             return;
         }
-        // pack pieces into slot k: contiguous in the slot, in order
+        // claim a run of pieces for slot k: contiguous in the slot, in order (pieces are at most a slot)
+        size_t a, b;
+        if (!claim(job, dev_budget(job), kMaxPiecesPerSlot, &a, &b)) break;
         std::vector<size_t> &ps = slot_pieces[k];
         ps.clear();
-        size_t fill = 0;
-        while (next < mine.size() && ps.size() < kMaxPiecesPerSlot) {
-            const Piece &pc = job->pieces[mine[next]];
-            if (fill + pc.len > kSlotBytes && !ps.empty()) break;
-            ps.push_back(mine[next]);
-            fill += pc.len;
-            ++next;
-        }
+        for (size_t q = a; q < b; ++q) ps.push_back(q);
+        job->dev_bytes.fetch_add(job->piece_start[b] - job->piece_start[a], std::memory_order_relaxed);
         // H2D: runs of host-contiguous pinned pieces go straight from the caller's memory; the rest
         // through the pinned mirror (memcpy by this thread, then one DMA per run)
         size_t off = 0;
@@ -313,6 +354,26 @@ void device_worker_body(JobImpl *job, int dev, const std::vector<size_t> &mine) 
     }
     for (int j = 0; j < kSlots; ++j)
         if (!harvest(j)) job->set_error(AWS_CRT_AMD_ERR_HIP, "slot results");
+}
+
+// A hybrid CRC job's host thread: claimed runs of pieces on the host path, into piece_val like a lane
+void crc_host_worker(JobImpl *job) noexcept {
+    size_t a, b;
+    while (job->rc.load() == 0) {
+        const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
+        const uint64_t rem = job->piece_start.back() - job->piece_start[c];
+        const uint64_t budget = std::min<uint64_t>(kHostClaim, std::max<uint64_t>(rem / (4 * (job->hthreads + (size_t)job->ndev)), 1));
+        if (!claim(job, budget, SIZE_MAX, &a, &b)) return;
+        for (size_t q = a; q < b; ++q) {
+            const Piece &pc = job->pieces[q];
+            const uint8_t *p = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
+            switch (job->alg) {
+                case AWS_CRT_AMD_CRC32: job->piece_val[q] = cpu::crc32(p, pc.len, (uint32_t)pc.seed); break;
+                case AWS_CRT_AMD_CRC32C: job->piece_val[q] = cpu::crc32c(p, pc.len, (uint32_t)pc.seed); break;
+                default: job->piece_val[q] = cpu::crc64nvme(p, pc.len, pc.seed); break;
+            }
+        }
+    }
 }
 
 // A job's buffers on the host path (xxHash, or no device): buffers round-robin over `threads`
@@ -427,8 +488,9 @@ AWS_CRT_AMD_API int aws_crt_amd_unregister_host(void *p) {
     return hipHostUnregister(p) == hipSuccess ? 0 : AWS_CRT_AMD_ERR_HIP;
 }
 
-AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
-                                            const void *h_seeds, void *h_out, int ndevices, struct aws_crt_amd_job **job_out) {
+AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
+                                               const void *h_seeds, void *h_out, const struct aws_crt_amd_ingest_options *opt,
+                                               struct aws_crt_amd_job **job_out) {
     return guarded(job_err_sink, [&]() -> int {
         if (!job_out) return AWS_CRT_AMD_ERR_INVALID_ARG;
         *job_out = nullptr;
@@ -436,6 +498,8 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, 
         if (count && (!h_ptrs || !lens || !h_out)) return AWS_CRT_AMD_ERR_INVALID_ARG;
         for (size_t i = 0; i < count; ++i)
             if (lens[i] && !h_ptrs[i]) return AWS_CRT_AMD_ERR_INVALID_ARG;
+        const int ndevices = opt ? opt->ndevices : 0;
+        const int want_host = opt ? opt->host_threads : -1;
         std::unique_ptr<aws_crt_amd_job> job(new (std::nothrow) aws_crt_amd_job);
         if (!job) return AWS_CRT_AMD_ERR_OOM;
         JobImpl &J = job->impl;
@@ -444,6 +508,8 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, 
         J.lens = lens;
         J.count = count;
         J.h_out = h_out;
+        J.dev_bytes_out = opt ? opt->device_bytes : nullptr;
+        if (J.dev_bytes_out) *J.dev_bytes_out = 0;
         const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
         J.seeds.assign(count, 0);
         for (size_t i = 0; h_seeds && i < count; ++i)
@@ -455,29 +521,48 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, 
             G = 0;
         }
         if (!is_crc(alg) || G <= 0) {
-            // xxHash (or no device): the host path, one thread per device the job would have used
-            const size_t threads = (size_t)std::max(1, std::min(G > 0 ? G : 1, 16));
+            // xxHash (or no usable device): the host path on the process's CPU share
+            const size_t threads = host_threads(count);
             for (size_t t = 0; t < threads; ++t) J.spawn(host_worker, &J, t, threads);
             *job_out = job.release();
             return 0;
         }
-        // pieces, buffer by buffer; buffer i goes to device i % G
-        std::vector<std::vector<size_t>> per_dev((size_t)G);
+        // host threads beside the lanes: the CPU share less one thread per lane (auto), or as asked
+        uint64_t total = 0;
+        for (size_t i = 0; i < count; ++i) total += lens[i];
+        const size_t share = host_threads(SIZE_MAX);
+        size_t H = want_host < 0 ? (share > (size_t)G ? share - (size_t)G : 0) : (size_t)want_host;
+        const size_t piece = H ? kHybridPiece : kSlotBytes;
+        // pieces, buffer by buffer, in job order
         for (size_t i = 0; i < count; ++i) {
             size_t off = 0;
             do {
-                const size_t n = std::min(kSlotBytes, lens[i] - off);
-                per_dev[i % (size_t)G].push_back(J.pieces.size());
+                const size_t n = std::min(piece, lens[i] - off);
                 J.pieces.push_back({i, off, n, off == 0 ? J.seeds[i] : 0});
                 off += n;
             } while (off < lens[i]);
         }
+        J.piece_start.resize(J.pieces.size() + 1, 0);
+        for (size_t q = 0; q < J.pieces.size(); ++q) J.piece_start[q + 1] = J.piece_start[q] + J.pieces[q].len;
         J.piece_val.assign(J.pieces.size(), 0);
-        for (int g = 0; g < G; ++g)
-            if (!per_dev[(size_t)g].empty()) J.spawn(device_worker, &J, g, std::move(per_dev[(size_t)g]));
+        H = std::min(H, J.pieces.size());
+        G = (int)std::min<size_t>((size_t)G, std::max<size_t>(1, (size_t)(total / kMinDevClaim)));  // tiny jobs: fewer lanes
+        // a hybrid job smaller than one slot finishes on the host threads before a lane's first copy
+        // and launch would (tens of microseconds): no lane
+        if (H > 0 && total < kSlotBytes) G = 0;
+        J.ndev = G;
+        J.hthreads = H;
+        for (int g = 0; g < G; ++g) J.spawn(device_worker, &J, g);
+        for (size_t t = 0; t < H; ++t) J.spawn(crc_host_worker, &J);
         *job_out = job.release();
         return 0;
     });
+}
+
+AWS_CRT_AMD_API int aws_crt_amd_host_submit(int alg, const void *const *h_ptrs, const size_t *lens, size_t count,
+                                            const void *h_seeds, void *h_out, int ndevices, struct aws_crt_amd_job **job_out) {
+    const struct aws_crt_amd_ingest_options opt = {ndevices, -1, nullptr};
+    return aws_crt_amd_host_submit_ex(alg, h_ptrs, lens, count, h_seeds, h_out, &opt, job_out);
 }
 
 AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
@@ -496,6 +581,7 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
             amdcrc_note_fallback();
             rc = 0;
         } else if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
+            if (J.dev_bytes_out) *J.dev_bytes_out = J.dev_bytes.load();
             // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
             const uint64_t poly = alg_poly(J.alg);
             const int w = alg_width(J.alg);

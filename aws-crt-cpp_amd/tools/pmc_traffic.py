@@ -19,10 +19,10 @@ import json
 import statistics
 
 
-def per_dispatch(path, kernel_substr):
+def per_dispatch(path, kernel_substr, grid=None):
     vals = {}
     for r in csv.DictReader(open(path)):
-        if kernel_substr not in r["Kernel_Name"]:
+        if kernel_substr not in r["Kernel_Name"] or (grid and int(r["Grid_Size"]) != grid):
             continue
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return vals
@@ -33,21 +33,22 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--rdreq")
     ap.add_argument("--kernel", default="crc32_stream_kernel")
+    ap.add_argument("--grid", type=int, help="only dispatches of this grid size (work-items): the launch shape measured")
     ap.add_argument("--workload", required=True)
     ap.add_argument("--bytes-per-launch", type=int, required=True)
     ap.add_argument("--batches-per-launch", type=int, default=1)
     ap.add_argument("--source", default="", help="where the counter CSV came from (recorded in the output)")
     ap.add_argument("--update", help="JSON file of records to add this record to (replacing the same shape)")
     a = ap.parse_args()
-    f = per_dispatch(a.fetch, a.kernel)["FETCH_SIZE"]
+    f = per_dispatch(a.fetch, a.kernel, a.grid)["FETCH_SIZE"]
     fetch_bytes = 2 * 1024 * statistics.median(f)
     rec = {"workload": a.workload, "batches_per_launch": a.batches_per_launch, "source": a.source,
-           "kernel": a.kernel, "dispatches": len(f),
+           "kernel": a.kernel, "grid_size": a.grid, "dispatches": len(f),
            "hbm_bytes_per_launch": round(fetch_bytes), "algorithmic_bytes_per_launch": a.bytes_per_launch,
            "traffic_over_algorithmic": round(fetch_bytes / a.bytes_per_launch, 4),
            "method": "2 x 1024 x median FETCH_SIZE per dispatch (gfx950 half-count correction)"}
     if a.rdreq:
-        r = per_dispatch(a.rdreq, a.kernel)
+        r = per_dispatch(a.rdreq, a.kernel, a.grid)
         req = statistics.median(r["TCC_EA0_RDREQ_sum"])
         req32 = statistics.median(r.get("TCC_EA0_RDREQ_32B_sum", [0.0]))
         rec["rdreq_bytes_per_launch"] = round(128 * (req - req32) + 32 * req32)

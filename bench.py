@@ -290,6 +290,42 @@ def kernel_name(alg, nbuf, L):
     return "xxh3_blocksum_kernel + xxh3_wave_kernel"
 
 
+def ingest_rates(eng, alg_id, ptrs, lens, reps=3):
+    """One host-ingest job over host buffers, hybrid (the CPU share's threads beside the device lane,
+    aws_crt_amd_host_submit's default) and devices only (the PCIe-bound pipeline): GiB/s (best of
+    `reps` after a warm-up), the devices' share of the bytes, and the hybrid job's results."""
+    nbytes = sum(lens)
+    out = {}
+    for name, ht in (("hybrid", -1), ("devices_only", 0)):
+        job = eng.HostJob(alg_id, ptrs, lens, host_threads=ht)
+        job.run()  # warm-up: device lanes, the first DMA touch of the pinned pages
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            job.run()
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        out[name] = {"gibs": round(nbytes / best / 2**30, 2), "device_share": round(job.device_bytes / max(nbytes, 1), 4)}
+        if ht < 0:
+            out["results"] = job.results()
+    return {"value": out["hybrid"]["gibs"], "unit": "GiB/s", "device_share": out["hybrid"]["device_share"],
+            "devices_only_gibs": out["devices_only"]["gibs"], "results": out["results"],
+            "api": "aws_crt_amd_host_submit (hybrid: host threads + device lane) + aws_crt_amd_job_wait"}
+
+
+def config_label(alg, count, L):
+    """the BASELINE.json config a bench shape is, or "custom" """
+    if alg == "crc32c" and count == 1024 and L == 65536:
+        return "C2"
+    if alg in ("crc64nvme", "xxh64") and L == 64 << 20:
+        return "C5"
+    if alg in ("crc32", "crc32c") and count == 16 and L == 256 << 20:
+        return "C3"
+    if count == 131072 and L == 8192:
+        return "C4 per-GPU shard"
+    return "custom"
+
+
 def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
     """One config step from pinned host memory through the host-ingest API (SURVEY.md §8(d)
     end-to-end row): results in host memory, checked against the device-resident results; beside it
@@ -299,12 +335,8 @@ def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
     host = torch.empty(nbuf * L, dtype=torch.uint8, pin_memory=True)
     host.copy_(dev_step[: nbuf * L])
     ptrs = [host.data_ptr() + i * L for i in range(nbuf)]
-    job = eng.HostJob(ALG[alg], ptrs, [L] * nbuf)
-    job.run()  # warm-up (device lanes, first DMA touch of the pinned pages)
-    t0 = time.perf_counter()
-    job.run()
-    el = time.perf_counter() - t0
-    parity = job.results() == gpu_results[:nbuf]
+    hy = ingest_rates(eng, ALG[alg], ptrs, [L] * nbuf)
+    parity = hy.pop("results")[:nbuf] == gpu_results[:nbuf]
     slot = torch.empty(min(nbuf * L, 256 << 20), dtype=torch.uint8, device=dev_step.device)
     cs = torch.cuda.Stream(device=dev_step.device)
     torch.cuda.synchronize()
@@ -316,9 +348,8 @@ def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
     torch.cuda.synchronize()
     el_h2d = time.perf_counter() - t1
     del host
-    return {"value": round(nbuf * L / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(nbuf * L / el_h2d / 2**30, 2),
-            "api": "aws_crt_amd_host_submit + aws_crt_amd_job_wait", "parity_with_device_path": parity,
-            "sample": f"one step ({nbuf} x {L} B) from pinned host memory, results to host memory"}
+    return dict(hy, h2d_only_gibs=round(nbuf * L / el_h2d / 2**30, 2), parity_with_device_path=parity,
+                sample=f"one step ({nbuf} x {L} B) from pinned host memory, results to host memory")
 
 
 def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,
@@ -390,12 +421,8 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
     ptrs = [base + (i % nb) * step + j * L for i in range(iters) for j in range(count)]
     lens = [L] * len(ptrs)
     first = eng.host_job(alg_id, ptrs[:count], lens[:count])
-    job = eng.HostJob(alg_id, ptrs, lens)  # argument arrays built before the timed region
-    job.run()  # warm-up: device lanes, and the first DMA touch of every pinned page
-    t0 = time.perf_counter()
-    job.run()
-    el = time.perf_counter() - t0
-    res = job.results()
+    hy = ingest_rates(eng, alg_id, ptrs, lens)
+    res = hy.pop("results")
     dev_out = eng.checksum_strided(alg_id, dev_data, L, L, count)
     torch.cuda.synchronize()
     parity = first == eng.as_unsigned(dev_out) and res[:count] == first
@@ -408,10 +435,9 @@ def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
             slot.copy_(host[(i % nb) * step:((i % nb) + 1) * step], non_blocking=True)
     torch.cuda.synchronize()
     el_h2d = time.perf_counter() - t1
-    return {"value": round(iters * step / el / 2**30, 2), "unit": "GiB/s", "h2d_only_gibs": round(iters * step / el_h2d / 2**30, 2),
-            "api": "aws_crt_amd_host_submit + aws_crt_amd_job_wait", "parity_with_device_path": parity,
-            "sample": f"{iters} C2 batches ({iters * count} parts of {L // 1024} KiB) from {nb * step >> 20} MiB pinned host "
-                      f"memory in one host job, results to host memory"}
+    return dict(hy, h2d_only_gibs=round(iters * step / el_h2d / 2**30, 2), parity_with_device_path=parity,
+                sample=f"{iters} C2 batches ({iters * count} parts of {L // 1024} KiB) from {nb * step >> 20} MiB pinned host "
+                       f"memory in one host job, results to host memory")
 
 
 def main_inproc(args):
@@ -468,7 +494,7 @@ def main_inproc(args):
         "unit": "GiB/s", "n_gpus": ndev, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes on device)",
-        "config": {"workload": f"C2: {count} x {L // 1024} KiB per step, {alg.upper()}, steps round-robin over "
+        "config": {"workload": f"{config_label(alg, count, L)}: {count} x {L // 1024} KiB per step, {alg.upper()}, steps round-robin over "
                                f"{ndev} GPU(s) of one process", "launch": f"in-process fan-out, up to {G} batches per launch, "
                                "one HIP stream per GPU", "parallelism": f"in-process, {ndev} device(s), no collective"},
         "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / ndev / HBM_PEAK_GBS, 2)}), flush=True)
@@ -702,8 +728,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint bytes on device)",
-            "config": {"workload": f"C2: {count} x {L // 1024} KiB independent buffers per step, {alg.upper()}, "
-                                   f"device-resident, per GPU",
+            "config": {"workload": f"{config_label(alg, count, L)}: {count} x {L // 1024} KiB independent buffers per step, "
+                                   f"{alg.upper()}, device-resident, per GPU",
                        "buffers_per_step": count, "buffer_bytes": L, "rotating_batches": nb,
                        "resident_bytes_per_gpu": nb * step_bytes,
                        "launch": f"aws_crt_amd_checksum_batches, up to {G} queued batches per launch "

@@ -97,6 +97,19 @@ AWS_CRT_AMD_API int aws_crt_amd_device_count(void);
 AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void);
 
 /*
+ * Per-stream state.  Launches on one stream share engine scratch in stream order (cross-tile
+ * workspace, descriptor staging, XXH3 block sums, multipart results), so the engine keeps that state
+ * per stream.  At most 64 streams per device hold state: a new stream beyond that takes over the
+ * state of the least recently used stream whose engine work has completed.  A caller that creates
+ * streams per request should release each one (before hipStreamDestroy): its state goes back at once
+ * and is reused once its last launch has completed -- release never waits and never frees, so device
+ * and pinned memory stay bounded by the streams whose work is in flight.  aws_crt_amd_stream_states
+ * reports the current device's live / spare / ever-created states.
+ */
+AWS_CRT_AMD_API int aws_crt_amd_stream_release(void *hip_stream);
+AWS_CRT_AMD_API int aws_crt_amd_stream_states(size_t *live, size_t *spare, size_t *created);
+
+/*
  * Uniform batch: buffer i = [d_base + i*stride, + len), i < count.  stride must be a multiple of
  * 16 (or count == 1).  d_seeds: device array of count seeds (uint32_t for CRC32/32C, uint64_t
  * otherwise) or NULL for seed 0.  This is the shape of BASELINE.json configs 2, 4 and 5.
@@ -133,14 +146,36 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_batches(
     void *hip_stream);
 
 /*
+ * Prepared submission: the planning of aws_crt_amd_checksum_batches (runs of batches, kernel, tile
+ * size, launch geometry, constant tables) done once for fixed batches; aws_crt_amd_plan_launch then
+ * only launches, on any stream of the plan's device, as often as wanted (a producer that re-submits
+ * the same resident buffers, e.g. a ring of part slots).  The batches' memory must stay valid while
+ * the plan may be launched.  plan_launches = launches per plan_launch (hashes: one per batch).
+ */
+struct aws_crt_amd_plan;
+AWS_CRT_AMD_API int aws_crt_amd_plan_create(
+    int algorithm,
+    const struct aws_crt_amd_batch *batches,
+    size_t nbatches,
+    size_t stride,
+    size_t len,
+    size_t count,
+    struct aws_crt_amd_plan **out_plan);
+AWS_CRT_AMD_API int aws_crt_amd_plan_launch(struct aws_crt_amd_plan *plan, void *hip_stream);
+AWS_CRT_AMD_API size_t aws_crt_amd_plan_launches(const struct aws_crt_amd_plan *plan);
+AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(struct aws_crt_amd_plan *plan);
+
+/*
  * Submission queue: a producer that gets one uniform batch at a time (aws-c-s3 checksumming parts as
  * they arrive, source/s3/S3.cpp:1133-1149) pushes each batch and the engine launches them together:
  * a push queues (base, seeds, out) without launching; the queue launches on its stream when it holds
  * 32 batches (one launch, as aws_crt_amd_checksum_batches), and at aws_crt_amd_queue_flush or
  * aws_crt_amd_queue_destroy.  Work is on the stream only after the launch that holds it: a caller
  * that synchronises the stream, records an event on it or reads a result flushes first.  Every
- * batch of a queue has the queue's algorithm and shape (stride, len, count).  Push, flush and pending
- * may be called from several threads; destroy must not overlap any other call on the same queue.
+ * batch of a queue has the queue's algorithm and shape (stride, len, count).  Push, flush, pending,
+ * status and wait may be called from several threads; destroy must not overlap any other call on the
+ * same queue.  A refused launch (e.g. a HIP error) drops the batches it held: the push or flush that
+ * made it returns the error, and every dropped batch's ticket reports it (below).
  */
 struct aws_crt_amd_queue;
 AWS_CRT_AMD_API int aws_crt_amd_queue_create(
@@ -154,8 +189,46 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_push(struct aws_crt_amd_queue *queue, cons
 AWS_CRT_AMD_API int aws_crt_amd_queue_flush(struct aws_crt_amd_queue *queue);
 /* batches pushed and not yet launched */
 AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const struct aws_crt_amd_queue *queue);
-/* flushes, then frees the queue; returns the flush's status */
+/* flushes (and stops the age flusher), then frees the queue; returns the flush's status */
 AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
+
+/*
+ * Queue policy and per-push completion (round 4).
+ *   max_batches  launch when this many batches are queued (1..32; 0 = 32)
+ *   max_age_us   0 = no age bound; otherwise a flusher thread launches the queued batches once the
+ *                oldest has waited this long, so no push waits for later pushes indefinitely
+ * Each push_ex returns a ticket (1, 2, ... per queue).  queue_status(ticket):
+ *   AWS_CRT_AMD_TICKET_QUEUED    pushed, not launched yet
+ *   AWS_CRT_AMD_TICKET_LAUNCHED  on the stream, not complete
+ *   0                            complete: the batch's results are written
+ *   < 0                          the launch that held it was refused (that status): its results are
+ *                                never written -- every batch of a refused launch reports it
+ * queue_wait(ticket) launches the ticket's batch if it is still queued and waits for it; it returns 0
+ * or the error.  queue_first_pending: the ticket of the oldest queued batch (every lower ticket has
+ * been launched or refused).  Status and wait may be called from any thread.
+ */
+enum { AWS_CRT_AMD_TICKET_QUEUED = 1, AWS_CRT_AMD_TICKET_LAUNCHED = 2 };
+struct aws_crt_amd_queue_options {
+    size_t max_batches;
+    uint64_t max_age_us;
+};
+AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(
+    int algorithm,
+    size_t stride,
+    size_t len,
+    size_t count,
+    void *hip_stream,
+    const struct aws_crt_amd_queue_options *options,
+    struct aws_crt_amd_queue **out_queue);
+AWS_CRT_AMD_API int aws_crt_amd_queue_push_ex(
+    struct aws_crt_amd_queue *queue,
+    const void *d_base,
+    const void *d_seeds,
+    void *d_out,
+    uint64_t *ticket);
+AWS_CRT_AMD_API int aws_crt_amd_queue_status(struct aws_crt_amd_queue *queue, uint64_t ticket);
+AWS_CRT_AMD_API int aws_crt_amd_queue_wait(struct aws_crt_amd_queue *queue, uint64_t ticket);
+AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_first_pending(const struct aws_crt_amd_queue *queue);
 
 /*
  * Ragged batch: buffer i = [d_ptrs[i], + lens[i]).  d_ptrs and lens are HOST arrays describing
@@ -224,11 +297,14 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_host(
  * S3.cpp:1133-1149).  Asynchronous: checksums `count` HOST buffers and writes one result per buffer
  * to the HOST array h_out (u32 CRC32/32C, u64 CRC64NVME/XXH64/XXH3_64, two u64 {high, low}
  * XXH3_128) once aws_crt_amd_job_wait(job) returns 0.  Buffers, seeds and h_out must stay valid
- * until then.  CRCs: buffers round-robin over `ndevices` GPUs (0 = all visible), each device a
- * three-slot pipeline (H2D on a copy stream overlapping the scans; 32 MiB slots; longer buffers cut
- * into pieces folded with Combine).  Registered / pinned memory is DMA'd in place; pageable memory
- * goes through pinned mirrors.  xxHash (a serial chain per buffer), and every algorithm when no
- * device is visible, run on the host path.  h_seeds: u32 (CRC32/32C) or u64 per buffer, or NULL.
+ * until then.  CRCs are split between the host threads of the process's CPU share and `ndevices`
+ * GPUs (0 = all visible): both take runs of pieces from one cursor over the job (work stealing), so
+ * a job is never slower than the host path alone.  Each device runs a three-slot pipeline (H2D on a
+ * copy stream overlapping the scans; 32 MiB slots); buffers longer than a piece (8 MiB, or a slot
+ * when no host thread takes part) are cut into pieces folded with Combine.  Registered / pinned
+ * memory is DMA'd in place; pageable memory goes through pinned mirrors.  xxHash (a serial chain per
+ * buffer), and every algorithm when no device is usable, run on the host path.  h_seeds: u32
+ * (CRC32/32C) or u64 per buffer, or NULL.
  */
 struct aws_crt_amd_job;
 AWS_CRT_AMD_API int aws_crt_amd_host_submit(
@@ -239,6 +315,26 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(
     const void *h_seeds,
     void *h_out,
     int ndevices,
+    struct aws_crt_amd_job **job);
+/*
+ * aws_crt_amd_host_submit with options.  host_threads: -1 = the CPU share less one thread per device
+ * lane (what aws_crt_amd_host_submit does), 0 = devices only (the PCIe-bound pipeline), n = n host
+ * threads beside the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the
+ * devices checksummed.
+ */
+struct aws_crt_amd_ingest_options {
+    int ndevices;
+    int host_threads;
+    uint64_t *device_bytes;
+};
+AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(
+    int algorithm,
+    const void *const *h_ptrs,
+    const size_t *lens,
+    size_t count,
+    const void *h_seeds,
+    void *h_out,
+    const struct aws_crt_amd_ingest_options *options,
     struct aws_crt_amd_job **job);
 /* Wait for a job and release it; returns its status (aws_crt_amd_job_last_error() on failure). */
 AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job);

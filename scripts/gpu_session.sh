@@ -17,8 +17,18 @@ for s in "$@"; do
     test)  step 900 $O/pytest.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest.log ;;
     smoke) step 180 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; tail -2 $O/smoke.log ;;
     bench) step 400 $O/bench.log python -u bench.py ${BENCH_ARGS:-}; rc=$?; tail -1 $O/bench.log ;;
+    driver*) step 400 $O/$s.log python -u bench.py --gpus 1 --steps 20 --warmup 5; rc=$?; grep '^{' $O/$s.log | cut -c1-400 ;;
+    # the timed region decomposed: kernel + HIP API trace of the driver's timed region (legs trimmed)
+    trace) (cd /tmp && step 300 $O/trace.log rocprofv3 --kernel-trace --hip-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0); rc=$? ;;
+    # kernel trace of the driver's exact command
+    kprof) (cd /tmp && step 420 $O/kprof.log rocprofv3 --kernel-trace --stats -d $O/kprof -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5); rc=$? ;;
     prof)  (cd /tmp && step 300 $O/prof.log rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $P ${PROF_ARGS:-}); rc=$? ;;
     pmc)   (cd /tmp && step 120 $O/pmc_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py $P ${PROF_ARGS:-}); rc=$? ;;
+    # the driver-shaped region per submission path, under HIP runtime settings (one process each)
+    probe) for v in "" "ROC_ACTIVE_WAIT_TIMEOUT=1000" "HIP_FORCE_DEV_KERNARG=0" "HIP_FORCE_DEV_KERNARG=1" "AMDCRC_PROBE_SCHED=spin" "AMDCRC_PROBE_SCHED=blocking"; do
+             step 120 $O/probe.log.tmp env $v python -u aws-crt-cpp_amd/tools/overhead_probe.py 20 40; rc=$?; cat $O/probe.log.tmp >> $O/probe.log
+             [ $rc -ne 0 ] && break; done; grep '^{' $O/probe.log | cut -c1-600 ;;
+    tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac

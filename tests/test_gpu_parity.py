@@ -154,6 +154,21 @@ def test_xxh64_strided_wave_kernel(engine, L, off, count, stride_pad):
                                              for i, s in enumerate(seeds)]
 
 
+def test_xxh64_overlapping_long_buffers(engine):
+    """Few long XXH64 buffers whose stride is below their length -- stride 0 (one buffer under several
+    seeds) and overlapping windows -- cannot be copied row by row (a 2D copy's pitch must cover its
+    width): they stay on the kernels and equal the oracle."""
+    L, n = (1 << 20) + 77, 6
+    d = dev_random(L + n * 4096 + 64, 79)
+    h = host_bytes(d)
+    rng = random.Random(79)
+    for stride in (0, 4096, 16):
+        seeds = [rng.getrandbits(64) for _ in range(n)]
+        out = engine.checksum_strided(ALG["xxh64"], d, stride, L, n, seeds=seeds_tensor("xxh64", seeds), base_offset=5)
+        assert results(engine, "xxh64", out) == [oracle.checksum("xxh64", h[5 + i * stride: 5 + i * stride + L], s)
+                                                 for i, s in enumerate(seeds)], stride
+
+
 def test_xxh64_few_long_buffers_host_route(engine):
     """Strided XXH64 batches of at most 32 buffers of >= 1 MiB take the stream-ordered host route
     (engine.cpp xxh64_host_route: D2H slices, host threads, results H2D on the caller's stream; a
@@ -506,6 +521,36 @@ def test_checksum_batches(engine, alg):
             want = [oracle.checksum(alg, h[offs[j] + i * stride: offs[j] + i * stride + L], seeds[j][i] if seeds[j] else 0)
                     for i in range(count)]
             assert engine.as_unsigned(outs[j]) == want, (L, j)
+
+
+@pytest.mark.parametrize("alg", ["crc32c", "crc64nvme", "xxh64"])
+def test_plan_launch(engine, alg):
+    """aws_crt_amd_plan_*: a prepared submission launched twice, on two streams, equals the oracle
+    each time; shapes whose kernels need the per-stream cross-tile workspace (multi-tile buffers,
+    CRC64NVME XCD-window chunks) take it from the launch's stream."""
+    import torch
+
+    rng = random.Random(0x91A + ALG[alg])
+    for L, count, nb in [(65536, 64, 5), (1 << 20, 40, 3), (4 << 20, 3, 2), (4096 * 3 + 20, 33, 4)]:
+        stride = (L + 15) // 16 * 16 + 16
+        d = dev_random(nb * (stride * count + 64), 77 + L % 11)
+        offs = [j * (stride * count + 64) + (3 if j == 1 else 0) for j in range(nb)]
+        seeds = [[rng.getrandbits(64 if alg in W64 else 32) for _ in range(count)] if j % 2 else None for j in range(nb)]
+        outs = [torch.full((count,), 7, dtype=torch.int64 if alg in W64 else torch.int32, device="cuda") for _ in range(nb)]
+        batches = [(d.data_ptr() + o, seeds_tensor(alg, sd) if sd else None, out) for o, sd, out in zip(offs, seeds, outs)]
+        plan = engine.BatchSet(ALG[alg], batches, stride, L, count)
+        assert plan.launches >= 1
+        h = host_bytes(d)
+        want = [[oracle.checksum(alg, h[offs[j] + i * stride: offs[j] + i * stride + L], seeds[j][i] if seeds[j] else 0)
+                 for i in range(count)] for j in range(nb)]
+        for st in (torch.cuda.Stream(), torch.cuda.Stream()):
+            for o in outs:
+                o.fill_(7)
+            torch.cuda.synchronize()
+            plan.run(st)
+            torch.cuda.synchronize()
+            for j in range(nb):
+                assert engine.as_unsigned(outs[j]) == want[j], (L, j)
 
 
 @pytest.mark.parametrize("alg", ["xxh3_64", "xxh3_128"])

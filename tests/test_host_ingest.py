@@ -40,15 +40,46 @@ def test_host_job_without_device_uses_host_path():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("host_threads", [-1, 0])
 @pytest.mark.parametrize("alg", list(ALG))
-def test_host_job_pageable(engine, alg):
+def test_host_job_pageable(engine, alg, host_threads):
+    """hybrid (host threads beside the device lane, the default) and devices only"""
     rng = random.Random(0x1A + ALG[alg])
     sizes = [0, 1, 15, 4096, 65536, 65537, (32 << 20) - 3, (32 << 20) + 17, (70 << 20) + 5] + \
             [rng.randrange(1, 300000) for _ in range(200)]
     bufs = _bufs(rng, sizes)
     seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
-    got = engine.host_job(ALG[alg], [_addr(b) for b in bufs], [b.size for b in bufs], seeds)
+    got = engine.host_job(ALG[alg], [_addr(b) for b in bufs], [b.size for b in bufs], seeds, host_threads=host_threads)
     assert got == [oracle.checksum(alg, b, s) for b, s in zip(bufs, seeds)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ["crc32c", "crc64nvme"])
+def test_host_job_hybrid_split(engine, alg):
+    """A hybrid job's pieces go to the host threads and the device lane (both take some), a
+    devices-only job's all to the lane, a host-threads-only split with a fixed thread count; buffers
+    cut into 8 MiB pieces at odd offsets join with Combine."""
+    import torch
+
+    rng = random.Random(0x4B + ALG[alg])
+    lens = [(8 << 20) + 5, 3, (24 << 20) - 7, 65536] * 6 + [rng.randrange(1, 1 << 20) for _ in range(64)]
+    total = sum(lens)
+    host = torch.randint(0, 256, (total + 64,), dtype=torch.uint8).pin_memory()
+    a = host.numpy()
+    offs, o = [], 1
+    for n in lens:
+        offs.append(o)
+        o += n
+    ptrs = [host.data_ptr() + o for o in offs]
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    want = [oracle.checksum(alg, a[o:o + n], s) for o, n, s in zip(offs, lens, seeds)]
+    for ht, check in ((-1, lambda d: 0 < d < total), (0, lambda d: d == total), (3, lambda d: 0 < d < total)):
+        job = engine.HostJob(ALG[alg], ptrs, lens, seeds, host_threads=ht)
+        job.run()  # the first job may find the lane still being set up (it claims once it is ready)
+        assert job.results() == want, ht
+        job.run()
+        assert job.results() == want, ht
+        assert check(job.device_bytes), (ht, job.device_bytes, total)
 
 
 @pytest.mark.gpu

@@ -49,6 +49,55 @@ def test_queue_host_logic_without_device():
                    "flush": "-1", "pending_after": "0", "destroy_empty": "0"}
 
 
+def test_queue_tickets_refused_launch_and_age_flush_without_device():
+    """Tickets and completion without a device: every batch of a refused launch reports the launch's
+    error (AWS_CRT_AMD_ERR_NO_DEVICE) through its ticket, queued tickets report QUEUED, unknown
+    tickets are refused; max_batches launches early; the age bound launches without a further push."""
+    code = (
+        "import ctypes, time\n"
+        f"L=ctypes.CDLL({LIB!r})\n"
+        "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
+        "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
+        "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
+        "L.aws_crt_amd_queue_status.argtypes=[vp,u64]; L.aws_crt_amd_queue_wait.argtypes=[vp,u64]\n"
+        "L.aws_crt_amd_queue_pending.argtypes=[vp]; L.aws_crt_amd_queue_pending.restype=sz\n"
+        "L.aws_crt_amd_queue_first_pending.argtypes=[vp]; L.aws_crt_amd_queue_first_pending.restype=u64\n"
+        "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
+        "q=vp(); t=u64()\n"
+        "print('too_many', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(33,0)),ctypes.byref(q)))\n"
+        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(3,0)),ctypes.byref(q)))\n"
+        "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(4)]\n"
+        "print('push_rcs', ','.join(map(str,r)), 'last_ticket', t.value)\n"
+        "print('st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,5)))\n"
+        "print('bad_ticket', L.aws_crt_amd_queue_status(q,0), L.aws_crt_amd_queue_status(q,9))\n"
+        "print('first_pending', L.aws_crt_amd_queue_first_pending(q))\n"
+        "print('wait4', L.aws_crt_amd_queue_wait(q,4), 'pending', L.aws_crt_amd_queue_pending(q))\n"
+        "print('destroy', L.aws_crt_amd_queue_destroy(q))\n"
+        "print('create_age', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,2000)),ctypes.byref(q)))\n"
+        "for i in range(3): L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t))\n"
+        "dl=time.time()+5\n"
+        "while L.aws_crt_amd_queue_pending(q) and time.time()<dl: time.sleep(0.002)\n"
+        "print('age_pending', L.aws_crt_amd_queue_pending(q), 'age_st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,4)))\n"
+        "print('destroy_age', L.aws_crt_amd_queue_destroy(q))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+    assert r.returncode == 0, r.stderr
+    got = {}
+    for line in r.stdout.split("\n"):
+        f = line.split()
+        for i in range(0, len(f) - 1, 2):
+            got[f[i]] = f[i + 1]
+    assert got["too_many"] == "-2" and got["create"] == "0"
+    assert got["push_rcs"] == "0,0,-1,0" and got["last_ticket"] == "4"  # the 3rd push launched (max_batches 3): refused
+    assert got["st"] == "-1,-1,-1,1"  # the refused launch's three tickets; ticket 4 still queued
+    assert got["bad_ticket"] == "-2" and got["first_pending"] == "4"
+    assert got["wait4"] == "-1" and got["pending"] == "0"  # wait launched it (refused) and reports that
+    assert got["destroy"] == "0" and got["create_age"] == "0"
+    assert got["age_pending"] == "0" and got["age_st"] == "-1,-1,-1"  # the flusher launched them, no push needed
+    assert got["destroy_age"] == "0"
+
+
 def _dev_random(n, seed):
     import torch
 
@@ -109,3 +158,52 @@ def test_queue_close_flushes(engine, alg, n, L):
         for i in range(n):
             o = (j * n + i) * L
             assert got[i] == oracle.checksum(alg, h[o:o + L]), (j, i)
+
+
+@pytest.mark.gpu
+def test_queue_tickets_age_bound_and_refused_flush(engine):
+    """Per-push completion on the GPU: tickets complete (0) once their launch has run, with correct
+    results; an age-bounded queue launches a lone push by itself; and a flush the engine refuses --
+    queued on a stream under graph capture, whose batch needs a workspace the engine may not allocate
+    during capture -- reports the error to every batch it dropped."""
+    import time
+
+    import torch
+
+    n, L = 16, 65536
+    d = _dev_random(n * L * 4, 0xA1)
+    h = d.cpu().numpy()
+    outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(4)]
+    q = engine.Queue(ALG["crc32c"], L, L, n, max_batches=2)
+    t = [q.push(d[j * n * L:], outs[j]) for j in range(3)]
+    assert t == [1, 2, 3] and q.status(3) == engine.TICKET_QUEUED
+    assert q.wait(1) == 0 and q.wait(3) == 0 and q.status(2) == 0
+    for j in range(3):
+        assert engine.as_unsigned(outs[j])[5] == oracle.crc("crc32c", h[(j * n + 5) * L:(j * n + 6) * L]), j
+    q.close()
+    # age bound: a single push is launched by the flusher
+    qa = engine.Queue(ALG["crc32c"], L, L, n, max_age_us=500)
+    ta = qa.push(d[3 * n * L:], outs[3])
+    deadline = time.time() + 5
+    while qa.pending() and time.time() < deadline:
+        time.sleep(0.001)
+    assert qa.pending() == 0 and qa.wait(ta) == 0
+    assert engine.as_unsigned(outs[3])[0] == oracle.crc("crc32c", h[3 * n * L:(3 * n + 1) * L])
+    qa.close()
+    # refused flush: one 6 GiB buffer is 24,576 tiles, whose tile-shift columns the engine has never
+    # built (nothing else scans a buffer that long); on a stream that is capturing the engine refuses
+    # to build them (no allocation under capture), so the launch is refused.  The bytes are never read.
+    big = torch.empty(6 << 30, dtype=torch.uint8, device="cuda")
+    bo = [torch.empty(1, dtype=torch.int32, device="cuda") for _ in range(2)]
+    cs = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    qr = None
+    with torch.cuda.graph(g, stream=cs):
+        qr = engine.Queue(ALG["crc32c"], 6 << 30, 6 << 30, 1, stream=cs)
+        tr = [qr.push(big, bo[j]) for j in range(2)]
+        with pytest.raises(engine.EngineError):
+            qr.flush()
+    assert [qr.status(x) for x in tr] == [-2, -2]  # AWS_CRT_AMD_ERR_INVALID_ARG, for both batches
+    assert qr.wait(tr[1]) == -2
+    qr.close()
+    del big
