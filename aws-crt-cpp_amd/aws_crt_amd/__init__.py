@@ -144,28 +144,50 @@ def _out_dtype(alg: int):
 
 
 def time_next_launch(start_event, stop_event) -> None:
-    """Diagnostics: the next scan launched by this thread stamps its own dispatch start / end into
-    these torch.cuda.Event objects (created with enable_timing=True)."""
+    """Profiling (aws_crt_amd_profile_next_launch): the next launch made by this thread stamps its own
+    dispatch start / end into these torch.cuda.Event objects (created with enable_timing=True)."""
     L = lib()
-    L.aws_crt_amd_debug_time_next_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    L.aws_crt_amd_debug_time_next_launch(start_event.cuda_event, stop_event.cuda_event)
+    L.aws_crt_amd_profile_next_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.aws_crt_amd_profile_next_launch(start_event.cuda_event, stop_event.cuda_event)
 
 
-def read_ceiling(base, nbytes: int, stream=None, base_offset: int = 0) -> None:
-    """Diagnostics: one launch of the streaming-read ceiling kernel (the W=32 streaming scan's launch
-    shape, CRC removed) over nbytes of device memory; honours time_next_launch."""
-    L = lib()
-    L.aws_crt_amd_debug_read_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+DIAG_LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-crt-cpp-amd-diag.so")
+_diag = None
+
+
+def diag_lib() -> ctypes.CDLL:
+    """The diagnostic build of the engine (make diag: the same sources plus the read-ceiling kernel and
+    the host-tier hook).  Measurement and tests only; checksums always go through lib()."""
+    global _diag
+    if _diag is None:
+        lib()  # torch's HIP runtime first (one runtime per process)
+        if not os.path.exists(DIAG_LIB_PATH):
+            raise EngineError(f"diagnostic engine not built: {DIAG_LIB_PATH} missing (make -C aws-crt-cpp_amd diag)")
+        _diag = ctypes.CDLL(DIAG_LIB_PATH)
+    return _diag
+
+
+def read_ceiling(base, nbytes: int, stream=None, base_offset: int = 0, start_event=None, stop_event=None) -> None:
+    """Diagnostics (diagnostic library): one launch of the streaming-read ceiling kernel (the W=32
+    streaming scan's launch shape, CRC removed) over nbytes of device memory, optionally stamping its
+    dispatch into (start_event, stop_event)."""
+    D = diag_lib()
+    D.aws_crt_amd_debug_read_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    if start_event is not None:
+        D.aws_crt_amd_profile_next_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        D.aws_crt_amd_profile_next_launch(start_event.cuda_event, stop_event.cuda_event)
     addr = (base.data_ptr() if hasattr(base, "data_ptr") else int(base)) + base_offset
-    _check(L.aws_crt_amd_debug_read_ceiling(addr, nbytes, _stream_handle(stream)))
+    rc = D.aws_crt_amd_debug_read_ceiling(addr, nbytes, _stream_handle(stream))
+    if rc != 0:
+        raise EngineError(f"read ceiling launch failed ({rc})")
 
 
 def event_ms(start_event, stop_event) -> float:
-    """Milliseconds between two events stamped by time_next_launch."""
+    """Milliseconds between two events stamped by time_next_launch (aws_crt_amd_profile_elapsed_ms)."""
     L = lib()
-    L.aws_crt_amd_debug_event_ms.restype = ctypes.c_float
-    L.aws_crt_amd_debug_event_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    ms = L.aws_crt_amd_debug_event_ms(start_event.cuda_event, stop_event.cuda_event)
+    L.aws_crt_amd_profile_elapsed_ms.restype = ctypes.c_float
+    L.aws_crt_amd_profile_elapsed_ms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    ms = L.aws_crt_amd_profile_elapsed_ms(start_event.cuda_event, stop_event.cuda_event)
     if ms < 0:
         raise EngineError("event timing failed")
     return ms

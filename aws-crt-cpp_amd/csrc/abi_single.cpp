@@ -241,11 +241,13 @@ AWS_CRT_AMD_API const char *aws_crt_amd_cpu_tier(void) {
     }
 }
 
-// Test hook (not in the public headers): one CRC on a given host tier (0 tables, 1 PCLMULQDQ,
-// 2 AVX-512 VPCLMULQDQ; clamped to what the host supports), so every tier is checked on any host.
+#if AWS_CRT_AMD_DIAG
+// Diagnostic library only: one CRC on a given host tier (0 tables, 1 PCLMULQDQ, 2 AVX-512
+// VPCLMULQDQ; clamped to what the host supports), so every tier is checked on any host.
 AWS_CRT_AMD_API uint64_t aws_crt_amd_debug_cpu_crc(int alg, int tier, const uint8_t *p, size_t n, uint64_t previous) {
     return cpu::crc_tier(alg, p, n, previous, (cpu::Tier)tier);
 }
+#endif
 
 // ---- aws-checksums CRC ABI (include/aws/checksums/crc.h)
 AWS_CRT_AMD_API void aws_checksums_library_init(struct aws_allocator *) {

@@ -2452,7 +2452,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
 // ------------------------------------------------------------------------------------------
 // W = 64 scan of long uniform buffers in XCD windows (crc64_xcd_kernel, round 3).  Streaming reads
 // ran 4-10 % faster when the waves of one XCD read neighbouring 4-16 KiB pieces of one window than
-// when every wave streams its own contiguous range (aws-crt-cpp_amd/tools/readpattern.hip; with the
+// when every wave streams its own contiguous range (experiments/readpattern.hip; with the
 // CRC64 scan's slower waves the gap was 6 %: profiles/r03/order).  So the launch's main bytes, all
 // buffers' main regions in order, are cut into chunks of kXcdChunkGroups 4 KiB groups; XCD x
 // (blockIdx mod 8 under round-robin dispatch) takes the x-th eighth of the chunks, and its nwx waves
@@ -3416,15 +3416,29 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
     }
     uint64_t k = n >> 3;
     // 16 bytes per lane per load instruction: the lanes of a wave read 64 different buffers, so the
-    // instruction count per byte (one cache-line request per lane), not bandwidth, bounds this loop
-    for (; k >= 8; k -= 8, w += 8) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
-        uint64_t v[8];
+    // instruction count per byte (one cache-line request per lane), not bandwidth, bounds this loop.
+    // Software-pipelined (round 4): the next 64 bytes' loads are in flight while the current 64 are
+    // folded, so a lane waits for memory once per buffer, not once per 64 bytes.
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+    auto load8 = [](const uint64_t *p, uint64_t *v) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const u64x2 x = *(const __attribute__((address_space(1))) u64x2 *)(w + 2 * j);
+            const u64x2 x = *(const __attribute__((address_space(1))) u64x2 *)(p + 2 * j);
             v[2 * j] = x.x;
             v[2 * j + 1] = x.y;
+        }
+    };
+    if (k >= 8) {
+        uint64_t v[8], nv[8];
+        load8(w, v);
+        w += 8;
+        k -= 8;
+        for (; k >= 8; k -= 8, w += 8) {
+            load8(w, nv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = nv[j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
@@ -3508,6 +3522,7 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
 
 }  // namespace
 
+#if AWS_CRT_AMD_DIAG  // diagnostic library only (lib/libaws-crt-cpp-amd-diag.so)
 // ------------------------------------------------------------------------------------------
 // Streaming-read ceiling (diagnostics; SURVEY.md §8(d) "secondary denominator"): the W=32 streaming
 // scan's launch shape with the CRC removed -- 512-thread workgroups, one per CU, each wave a
@@ -3557,6 +3572,7 @@ extern "C" int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint
     return (int)hipGetLastError();
 }
 
+#if AWS_CRT_AMD_DIAG
 // Debug builds (-DAMDCRC_GUARD): read and clear the streaming scan's guard record
 extern "C" __attribute__((visibility("default"))) int amdcrc_debug_guard(unsigned long long *out4) {
 #ifdef AMDCRC_GUARD
@@ -3568,6 +3584,8 @@ extern "C" __attribute__((visibility("default"))) int amdcrc_debug_guard(unsigne
     return 0;
 #endif
 }
+#endif
+#endif  // AWS_CRT_AMD_DIAG
 
 extern "C" int amdcrc_launch_combine(int alg, const CombineParams *p, void *stream) {
     const unsigned blocks = (unsigned)((p->n + 255) / 256);

@@ -632,7 +632,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
 
 // ---- XXH64 over few long device buffers: the stream-ordered host route.
 // XXH64 is one serial chain per buffer (four lanes whose every round depends on the last): on a
-// gfx950 SIMD a round is issue-bound at about 41 cycles (tools/chainbench: 31.5 for the six chain
+// gfx950 SIMD a round is issue-bound at about 41 cycles (experiments/chainbench.hip: 31.5 for the six chain
 // instructions, 9 more for the two DPP moves that bring the next stripe's product in), 1.7 GiB/s
 // per buffer, against about 1.3 ns per round on one host core.  A batch of at most kX64HostMaxBuffers
 // long buffers therefore goes to the host: slices of every buffer (one hipMemcpy2DAsync per slice)
@@ -1358,27 +1358,28 @@ AWS_CRT_AMD_API int aws_crt_amd_device_count(void) { return device_count_noinit(
 
 AWS_CRT_AMD_API const char *aws_crt_amd_last_error(void) { return g_last_error.c_str(); }
 
-// Measurement hook (not part of the public headers): the next scan launched by this thread records
-// the dispatch's own start / end timestamps into these hipEvent_t (hipExtLaunchKernel), the interval
-// a kernel-trace profiler reports, without the marker packets of a hipEventRecord pair.
-AWS_CRT_AMD_API void aws_crt_amd_debug_time_next_launch(void *start_event, void *stop_event) {
+// Launch profiling (checksums_batch.h): the next launch made by this thread stamps the dispatch's own
+// start / end timestamps into these hipEvent_t (hipExtLaunchKernel), the interval a kernel-trace
+// profiler reports, without the marker packets of a hipEventRecord pair.
+AWS_CRT_AMD_API void aws_crt_amd_profile_next_launch(void *start_event, void *stop_event) {
     g_time_events[0] = start_event;
     g_time_events[1] = stop_event;
 }
 
-// Measurement hook: elapsed milliseconds between two events stamped by
-// aws_crt_amd_debug_time_next_launch (torch's Event.elapsed_time refuses events it did not record).
-AWS_CRT_AMD_API float aws_crt_amd_debug_event_ms(void *start_event, void *stop_event) {
+// Elapsed milliseconds between two events stamped by aws_crt_amd_profile_next_launch (waits for the
+// stop event); -1 on failure.
+AWS_CRT_AMD_API float aws_crt_amd_profile_elapsed_ms(void *start_event, void *stop_event) {
     float ms = -1.0f;
     if (hipEventSynchronize((hipEvent_t)stop_event) != hipSuccess) return -1.0f;
     if (hipEventElapsedTime(&ms, (hipEvent_t)start_event, (hipEvent_t)stop_event) != hipSuccess) return -1.0f;
     return ms;
 }
 
-// Measurement hook: one launch of the streaming-read ceiling kernel (crc_kernels.hip
+#if AWS_CRT_AMD_DIAG
+// Diagnostic library only: one launch of the streaming-read ceiling kernel (crc_kernels.hip
 // read_ceiling_kernel) over [d_base, d_base + bytes), in the W=32 streaming scan's launch shape
 // (512-thread workgroups, one per CU below 256 MiB, two above).  Honours
-// aws_crt_amd_debug_time_next_launch.
+// aws_crt_amd_profile_next_launch.
 AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t bytes, void *hip_stream) {
     return guarded(err_sink, [&]() -> int {
         Device *d;
@@ -1398,6 +1399,7 @@ AWS_CRT_AMD_API int aws_crt_amd_debug_read_ceiling(const void *d_base, size_t by
         return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("read ceiling launch: ") + hipGetErrorString((hipError_t)e)) : 0;
     });
 }
+#endif
 
 // Per-stream state (stream_states.h): hand a stream's state back (before destroying the stream, or
 // when it will not be used with the engine for a while); at most kMaxStreamStates streams per device

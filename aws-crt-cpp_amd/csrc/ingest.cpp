@@ -203,7 +203,7 @@ bool claim(JobImpl *job, uint64_t budget, size_t max_pieces, size_t *a, size_t *
         const uint64_t lim = job->piece_start[cur] + std::max<uint64_t>(budget, 1);
         size_t e = (size_t)(std::upper_bound(job->piece_start.begin() + (long)cur + 1, job->piece_start.end(), lim) -
                             job->piece_start.begin()) - 1;
-        e = std::min(std::max(e, cur + 1), std::min(n, cur + max_pieces));
+        e = std::min(std::max(e, cur + 1), max_pieces >= n - cur ? n : cur + max_pieces);
         if (job->cursor.compare_exchange_weak(cur, e, std::memory_order_relaxed)) {
             *a = cur;
             *b = e;
@@ -520,18 +520,21 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
             amdcrc_note_fallback();  // a visible device the engine cannot use (not gfx950, HIP error)
             G = 0;
         }
-        if (!is_crc(alg) || G <= 0) {
-            // xxHash (or no usable device): the host path on the process's CPU share
+        if (!is_crc(alg)) {
+            // xxHash: the host path on the process's CPU share, a thread per buffer at a time
             const size_t threads = host_threads(count);
             for (size_t t = 0; t < threads; ++t) J.spawn(host_worker, &J, t, threads);
             *job_out = job.release();
             return 0;
         }
-        // host threads beside the lanes: the CPU share less one thread per lane (auto), or as asked
+        // host threads beside the lanes: the CPU share less one thread per lane (auto), or as asked;
+        // with no usable device the CPU share alone takes every piece
+        if (G < 0) G = 0;
         uint64_t total = 0;
         for (size_t i = 0; i < count; ++i) total += lens[i];
         const size_t share = host_threads(SIZE_MAX);
-        size_t H = want_host < 0 ? (share > (size_t)G ? share - (size_t)G : 0) : (size_t)want_host;
+        size_t H = want_host < 0 || G == 0 ? (share > (size_t)G ? share - (size_t)G : 1) : (size_t)want_host;
+        if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
         // pieces, buffer by buffer, in job order
         for (size_t i = 0; i < count; ++i) {
@@ -546,7 +549,7 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         for (size_t q = 0; q < J.pieces.size(); ++q) J.piece_start[q + 1] = J.piece_start[q] + J.pieces[q].len;
         J.piece_val.assign(J.pieces.size(), 0);
         H = std::min(H, J.pieces.size());
-        G = (int)std::min<size_t>((size_t)G, std::max<size_t>(1, (size_t)(total / kMinDevClaim)));  // tiny jobs: fewer lanes
+        if (G) G = (int)std::min<size_t>((size_t)G, std::max<size_t>(1, (size_t)(total / kMinDevClaim)));  // tiny jobs: fewer lanes
         // a hybrid job smaller than one slot finishes on the host threads before a lane's first copy
         // and launch would (tens of microseconds): no lane
         if (H > 0 && total < kSlotBytes) G = 0;

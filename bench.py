@@ -234,8 +234,10 @@ def pmc_traffic(alg, nbuf, L, batches_per_launch):
     return None
 
 
-def time_launches(eng, launch, st, nt):
-    """Mean dispatch duration (ms) of nt launches serialised on stream st behind a GPU-side hold."""
+def time_launches(eng, launch, st, nt, stamps=False):
+    """Mean dispatch duration (ms) of nt launches serialised on stream st behind a GPU-side hold.
+    stamps: launch(i, st, start_event, stop_event) stamps its own dispatch (the diagnostic library's
+    read-ceiling kernel); otherwise the engine's profiling hook stamps the next launch."""
     import torch
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
@@ -245,8 +247,11 @@ def time_launches(eng, launch, st, nt):
     for i in range(nt):
         starts[i].record(st)  # creates the events; the launch below re-stamps them
         ends[i].record(st)
-        eng.time_next_launch(starts[i], ends[i])
-        launch(i, st)
+        if stamps:
+            launch(i, st, starts[i], ends[i])
+        else:
+            eng.time_next_launch(starts[i], ends[i])
+            launch(i, st)
     torch.cuda.synchronize()
     durs = sorted(eng.event_ms(s_, e_) for s_, e_ in zip(starts, ends))
     return sum(durs) / nt, durs[nt // 2]
@@ -664,12 +669,15 @@ def main():
     # secondary denominator: the streaming-read ceiling of a one-batch launch and
     # of a launch of the timed region's size (the same bytes, read by an XOR-reduce kernel)
     if not args.no_read_ceiling and not args.only_coalesced:
-        rc_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, step_bytes, stream=st,
-                                                                     base_offset=(i % nb) * step_bytes), streams[0], nt)
+        rc_ms, _ = time_launches(eng, lambda i, st, e0, e1: eng.read_ceiling(data, step_bytes, stream=st,
+                                                                             base_offset=(i % nb) * step_bytes,
+                                                                             start_event=e0, stop_event=e1),
+                                 streams[0], nt, stamps=True)
         roof["single_batch"]["read_ceiling_kernel_ms"] = round(rc_ms, 5)
         roof["single_batch"]["read_ceiling_frac"] = roofline(step_bytes, rc_ms, "")["frac"]
-        rcg_ms, _ = time_launches(eng, lambda i, st: eng.read_ceiling(data, gsz * step_bytes, stream=st), streams[0],
-                                  max(2, nt // 4))
+        rcg_ms, _ = time_launches(eng, lambda i, st, e0, e1: eng.read_ceiling(data, gsz * step_bytes, stream=st,
+                                                                              start_event=e0, stop_event=e1),
+                                  streams[0], max(2, nt // 4), stamps=True)
         roof["read_ceiling"] = {"kernel_ms": round(rcg_ms, 5), "frac": roofline(gsz * step_bytes, rcg_ms, "")["frac"],
                                 "timing_launches": max(2, nt // 4),
                                 "scan_frac_of_ceiling": round(rcg_ms / kms, 4),

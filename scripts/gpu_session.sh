@@ -28,6 +28,7 @@ for s in "$@"; do
     probe) for v in "" "ROC_ACTIVE_WAIT_TIMEOUT=1000" "HIP_FORCE_DEV_KERNARG=0" "HIP_FORCE_DEV_KERNARG=1" "AMDCRC_PROBE_SCHED=spin" "AMDCRC_PROBE_SCHED=blocking"; do
              step 120 $O/probe.log.tmp env $v python -u aws-crt-cpp_amd/tools/overhead_probe.py 20 40; rc=$?; cat $O/probe.log.tmp >> $O/probe.log
              [ $rc -ne 0 ] && break; done; grep '^{' $O/probe.log | cut -c1-600 ;;
+    es)    step 180 $O/es.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames; rc=$?; grep '^{' $O/es.log | cut -c1-500 ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;

@@ -112,6 +112,11 @@ def test_release_library_has_no_diagnostics():
     syms = subprocess.run(["nm", "-C", LIB], capture_output=True, text=True, check=True).stdout
     for gone in ("crc32_stream8_kernel", "crc64_stream_kernel<", "debug_timeline"):
         assert gone not in syms, gone
+    # diagnostics (the read-ceiling kernel, test hooks) live only in the diagnostic build
+    dyn = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    for gone in ("aws_crt_amd_debug", "read_ceiling", "amdcrc_debug"):
+        assert gone not in dyn, gone
+    assert "read_ceiling_kernel" not in syms
     # the only getenv in the product selects the processor for host memory, never the arithmetic
     assert "AWS_CRT_AMD_DISPATCH" in strings
 

@@ -32,7 +32,8 @@ def test_host_job_without_device_uses_host_path():
     if eng.device_count() > 0:
         pytest.skip("device present: covered by the gpu tests")
     rng = random.Random(21)
-    bufs = _bufs(rng, [0, 1, 100, 4096, 70000, 1 << 20])
+    # buffers past a piece (8 MiB) are cut, spread over the host threads and joined with Combine
+    bufs = _bufs(rng, [0, 1, 100, 4096, 70000, 1 << 20, (8 << 20) + 5, (17 << 20) + 3, 8 << 20])
     for alg in ALG:
         seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in bufs]
         got = eng.host_job(ALG[alg], [_addr(b) for b in bufs], [b.size for b in bufs], seeds)
