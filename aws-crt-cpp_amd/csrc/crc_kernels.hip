@@ -1724,7 +1724,11 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         ga = g;
         u = 0;
         if (g == 0) {
+#ifdef AMDCRC_XP_LIST_NOHEAD  // experiment builds only (timing; results wrong): no head fold, no seed read
+            uint32_t s_h = ~0u;
+#else
             uint32_t s_h = head_state<true>(p, sc.b, eng);
+#endif
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
@@ -1732,6 +1736,10 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     };
     // the part [ga, g) ends: its share, moved to the buffer's end, finishes the buffer or joins it
     auto part_finish = [&]() {
+#ifdef AMDCRC_XP_LIST_NOFINISH  // experiment builds only (timing; results wrong): a part stores its lane-0 braid
+        if (lane == 0) asm volatile("global_store_dword %0, %1, off" : : "v"((uint32_t *)p.d_out + sc.b), "v"(u) : "memory");
+        return;
+#endif
         uint32_t r = wave_xor_s(eng.mulK(u, lane));
         for (uint32_t m = sc.vg - g, i = 0; m; m >>= 1, ++i)
             if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);

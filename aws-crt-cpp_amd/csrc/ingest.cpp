@@ -515,7 +515,7 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         for (size_t i = 0; h_seeds && i < count; ++i)
             J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
         const int vis = visible_devices();
-        int G = ndevices <= 0 ? vis : std::min(ndevices, vis);
+        int G = ndevices < 0 ? 0 : ndevices == 0 ? vis : std::min(ndevices, vis);  // < 0: the host path only
         if (is_crc(alg) && G > 0 && !amdcrc_gpu_usable()) {
             amdcrc_note_fallback();  // a visible device the engine cannot use (not gfx950, HIP error)
             G = 0;

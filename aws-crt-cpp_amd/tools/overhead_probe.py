@@ -56,16 +56,18 @@ def main(nbatch=20, reps=40):
                    ctypes.c_size_t, ctypes.c_void_p]
     sh = st.cuda_stream
     paths = {"batches": lambda: fn(eng.CRC32C, arr, nbatch, L, L, count, sh),
-             "plan": lambda: plan.fn(plan._plan, sh)}
+             "plan": lambda: plan.fn(plan._plan, sh),
+             "batchset_run": lambda: plan.run(st)}  # bench.py's call: the plan plus record_stream
     for f in paths.values():
         for _ in range(3):
             f()
     torch.cuda.synchronize()
     res = {"env": {k: os.environ[k] for k in sorted(os.environ) if k.startswith(("ROC_", "HIP_", "HSA_", "DEBUG_CLR", "AMDCRC_"))},
            "sched_rc": sched_rc}
-    for name, f in paths.items():
-        call, wall, outside, kern, wall_plain = [], [], [], [], []
-        for _ in range(reps):
+    acc = {name: ([], [], [], [], []) for name in paths}
+    for _ in range(reps):  # the paths interleaved rep by rep (clock and box drift hit both alike)
+        for name, f in paths.items():
+            call, wall, outside, kern, wall_plain = acc[name]
             # as bench.py's timed region: no events on the launch
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -88,6 +90,8 @@ def main(nbatch=20, reps=40):
             wall.append((t2 - t0) * 1e6)
             kern.append(k)
             outside.append((t2 - t0) * 1e6 - k)
+    for name in paths:
+        call, wall, outside, kern, wall_plain = acc[name]
         med = lambda v: round(statistics.median(v), 2)  # noqa: E731
         res[name] = {"host_call_us": med(call), "wall_us": med(wall_plain), "wall_min_us": round(min(wall_plain), 2),
                      "gibs_median": round(nbatch * step / (statistics.median(wall_plain) * 1e-6) / 2**30, 1),

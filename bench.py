@@ -136,9 +136,11 @@ def cpu_share():
     return threads, topo, limit
 
 
-def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
+def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5, step_buffers=None):
     """Engine host path (kind "port") on a bounded sample: `count` buffers of L bytes from `host`
-    (numpy), 1 thread and the box's CPU share, median of `reps` reps of >= rep_seconds each."""
+    (numpy), 1 thread and the box's CPU share, median of `reps` reps of >= rep_seconds each.
+    gpu_results: the GPU's results for the first buffers.  step_buffers: also time the first
+    step_buffers buffers alone (one step, which may sit in the host's last-level cache) beside it."""
     from oracle import oracle  # checker and secondary figure only
 
     threads, topo, limit = cpu_share()
@@ -146,7 +148,7 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
     ptrs = [base + i * L for i in range(count)]
     lens = [L] * count
     first = eng.cpu_batch(ALG[alg], ptrs, lens, threads=threads)
-    parity = first == gpu_results[:count]
+    parity = first[:len(gpu_results)] == gpu_results[:count]
 
     def rate(fn, nbytes):
         fn()  # warm-up
@@ -162,7 +164,7 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
             rs.append(passes * nbytes / el / 2**30)
         return statistics.median(rs)
 
-    n1 = max(1, min(count, (64 << 20) // L))
+    n1 = count  # the same sample on one thread
     # argument arrays prepared once: the timed calls are the C calls alone
     many, one = eng.CpuBatch(ALG[alg], ptrs, lens, threads=threads), eng.CpuBatch(ALG[alg], ptrs[:n1], lens[:n1], threads=1)
     v = rate(many.run, count * L)
@@ -170,7 +172,11 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
     ov = None
     if alg in oracle.ALG_INDEX:
         ov = rate(oracle.prepared_batch(alg, ptrs, lens, threads), count * L)
-    third = third_party_rates(alg, host, count, L, threads, gpu_results, rate)
+    cached = None
+    if step_buffers and step_buffers < count:
+        cached = round(rate(eng.CpuBatch(ALG[alg], ptrs[:step_buffers], lens[:step_buffers], threads=threads).run,
+                            step_buffers * L), 2)
+    third = third_party_rates(alg, host, min(count, len(gpu_results)), L, threads, gpu_results, rate)
     hashed = alg in ("xxh64", "xxh3_64", "xxh3_128")
     busy = min(threads, count) if hashed else threads
     return {"value": round(v, 2), "unit": "GiB/s", "cores": busy, "kind": "port",
@@ -180,6 +186,7 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5):
                       + ("(one per buffer: a hash is one serial chain)" if hashed else
                          "(buffers cut into >= 1 MiB pieces folded with Combine, so every thread is busy)"),
             "threads_limit": limit, "single_thread_gibs": round(v1, 2), "topology": topo,
+            "one_step_gibs": cached,
             "oracle_hw_tier_gibs": round(ov, 2) if ov is not None else None, "parity_with_gpu": parity,
             "third_party": third}
 
@@ -297,12 +304,13 @@ def kernel_name(alg, nbuf, L):
 
 def ingest_rates(eng, alg_id, ptrs, lens, reps=3):
     """One host-ingest job over host buffers, hybrid (the CPU share's threads beside the device lane,
-    aws_crt_amd_host_submit's default) and devices only (the PCIe-bound pipeline): GiB/s (best of
-    `reps` after a warm-up), the devices' share of the bytes, and the hybrid job's results."""
+    aws_crt_amd_host_submit's default), devices only (the PCIe-bound pipeline) and the host path alone
+    on the same bytes (no offload): GiB/s (best of `reps` after a warm-up), the devices' share of the
+    bytes, and the hybrid job's results."""
     nbytes = sum(lens)
     out = {}
-    for name, ht in (("hybrid", -1), ("devices_only", 0)):
-        job = eng.HostJob(alg_id, ptrs, lens, host_threads=ht)
+    for name, nd, ht in (("hybrid", 0, -1), ("devices_only", 0, 0), ("host_only", -1, -1)):
+        job = eng.HostJob(alg_id, ptrs, lens, ndevices=nd, host_threads=ht)
         job.run()  # warm-up: device lanes, the first DMA touch of the pinned pages
         best = None
         for _ in range(reps):
@@ -314,7 +322,8 @@ def ingest_rates(eng, alg_id, ptrs, lens, reps=3):
         if ht < 0:
             out["results"] = job.results()
     return {"value": out["hybrid"]["gibs"], "unit": "GiB/s", "device_share": out["hybrid"]["device_share"],
-            "devices_only_gibs": out["devices_only"]["gibs"], "results": out["results"],
+            "devices_only_gibs": out["devices_only"]["gibs"], "host_only_gibs": out["host_only"]["gibs"],
+            "results": out["results"],
             "api": "aws_crt_amd_host_submit (hybrid: host threads + device lane) + aws_crt_amd_job_wait"}
 
 
@@ -699,9 +708,13 @@ def main():
     configs = {}
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
+            # the sample: every resident batch (as many bytes as the timed region streams, more than
+            # the host's last-level cache, as the GPU's reads are beyond its caches), with one step
+            # alone (cache-resident on the host) reported beside it
             torch.cuda.synchronize()
-            host = data[:step_bytes].cpu().numpy()
-            cpu = cpu_baseline(eng, alg, host, count, L, eng.as_unsigned(outs[0]), args.cpu_seconds)
+            host = data[:nb * step_bytes].cpu().numpy()
+            cpu = cpu_baseline(eng, alg, host, nb * count, L, eng.as_unsigned(outs[0]), args.cpu_seconds,
+                               step_buffers=count)
         if args.e2e_batches > 0:
             e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
         if not args.no_configs:

@@ -317,9 +317,10 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(
     int ndevices,
     struct aws_crt_amd_job **job);
 /*
- * aws_crt_amd_host_submit with options.  host_threads: -1 = the CPU share less one thread per device
- * lane (what aws_crt_amd_host_submit does), 0 = devices only (the PCIe-bound pipeline), n = n host
- * threads beside the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the
+ * aws_crt_amd_host_submit with options.  ndevices: 0 = every visible device, n = the first n, < 0 =
+ * none (the host path alone, on the CPU share).  host_threads: -1 = the CPU share less one thread per
+ * device lane (what aws_crt_amd_host_submit does), 0 = devices only (the PCIe-bound pipeline), n = n
+ * host threads beside the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the
  * devices checksummed.
  */
 struct aws_crt_amd_ingest_options {

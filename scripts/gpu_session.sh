@@ -25,10 +25,14 @@ for s in "$@"; do
     prof)  (cd /tmp && step 300 $O/prof.log rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $P ${PROF_ARGS:-}); rc=$? ;;
     pmc)   (cd /tmp && step 120 $O/pmc_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $R/bench.py $P ${PROF_ARGS:-}); rc=$? ;;
     # the driver-shaped region per submission path, under HIP runtime settings (one process each)
-    probe) for v in "" "ROC_ACTIVE_WAIT_TIMEOUT=1000" "HIP_FORCE_DEV_KERNARG=0" "HIP_FORCE_DEV_KERNARG=1" "AMDCRC_PROBE_SCHED=spin" "AMDCRC_PROBE_SCHED=blocking"; do
+    probe) for v in ${PROBE_ENVS:-""}; do
              step 120 $O/probe.log.tmp env $v python -u aws-crt-cpp_amd/tools/overhead_probe.py 20 40; rc=$?; cat $O/probe.log.tmp >> $O/probe.log
              [ $rc -ne 0 ] && break; done; grep '^{' $O/probe.log | cut -c1-600 ;;
     es)    step 180 $O/es.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames; rc=$?; grep '^{' $O/es.log | cut -c1-500 ;;
+    # SQ issue / stall / LDS counters of the event-stream framing kernel (one pass)
+    sqes)  (cd /tmp && step 120 $O/sqes.log timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/sqes -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames --steps 12 --timing-launches 4); rc=$? ;;
+    sqes2) (cd /tmp && step 120 $O/sqes2.log timeout -s KILL 100 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES TCP_TCC_READ_REQ_sum TA_BUSY_avr GRBM_GUI_ACTIVE -d $O/sqes2 -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames --steps 12 --timing-launches 4); rc=$? ;;
+    ablist) step 900 $O/ablist.log env TAG=${TAG}/ablist VARIANTS="${VARIANTS:-A B C D}" REPS=${REPS:-2} bash scripts/ab_listprobe.sh; rc=$?; cat $O/ablist.log ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;
