@@ -1321,6 +1321,31 @@ __device__ __forceinline__ void stream_finish(const ScanParams &p, const Tile &d
     acc.val ^= (unsigned long long)v | (1ull << (32 + (d.k & 31)));
 }
 
+// XCD-window order (ScanParams::xcd_order): tile d of a buffer of T <= WAVES tiles, all scanned at the
+// same step by consecutive waves of this workgroup; its share moved to the buffer end joins LDS slot
+// `slot` (value XOR, one arrival bit per tile), and the tile completing the slot finishes the buffer.
+template <class B>
+__device__ __forceinline__ void stream_finish_xcd(const ScanParams &p, const Tile &d, uint32_t u, const B &eng, int lane,
+                                                  uint32_t slot) {
+    uint32_t r = wave_xor_s(eng.mulK(u, lane));
+    if (d.T == 1) {
+        if (lane == 0) finalize<false>(p, d.b, r, eng);
+        return;
+    }
+    const uint32_t m = (uint32_t)(d.T - 1 - d.k);
+    if (m) {
+        const uint32_t colv = lds32(eng.cbase(), (kPcolOff - kBKOff) + 4 * (m * 32 + (lane & 31)));
+        const uint32_t sel = lane < 32 ? (uint32_t)__builtin_amdgcn_sbfe((int)r, 31 - lane, 1) : 0u;
+        r = wave_xor_s(colv & sel);
+    }
+    if (lane == 0) {
+        const unsigned long long add = (unsigned long long)r | (1ull << (32 + d.k));
+        unsigned long long *sl = (unsigned long long *)(eng.cbase() + (kLocalOff - kBKOff)) + slot;
+        const unsigned long long now = __hip_atomic_fetch_xor(sl, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ^ add;
+        if ((now & 0xFFFFFFFF00000000ull) == (((1ull << d.T) - 1) << 32)) finalize<false>(p, d.b, (uint32_t)now, eng);
+    }
+}
+
 // Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
 // WB = bytes per lane word: 8 (512-thread workgroups, 64 KiB of tables, two per CU) or 16 (one
 // 1024-thread workgroup per CU, 128 KiB of tables); 4 remains as the AMDCRC_STREAM_W8=0 build.
@@ -1355,10 +1380,25 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
     const uint32_t voff = (uint32_t)WB * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    // the wave's tiles: t0, t0 + tstep, ... (ntw of them).  XCD windows (p.xcd_order): the waves of XCD
+    // x = blockIdx mod 8 take tiles j, j + nwx, ... of the x-th eighth, so at every step an XCD's waves
+    // read one compact window (DESIGN.md "Read order"); a buffer's T tiles go to T consecutive waves of
+    // one workgroup at the same step, combined in the workgroup's LDS slots (slot = step * WAVES / T +
+    // wave / T).  Otherwise each wave takes a contiguous range.
+    const bool xo = WB == 8 && p.xcd_order != 0;
+    uint64_t t0, tstep = 1, ntw;
+    if (xo) {
+        const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * p.ntiles / 8, xhi = (xcd + 1) * p.ntiles / 8;
+        t0 = rfl64(xlo + (uint64_t)(blockIdx.x >> 3) * WAVES + wv);
+        tstep = nwx;
+        ntw = rfl64(t0 < xhi ? (xhi - t0 + nwx - 1) / nwx : 0);
+    } else {
+        t0 = rfl64(gw * p.ntiles / nw);
+        ntw = rfl64((gw + 1) * p.ntiles / nw) - t0;
+    }
     const uint32_t gsh = __builtin_ctz(G);
-    const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
-    const bool work = t0 < t1;
+    const uint32_t nq = (uint32_t)(ntw << gsh);  // groups of this wave
+    const bool work = ntw > 0;
     // prefetch cursor: the next group to issue, as (buffer, tile, group); fbuf is the main-region
     // address of buffer fb, which walks batch by batch (fj, fi)
     uint32_t fq = 0;  // groups issued
@@ -1366,6 +1406,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     uint32_t fg = 0;
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
+    uint64_t ft = t0;  // XCD windows: the tile being issued
     auto f_addr = [&]() -> uint64_t {
         uint64_t a = fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
         if (!AMDCRC_GUARD_OK(fq >= nq || p.nbatch > 1 || (a >= p.base + hoff && a + kBraidRow * kBraidRowsPerGroup <=
@@ -1378,7 +1419,14 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         ++fq;
         if (++fg == G) {
             fg = 0;
-            if (++fk == T) {
+            if (xo) {  // the wave's next tile is tstep tiles on
+                ft += tstep;
+                if (fq < nq) {
+                    fb = ft / T, fk = ft - fb * T;
+                    fpos = batch_pos(p, fb);
+                    fbuf = karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff;
+                }
+            } else if (++fk == T) {
                 fk = 0, ++fb;
                 if (++fpos.i == p.bcount && fq < nq) {
                     fpos.i = 0, ++fpos.j;
@@ -1492,6 +1540,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     d.ngroups = G;
     uint32_t g = 0, u = 0;
     uint32_t q = 0;  // groups scanned
+    uint64_t st_t = t0, st_n = 0;  // XCD windows: the tile being scanned, tiles finished
     BGroupAcc acc{};
     acc.slot = ~0ull;
     auto step = [&](Grp &cur, Grp &nxt, bool first) {
@@ -1504,8 +1553,15 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         if (++g == G) {
             g = 0;
             await_consts();
-            stream_finish(p, d, u, eng, lane, acc, lb);
-            if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
+            if (xo) {
+                stream_finish_xcd(p, d, u, eng, lane, (uint32_t)(st_n * (WAVES / T) + wv / T));
+                ++st_n;
+                st_t += tstep;
+                d.b = st_t / T, d.k = st_t - d.b * T, d.tbase = d.b * T;
+            } else {
+                stream_finish(p, d, u, eng, lane, acc, lb);
+                if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
+            }
         }
     };
     // the first step is peeled (it publishes the constants, whose loads are then out of the loop),
@@ -3503,6 +3559,11 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
+#ifndef AMDCRC_ES_QUAD  // compile-time only (A/B builds): 0 keeps the one-lane-per-message kernel
+#define AMDCRC_ES_QUAD 1
+#endif
+
+#if !AMDCRC_ES_QUAD
 __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
     __shared__ uint32_t tab[8][256];
     lane_tables<uint32_t, kPoly32>(tab);
@@ -3527,6 +3588,7 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
     p.d_message_crc[m] = msg;
     p.d_status[m] = st;
 }
+#endif  // !AMDCRC_ES_QUAD
 
 }  // namespace
 
@@ -3686,10 +3748,123 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
     return (int)hipGetLastError();
 }
 
+// Event-stream framing check, four lanes per message (round 4; tests/test_eventstream_quad_model.py
+// restates it against zlib).  One lane per message read 64 messages per wave load -- 64 cache lines
+// per instruction, 16 bytes from each -- and a wave ran as long as the longest of its 64 messages
+// (profiles/r04: the software-pipelined form of that kernel still took 28.9 us per 65 MiB call, frac
+// 0.29).  Here a quad owns a message: lane j folds the body's words at 32 r + 8 j (r = row) with a
+// slice-by-8 step whose tables T'_t = T_(t+24) also skip the quad's other 24 bytes of the row; lane j's
+// share of the register is u_j * x^(-64 j) (byte tables per lane class), the quad XORs the shares, and
+// the last (body mod 32) bytes follow on the plain slice-by-8 path.  A wave load instruction reads 16
+// messages x 32 contiguous bytes, and a wave lasts as long as the longest of 16 messages at a quarter
+// of the steps.  Bodies start at any alignment: each lane reads the two aligned words around its word
+// (only when the message is unaligned), never past the aligned word holding the message's last byte.
+constexpr uint32_t kEsSkip = 24;  // bytes of a 32-byte row after a lane's word
+
+struct EsShareCols {  // column b of x^(-64 j), j = 1..3: (1 << b) * K_j
+    uint32_t c[3][32];
+    constexpr EsShareCols() : c() {
+        for (int j = 1; j <= 3; ++j) {
+            uint32_t k = 0x80000000u;  // x^0
+            for (int i = 0; i < 64 * j; ++i) k = (k & 0x80000000u) ? (((k ^ kPoly32) << 1) | 1u) : (k << 1);  // * x^-1
+            for (int b = 0; b < 32; ++b) c[j - 1][b] = (uint32_t)gf2_mulmod(1ull << b, k, kPoly32, 32);
+        }
+    }
+};
+
+__device__ __forceinline__ uint64_t es_word(const uint64_t *a, uint32_t o) {  // 8 bytes at (uint8*)a + o
+    const uint64_t lo = a[0];
+    if (!o) return lo;
+    const uint64_t hi = a[1];
+    return (lo >> (8 * o)) | (hi << (64 - 8 * o));
+}
+
+__global__ __launch_bounds__(256) void eventstream_quad_kernel(const EventStreamParams p) {
+    __shared__ uint32_t sd[8][256];     // standard slice-by-8 (prelude, tail)
+    __shared__ uint32_t tp[8][256];     // T'_t = T_(t+24): the row step
+    __shared__ uint32_t mj[3][4][256];  // lane shares of classes 1..3: (e << 8k) * x^(-64 j)
+    {
+        const uint32_t e = threadIdx.x;
+        uint32_t c = e;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? kPoly32 : 0u);
+        sd[0][e] = c;
+        __syncthreads();
+        for (int t = 1; t < 8 + (int)kEsSkip; ++t) {  // c = T_t[e] = e * x^(8(t+1))
+            c = (c >> 8) ^ sd[0][c & 0xff];
+            if (t < 8) sd[t][e] = c;
+            if (t >= (int)kEsSkip) tp[t - kEsSkip][e] = c;
+        }
+        constexpr EsShareCols C{};
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? C.c[j][8 * k + i] : 0u;
+                mj[j][k][e] = v;
+            }
+        __syncthreads();
+    }
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = gid >> 2;
+    const uint32_t j = (uint32_t)gid & 3u;
+    if (m >= p.count) return;  // whole quads: count messages x 4 lanes
+    const uint64_t off = p.d_offsets[m];
+    uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
+    if (off <= p.limit && p.limit - off >= 16) {
+        const uint8_t *q = p.base + off;
+        const uint64_t total = be32(q), headers = be32(q + 4);
+        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
+            const uint32_t s8 = lane_scan<uint32_t>(~0u, q, 8, sd);  // the prelude's register
+            pre = ~s8;
+            const uint8_t *body = q + 8;
+            const uint64_t nb = total - 12, R = nb >> 5;
+            const uint32_t o = (uint32_t)((uintptr_t)body & 7u);
+            const uint64_t *a = (const uint64_t *)((uintptr_t)body - o) + j;  // this lane's aligned word of row 0
+            uint32_t s = s8;
+            if (R) {
+                uint32_t u = 0;
+                uint64_t w = es_word(a, o);
+                if (j == 0) w ^= s8;  // the prelude state enters lane 0's first word
+                for (uint64_t r = 1; r < R; ++r) {
+                    const uint64_t wn = es_word(a + 4 * r, o);  // next row's word, in flight during this step
+                    u = lane_word<uint32_t>(u, w, tp);
+                    w = wn;
+                }
+                u = lane_word<uint32_t>(u, w, tp);
+                // lane j's share u * x^(-64 j), then the quad's XOR
+                uint32_t sh = u;
+                if (j) {
+                    const uint32_t (*t)[256] = mj[j - 1];
+                    sh = t[0][u & 0xff] ^ t[1][(u >> 8) & 0xff] ^ t[2][(u >> 16) & 0xff] ^ t[3][u >> 24];
+                }
+                sh ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sh, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+                sh ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sh, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+                s = sh;
+            }
+            s = lane_scan<uint32_t>(s, body + 32 * R, nb - 32 * R, sd);  // the last (body mod 32) bytes
+            msg = ~s;
+            st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
+        }
+    }
+    if (j == 0) {
+        p.d_prelude_crc[m] = pre;
+        p.d_message_crc[m] = msg;
+        p.d_status[m] = st;
+    }
+}
+
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
+    if (p->count == 0) return 0;
+#if AMDCRC_ES_QUAD
+    const uint64_t blocks = (p->count * 4 + 255) / 256;
+    launch(eventstream_quad_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
+#else
     const uint64_t blocks = (p->count + 255) / 256;
-    if (blocks == 0) return 0;
     launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
+#endif
     return (int)hipGetLastError();
 }
 

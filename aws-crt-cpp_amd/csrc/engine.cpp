@@ -510,6 +510,16 @@ constexpr uint64_t kXcdMinChunks = AMDCRC_XCD_MIN_CHUNKS;
 #ifndef AMDCRC_XP_STREAM64  // experiment: 0 sends aligned strided CRC64NVME batches to crc64_braid_kernel
 #define AMDCRC_XP_STREAM64 1
 #endif
+// W=32 streaming scans in XCD-window tile order (16 KiB tiles)
+#ifndef AMDCRC_STREAM_XCD  // compile-time only (A/B builds)
+#define AMDCRC_STREAM_XCD 0
+#endif
+constexpr bool kStreamXcd = AMDCRC_STREAM_XCD != 0;
+constexpr uint64_t kXoTile = 16384;
+#ifndef AMDCRC_STREAM_XCD_MIN  // smallest launch (main bytes) taking the XCD-window order
+#define AMDCRC_STREAM_XCD_MIN 0
+#endif
+constexpr uint64_t kXoMinBytes = AMDCRC_STREAM_XCD_MIN;
 constexpr uint64_t kRows16MinBuffers = 4 * 4096;
 constexpr uint64_t kRows16MaxBytes = 256u << 10;
 // Ragged lists whose buffers are all at most this long take the lane-per-buffer scan
@@ -947,6 +957,24 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     // large W=32 launches: 16-byte lane words in one 1024-thread workgroup per CU (the same waves per
     // CU as two 512-thread workgroups; the tiles hold 4 KiB groups either way)
     if (p.stream && w32 && kStreamW16 && !small) p.stream = 2;
+    // XCD-window tile order (crc32_stream_kernel, ScanParams::xcd_order): buffers of 1, 2, 4 or 8 tiles
+    // of 16 KiB; every XCD eighth a whole number of buffers; each wave's tile count within the LDS slots
+    if (kStreamXcd && w32 && !kStreamW16 && ml > 0 && ml % kXoTile == 0 && ml / kXoTile <= 8 &&
+        ((ml / kXoTile) & (ml / kXoTile - 1)) == 0 && (kXoMinBytes == 0 || ml * count >= kXoMinBytes)) {
+        const uint64_t To = ml / kXoTile, nt = To * count;
+        const ScanGeometry geo = scan_geometry(d, alg, nt, ml * count);
+        const uint64_t nwx = geo.blocks * geo.waves_per_block / 8;
+        const uint64_t rounds = nwx ? (nt / 8 + nwx - 1) / nwx : 0;
+        if (geo.blocks % 8 == 0 && geo.waves_per_block == 8 && nt % (8 * To) == 0 && rounds * (8 / To) <= 128) {
+            p.seg = (uint32_t)(kXoTile / kWave);
+            p.stream = 1;
+            p.tiles_per_buf = To;
+            p.ntiles = nt;
+            p.nstatic = 0;
+            p.xcd_order = 1;
+            return launch_scan(d, alg, p, count, To, ml * count, s);
+        }
+    }
     if (pool && !p.stream) {
         // workgroup pools need every wave to own a static tile: ntiles / blocks >= waves per block
         const ScanGeometry geo = scan_geometry(d, alg, p.ntiles, ml * count);

@@ -94,6 +94,11 @@ struct ScanParams {
     uint64_t nstatic;               // 0: no dynamic pool (every tile static)
     uint64_t dyn_chunk;             // pool tiles per shard
     unsigned int *d_claim;          // 2 words per shard, zero on entry, left zero on exit
+    // ---- crc32_stream_kernel tile order (round 4): 0 = each wave a contiguous range of tiles; 1 = XCD
+    // windows: the waves of XCD x (blockIdx mod 8) take tiles j, j + nwx, ... of the x-th eighth, a
+    // buffer's T <= WAVES tiles falling to consecutive waves of one workgroup (combined in LDS)
+    uint32_t xcd_order;
+    uint32_t reserved0;
 };
 
 // W=32 braided scan constants (engine.cpp get_braid_consts), u32 words:

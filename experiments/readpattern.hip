@@ -166,11 +166,11 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&buf, bytes * 2));
     CK(hipMalloc(&out, 1 << 20));
     CK(hipMemset(buf, 0x5a, bytes * 2));
+    // round 4: the orders a 64 KiB-buffer CRC32 scan could take (whole buffers per wave step: C, V16;
+    // 16 KiB quarters combined in the workgroup: V4) against the best (X)
     std::vector<Variant> vs = {
-        {"C S3 x2", readp<'C', 1, 3>, 2}, {"I S3 x2", readp<'I', 1, 3>, 2}, {"X S3 x2", readp<'X', 1, 3>, 2},
-        {"K16 S3 x2", readp<'K', 16, 3>, 2}, {"K4 S3 x2", readp<'K', 4, 3>, 2},
-        {"R S3 x2", readr<'R', 1, 3>, 2}, {"Q64 S3 x2", readr<'Q', 64, 3>, 2}, {"Q32 S3 x2", readr<'Q', 32, 3>, 2},
-        {"U64 S3 x2", readr<'U', 64, 3>, 2}, {"R S3 x1", readr<'R', 1, 3>, 1}, {"Q64 S3 x1", readr<'Q', 64, 3>, 1},
+        {"C S3 x2", readp<'C', 1, 3>, 2}, {"X S3 x2", readp<'X', 1, 3>, 2}, {"V4 S3 x2", readp<'V', 4, 3>, 2},
+        {"V16 S3 x2", readp<'V', 16, 3>, 2}, {"V8 S3 x2", readp<'V', 8, 3>, 2},
     };
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

@@ -33,6 +33,13 @@ for s in "$@"; do
     sqes)  (cd /tmp && step 120 $O/sqes.log timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/sqes -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames --steps 12 --timing-launches 4); rc=$? ;;
     sqes2) (cd /tmp && step 120 $O/sqes2.log timeout -s KILL 100 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES TCP_TCC_READ_REQ_sum TA_BUSY_avr GRBM_GUI_ACTIVE -d $O/sqes2 -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames --steps 12 --timing-launches 4); rc=$? ;;
     ablist) step 900 $O/ablist.log env TAG=${TAG}/ablist VARIANTS="${VARIANTS:-A B C D}" REPS=${REPS:-2} bash scripts/ab_listprobe.sh; rc=$?; cat $O/ablist.log ;;
+    readpat) step 150 $O/readpat.log bash -c "experiments/build/readpattern 1280 16 && experiments/build/readpattern 512 16"; rc=$?; cat $O/readpat.log ;;
+    # A/B of library builds on the driver-shaped bench (ab/lib$v.so for v in $VARIANTS)
+    abx)   step 900 $O/abx.log env TAG=${TAG}/abx VARIANTS="${XVARIANTS:-R X}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/abx.log ;;
+    # the GPU parity tests that cover the uniform-batch scans, on variant $XLIB (then the release build back)
+    xtests) cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/librel.so && cp ab/lib${XLIB:-X}.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so &&
+            step 600 $O/xtests.log python -u -m pytest tests/test_gpu_parity.py tests/test_queue.py tests/test_multipart.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?;
+            cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so; tail -3 $O/xtests.log ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;
