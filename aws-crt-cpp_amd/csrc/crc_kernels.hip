@@ -1358,7 +1358,7 @@ struct StreamShape {
     static constexpr int kKWord = WB == 16 ? kBraidK128Word : WB == 8 ? kBraidK64Word : 0;
 };
 
-template <uint32_t POLY, int WB>
+template <uint32_t POLY, int WB, bool XO = false>
 __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kernel(const ScanParams p) {
     using SS = StreamShape<WB>;
     using B = typename std::conditional<WB == 16, Braid32W16<POLY>,
@@ -1385,9 +1385,9 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // read one compact window (DESIGN.md "Read order"); a buffer's T tiles go to T consecutive waves of
     // one workgroup at the same step, combined in the workgroup's LDS slots (slot = step * WAVES / T +
     // wave / T).  Otherwise each wave takes a contiguous range.
-    const bool xo = WB == 8 && p.xcd_order != 0;
+    constexpr bool xo = WB == 8 && XO;  // a separate instantiation: the contiguous split's loop is unchanged
     uint64_t t0, tstep = 1, ntw;
-    if (xo) {
+    if constexpr (xo) {
         const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * p.ntiles / 8, xhi = (xcd + 1) * p.ntiles / 8;
         t0 = rfl64(xlo + (uint64_t)(blockIdx.x >> 3) * WAVES + wv);
         tstep = nwx;
@@ -1419,7 +1419,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         ++fq;
         if (++fg == G) {
             fg = 0;
-            if (xo) {  // the wave's next tile is tstep tiles on
+            if constexpr (xo) {  // the wave's next tile is tstep tiles on
                 ft += tstep;
                 if (fq < nq) {
                     fb = ft / T, fk = ft - fb * T;
@@ -1553,7 +1553,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         if (++g == G) {
             g = 0;
             await_consts();
-            if (xo) {
+            if constexpr (xo) {
                 stream_finish_xcd(p, d, u, eng, lane, (uint32_t)(st_n * (WAVES / T) + wv / T));
                 ++st_n;
                 st_t += tstep;
@@ -3560,7 +3560,7 @@ __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
 #ifndef AMDCRC_ES_QUAD  // compile-time only (A/B builds): 0 keeps the one-lane-per-message kernel
-#define AMDCRC_ES_QUAD 1
+#define AMDCRC_ES_QUAD 0
 #endif
 
 #if !AMDCRC_ES_QUAD
@@ -3691,7 +3691,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             else
 #endif
             if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
+                p->xcd_order ? launch(crc32_stream_kernel<kPoly32, 8, true>, nblocks, kBraidBlock, s, p, ev)
+                             : launch(crc32_stream_kernel<kPoly32, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list && p->stream == 4)
                 launch(crc32_list_stream_kernel<kPoly32>, nblocks, kBraidBlock, s, p, ev);
             else if (list)
@@ -3706,7 +3707,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             else
 #endif
             if (p->stream && !list)
-                launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
+                p->xcd_order ? launch(crc32_stream_kernel<kPoly32C, 8, true>, nblocks, kBraidBlock, s, p, ev)
+                             : launch(crc32_stream_kernel<kPoly32C, AMDCRC_STREAM_W8 ? 8 : 4>, nblocks, kBraidBlock, s, p, ev);
             else if (list && p->stream == 4)
                 launch(crc32_list_stream_kernel<kPoly32C>, nblocks, kBraidBlock, s, p, ev);
             else if (list)

@@ -515,7 +515,10 @@ constexpr uint64_t kXcdMinChunks = AMDCRC_XCD_MIN_CHUNKS;
 #define AMDCRC_STREAM_XCD 0
 #endif
 constexpr bool kStreamXcd = AMDCRC_STREAM_XCD != 0;
-constexpr uint64_t kXoTile = 16384;
+#ifndef AMDCRC_STREAM_XCD_TILE  // tile bytes of the XCD-window order (A/B builds)
+#define AMDCRC_STREAM_XCD_TILE 16384
+#endif
+constexpr uint64_t kXoTile = AMDCRC_STREAM_XCD_TILE;
 #ifndef AMDCRC_STREAM_XCD_MIN  // smallest launch (main bytes) taking the XCD-window order
 #define AMDCRC_STREAM_XCD_MIN 0
 #endif

@@ -5,6 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${TAG:-ab}; mkdir -p $O
+cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/ab_release.so  # put back at the end
 for r in $(seq 1 ${REPS:-3}); do
   for v in ${VARIANTS:-A B}; do
     cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so || exit 1
@@ -12,4 +13,4 @@ for r in $(seq 1 ${REPS:-3}); do
     echo "$v $r $(grep '^{' $O/${v}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.readline()); print(d["value"], d["roofline"]["frac"], d["roofline"]["kernel_ms"])')"
   done
 done
-cp ab/libA.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so
+cp /tmp/ab_release.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so

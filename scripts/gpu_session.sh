@@ -40,6 +40,12 @@ for s in "$@"; do
     xtests) cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/librel.so && cp ab/lib${XLIB:-X}.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so &&
             step 600 $O/xtests.log python -u -m pytest tests/test_gpu_parity.py tests/test_queue.py tests/test_multipart.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?;
             cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so; tail -3 $O/xtests.log ;;
+    # event-stream bench on library variants (ab/lib$v.so, v in $ESVARIANTS), then the release build back
+    abes)  cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/librel.so; rc=0
+           for v in ${ESVARIANTS:-R Q}; do for r in 1 2; do cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so &&
+             step 180 $O/abes_${v}_$r.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames || { rc=$?; break 2; }
+             echo "$v $r $(grep '^{' $O/abes_${v}_$r.log | cut -c180-420)"; done; done
+           cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;
