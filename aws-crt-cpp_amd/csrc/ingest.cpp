@@ -18,8 +18,8 @@
 // Hybrid jobs (round 4, the default): the data starts in host memory, where the host path checksums
 // it at 20-45 GiB/s per core while one device lane is bound by PCIe (~50 GiB/s).  So the CPU share's
 // threads and the device lanes both take pieces from one cursor over the job (work stealing by
-// claims of contiguous pieces): a device claims about its share of what is left (its PCIe rate
-// against the host threads'), a host thread a run of about 1 MiB.  Offloading is then never slower
+// claims of contiguous pieces): a device claims a slot's part of its share of what is left (its PCIe
+// rate against the host threads'), a host thread a run of about 1 MiB.  Offloading is then never slower
 // than the host path alone, and the devices add their PCIe rate on top.
 //
 // Device-resident lists spanning several devices (aws_crt_amd_checksum_list_devices) are grouped by
@@ -212,14 +212,16 @@ bool claim(JobImpl *job, uint64_t budget, size_t max_pieces, size_t *a, size_t *
     }
 }
 
-// A device lane's claim: about its share of the unclaimed bytes, at one lane's PCIe rate (~50 GiB/s)
-// against a host thread's CRC rate (~20 GiB/s and up): 5 : 2 per lane and thread.  Devices alone: a
-// whole slot.
+// A device lane's claim: its share of the unclaimed bytes, at one lane's PCIe rate (~50 GiB/s)
+// against a host thread's CRC rate over DRAM-resident parts (~17 GiB/s on the pool's EPYC boxes):
+// 3 : 1 per lane and thread, spread over the lane's kSlots claims in flight (round 4: one claim of
+// the whole share per slot gave the lane 21 % of a C2 job and left the host threads waiting for it,
+// profiles/r04/e).  Devices alone: a whole slot.
 uint64_t dev_budget(const JobImpl *job) {
     if (!job->hthreads) return kSlotBytes;
     const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
     const uint64_t rem = job->piece_start.back() - job->piece_start[c];
-    const uint64_t share = rem * 5 / (5 * (uint64_t)job->ndev + 2 * (uint64_t)job->hthreads);
+    const uint64_t share = rem * 3 / ((3 * (uint64_t)job->ndev + (uint64_t)job->hthreads) * kSlots);
     return std::min<uint64_t>(kSlotBytes, std::max(kMinDevClaim, share));
 }
 
@@ -556,7 +558,9 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         J.ndev = G;
         J.hthreads = H;
         for (int g = 0; g < G; ++g) J.spawn(device_worker, &J, g);
-        for (size_t t = 0; t < H; ++t) J.spawn(crc_host_worker, &J);
+        // the host threads: the host path's persistent pool (a std::thread per job thread cost its
+        // creation on every job), driven by one coordinator thread the job joins
+        if (H) J.spawn([](JobImpl *j, size_t h) { cpu::parallel(h, [j](size_t) { crc_host_worker(j); }); }, &J, H);
         *job_out = job.release();
         return 0;
     });

@@ -1,6 +1,13 @@
 #!/usr/bin/env python3
-"""Host-ingest throughput probe (aws_crt_amd_host_submit / job_wait): GiB/s for several part shapes
-from pinned and pageable host memory, beside the plain H2D rate of the same bytes."""
+"""Host-ingest throughput probe: GiB/s of one CRC32C job over host memory, for several part shapes,
+pinned and pageable, through
+
+  cpu_batch     aws_crt_amd_cpu_batch (the CPU baseline's call: persistent pool, the CPU share)
+  host_only     aws_crt_amd_host_submit_ex, ndevices < 0
+  hybrid        aws_crt_amd_host_submit_ex (host threads beside the device lane; the default)
+  devices_only  aws_crt_amd_host_submit_ex, host_threads 0
+
+best of `reps` after a warm-up each, and the plain H2D rate of the same bytes."""
 import json
 import os
 import sys
@@ -14,33 +21,48 @@ import torch  # noqa: E402
 import aws_crt_amd as eng  # noqa: E402
 
 
-def main():
-    eng.init()
-    total = 4 << 30
-    pinned = torch.randint(0, 256, (total,), dtype=torch.uint8).pin_memory()
-    pageable = torch.empty(512 << 20, dtype=torch.uint8)
-    pageable.copy_(pinned[: 512 << 20])
-    out = []
-    for name, host, part in [("pinned 64 KiB parts", pinned, 64 << 10), ("pinned 1 MiB parts", pinned, 1 << 20),
-                             ("pinned 32 MiB parts", pinned, 32 << 20), ("pinned 256 MiB parts", pinned, 256 << 20),
-                             ("pageable 1 MiB parts", pageable, 1 << 20), ("pinned 8 KiB parts (C4 shape)", pinned, 8 << 10)]:
-        n = host.numel() // part
-        job = eng.HostJob(eng.CRC32C, [host.data_ptr() + i * part for i in range(n)], [part] * n)
-        job.run()  # warm
+def best(fn, reps):
+    fn()
+    t = None
+    for _ in range(reps):
         t0 = time.perf_counter()
-        job.run()
+        fn()
         el = time.perf_counter() - t0
-        out.append({"shape": name, "bytes": n * part, "gibs": round(n * part / el / 2**30, 2)})
-        print(out[-1], flush=True)
+        t = el if t is None else min(t, el)
+    return t
+
+
+def main(total_mib=1280, reps=3):
+    eng.init()
+    total = total_mib << 20
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    pinned = torch.randint(0, 256, (total,), dtype=torch.uint8).pin_memory()
+    pageable = torch.empty(total, dtype=torch.uint8)
+    pageable.copy_(pinned)
+    res = []
+    for mem, host in (("pinned", pinned), ("pageable", pageable)):
+        for part in (64 << 10, 8 << 20):
+            n = total // part
+            ptrs, lens = [host.data_ptr() + i * part for i in range(n)], [part] * n
+            row = {"memory": mem, "part_bytes": part, "parts": n}
+            cb = eng.CpuBatch(eng.CRC32C, ptrs, lens, threads=threads)
+            row["cpu_batch"] = round(total / best(cb.run, reps) / 2**30, 1)
+            for name, nd, ht in (("host_only", -1, -1), ("hybrid", 0, -1), ("devices_only", 0, 0)):
+                job = eng.HostJob(eng.CRC32C, ptrs, lens, ndevices=nd, host_threads=ht)
+                row[name] = round(total / best(job.run, reps) / 2**30, 1)
+                if name == "hybrid":
+                    row["hybrid_device_share"] = round(job.device_bytes / total, 3)
+            res.append(row)
+            print(json.dumps(row), flush=True)
     dev = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(total // (256 << 20)):
         dev.copy_(pinned[i * (256 << 20):(i + 1) * (256 << 20)], non_blocking=True)
     torch.cuda.synchronize()
-    out.append({"shape": "H2D only (torch, 256 MiB copies)", "bytes": total, "gibs": round(total / (time.perf_counter() - t0) / 2**30, 2)})
-    print(json.dumps(out))
+    print(json.dumps({"h2d_only_gibs": round(total / (time.perf_counter() - t0) / 2**30, 1), "threads": threads,
+                      "results": res}))
 
 
 if __name__ == "__main__":
-    main()
+    main(*(int(a) for a in sys.argv[1:]))

@@ -46,6 +46,7 @@ for s in "$@"; do
              step 180 $O/abes_${v}_$r.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames || { rc=$?; break 2; }
              echo "$v $r $(grep '^{' $O/abes_${v}_$r.log | cut -c180-420)"; done; done
            cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so ;;
+    ingest) step 300 $O/ingest.log python -u aws-crt-cpp_amd/tools/ingest_probe.py; rc=$?; grep '^{' $O/ingest.log | tail -1 | cut -c1-300 ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
     *) echo "unknown step $s"; rc=2 ;;
