@@ -2745,7 +2745,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
         if (threadIdx.x >= 64) return;
         // wave 0: entry e in lane e (< 2 per wave); one publication per distinct buffer
         constexpr int kEntries = 2 * kWaves;
-        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane & (kEntries - 1));
+        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane < kEntries ? lane : 0);
         uint64_t eb = lane < kEntries ? slot[0] : ~0ull;
         const uint64_t er = slot[1];
         const uint32_t en = (uint32_t)slot[2];
@@ -3446,43 +3446,109 @@ __device__ __forceinline__ void lane_tables(T (*tab)[256]) {
     __syncthreads();
 }
 
+// The lane scans' folds.  TabFold: eight plain 256-entry tables (lane_tables; any width): a lane's
+// eight lookups of a word meet random banks, about 3.5-way conflicted per half-wave.  LaneW8 (W = 32,
+// round 4): the same tables T_t[e] = e * x^(8(t+1)) in crc32_stream_kernel's 8-copy layout (64 KiB,
+// one 256-byte row per entry: table t at 32 t, copy c at 4 c), looked up with its per-lane byte
+// rotation, so each ds_read_b32 half-wave meets 32 distinct banks whatever the data.  With one lane
+// per buffer the lookups' LDS cycles bound the scan (event-stream framing: 28.3 us per 65 MiB call on
+// the random-bank tables against ~9 us of HBM time).
+template <class T>
+struct TabFold {
+    const T (*tab)[256];
+    __device__ __forceinline__ T word(T s, uint64_t v) const {
+        if (sizeof(T) == 4) {
+            const uint32_t lo = (uint32_t)v ^ (uint32_t)s, hi = (uint32_t)(v >> 32);
+            return tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
+                   tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
+        } else {
+            const uint64_t x = v ^ (uint64_t)s;
+            return tab[7][x & 0xff] ^ tab[6][(x >> 8) & 0xff] ^ tab[5][(x >> 16) & 0xff] ^ tab[4][(x >> 24) & 0xff] ^
+                   tab[3][(x >> 32) & 0xff] ^ tab[2][(x >> 40) & 0xff] ^ tab[1][(x >> 48) & 0xff] ^ tab[0][x >> 56];
+        }
+    }
+    __device__ __forceinline__ T bytes(T s, uint64_t v, uint32_t nb) const {
+        for (uint32_t j = 0; j < nb; ++j, v >>= 8) s = (s >> 8) ^ tab[0][(s ^ (T)v) & 0xff];
+        return s;
+    }
+};
+
+constexpr uint32_t kLaneW8Lds = 65536;
+template <uint32_t POLY>
+struct LaneW8Basis {
+    uint32_t b[8][8];  // b[t][i] = T_t[1 << i]
+    constexpr LaneW8Basis() : b() {
+        for (int t = 0; t < 8; ++t)
+            for (int i = 0; i < 8; ++i) b[t][i] = (uint32_t)gf2_table_entry(1u << i, t, POLY);
+    }
+};
+// the 64 KiB table image from a 256-thread workgroup: thread e writes entry e's row (8 tables x 8 copies)
+template <uint32_t POLY>
+__device__ __forceinline__ void lane_w8_tables(char *lds) {
+    constexpr LaneW8Basis<POLY> B{};
+    const uint32_t e = threadIdx.x;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[t][i] : 0u;
+        const uint4 q = make_uint4(v, v, v, v);
+        *(uint4 *)(lds + (e << 8) + (t << 5)) = q;
+        *(uint4 *)(lds + (e << 8) + (t << 5) + 16) = q;
+    }
+    __syncthreads();
+}
+struct LaneW8 {
+    const char *L;
+    uint32_t cst8[8], sel8[8], c4;
+    __device__ void init(const char *lds, uint32_t lane) {  // Braid32W8::init's schedule
+        L = lds;
+        const uint32_t j = (lane >> 3) & 3u, c = lane & 7u;
+        c4 = c << 2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q = (k + j) & 3u;
+            cst8[k] = ((7u - q) << 5) | (c << 2);
+            cst8[4 + k] = ((3u - q) << 5) | (c << 2);
+            sel8[k] = sel8[4 + k] = 0x0c0c0004u | (q << 8);  // byte0 <- cst, byte1 <- byte q of the dword
+        }
+    }
+    __device__ __forceinline__ uint32_t word(uint32_t s, uint64_t v) const {
+        const uint32_t lo = (uint32_t)v ^ s, hi = (uint32_t)(v >> 32);
+        uint32_t x[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[k] = lds32(L, __builtin_amdgcn_perm(cst8[k], lo, sel8[k]));
+            x[4 + k] = lds32(L, __builtin_amdgcn_perm(cst8[4 + k], hi, sel8[4 + k]));
+        }
+        return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
+    }
+    __device__ __forceinline__ uint32_t bytes(uint32_t s, uint64_t v, uint32_t nb) const {  // T_0, copy c
+        for (uint32_t j = 0; j < nb; ++j, v >>= 8) s = (s >> 8) ^ lds32(L, ((((s ^ (uint32_t)v) & 0xffu)) << 8) | c4);
+        return s;
+    }
+};
+
 // register s advanced over [ptr, ptr + n).  All loads are aligned 8-byte words: the unaligned head
 // and the tail come from the aligned words that contain them (never past their page), so a short
 // buffer costs a few independent loads, not a serial chain of byte loads; whole words go eight loads
 // at a time before their slice-by-8 steps.
-template <class T>
-__device__ __forceinline__ T lane_word(T s, uint64_t v, const T (*tab)[256]) {
-    if (sizeof(T) == 4) {
-        const uint32_t lo = (uint32_t)v ^ (uint32_t)s, hi = (uint32_t)(v >> 32);
-        return tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
-               tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
-    } else {
-        const uint64_t x = v ^ (uint64_t)s;
-        return tab[7][x & 0xff] ^ tab[6][(x >> 8) & 0xff] ^ tab[5][(x >> 16) & 0xff] ^ tab[4][(x >> 24) & 0xff] ^
-               tab[3][(x >> 32) & 0xff] ^ tab[2][(x >> 40) & 0xff] ^ tab[1][(x >> 48) & 0xff] ^ tab[0][x >> 56];
-    }
-}
-template <class T>
-__device__ __forceinline__ T lane_bytes(T s, uint64_t v, uint32_t nb, const T (*tab)[256]) {
-    for (uint32_t j = 0; j < nb; ++j, v >>= 8) s = (s >> 8) ^ tab[0][(s ^ (T)v) & 0xff];
-    return s;
-}
-template <class T>
-__device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, const T (*tab)[256]) {
+template <class T, class F>
+__device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, const F &f) {
     if (n == 0) return s;
     const uintptr_t a = (uintptr_t)ptr;
     const uint64_t *w = (const uint64_t *)(a & ~(uintptr_t)7);
     const uint32_t o = (uint32_t)(a & 7);
     if (o) {
         const uint32_t hb = n < 8 - o ? (uint32_t)n : 8 - o;
-        s = lane_bytes<T>(s, *w++ >> (8 * o), hb, tab);
+        s = f.bytes(s, *w++ >> (8 * o), hb);
         n -= hb;
     }
     uint64_t k = n >> 3;
     // 16 bytes per lane per load instruction: the lanes of a wave read 64 different buffers, so the
-    // instruction count per byte (one cache-line request per lane), not bandwidth, bounds this loop.
+    // instruction count per byte (one cache-line request per lane), not bandwidth, bounds the loads.
     // Software-pipelined (round 4): the next 64 bytes' loads are in flight while the current 64 are
-    // folded, so a lane waits for memory once per buffer, not once per 64 bytes.
+    // folded.  (Deeper rings -- 2, 4, 8 steps in flight -- measured slower: profiles/r04/f.)
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));
     auto load8 = [](const uint64_t *p, uint64_t *v) {
 #pragma unroll
@@ -3500,31 +3566,40 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
         for (; k >= 8; k -= 8, w += 8) {
             load8(w, nv);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
+            for (int j = 0; j < 8; ++j) s = f.word(s, v[j]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = nv[j];
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s = lane_word<T>(s, v[j], tab);
+        for (int j = 0; j < 8; ++j) s = f.word(s, v[j]);
     }
     if (k >= 4) {
         const uint64_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
-        s = lane_word<T>(s, v0, tab);
-        s = lane_word<T>(s, v1, tab);
-        s = lane_word<T>(s, v2, tab);
-        s = lane_word<T>(s, v3, tab);
+        s = f.word(s, v0);
+        s = f.word(s, v1);
+        s = f.word(s, v2);
+        s = f.word(s, v3);
         k -= 4;
         w += 4;
     }
-    for (; k; --k) s = lane_word<T>(s, *w++, tab);
-    if (n & 7) s = lane_bytes<T>(s, *w, (uint32_t)(n & 7), tab);
+    for (; k; --k) s = f.word(s, *w++);
+    if (n & 7) s = f.bytes(s, *w, (uint32_t)(n & 7));
     return s;
 }
 
+// one lane per buffer: W = 32 on the conflict-free 8-copy tables, W = 64 on plain tables
 template <class T, T POLY>
 __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
-    __shared__ T tab[8][256];
-    lane_tables<T, POLY>(tab);
+    constexpr bool w8 = sizeof(T) == 4;
+    __shared__ __attribute__((aligned(16))) char lds[w8 ? kLaneW8Lds : 8 * 256 * sizeof(T)];
+    TabFold<T> tf{(const T (*)[256])lds};
+    LaneW8 lw;
+    if constexpr (w8) {
+        lane_w8_tables<(uint32_t)POLY>(lds);
+        lw.init(lds, threadIdx.x & 63u);
+    } else {
+        lane_tables<T, POLY>((T (*)[256])lds);
+    }
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= p.nbuf) return;
     const uint8_t *ptr;
@@ -3547,26 +3622,29 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
     }
     uint64_t seed = p.seed_all;
     if (seeds) seed = sizeof(T) == 4 ? (uint64_t)((const uint32_t *)seeds)[ix] : ((const uint64_t *)seeds)[ix];
-    const T s = lane_scan<T>((T)~seed, ptr, n, tab);
+    T s;
+    if constexpr (w8)
+        s = (T)lane_scan<uint32_t>((uint32_t)~seed, ptr, n, lw);
+    else
+        s = lane_scan<T>((T)~seed, ptr, n, tf);
     ((T *)out)[ix] = (T)~s;
 }
 
 // Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads
 // total_length and headers_length from the message's prelude (big-endian), refuses lengths outside
-// [16, limit - offset] and headers longer than total - 16 before touching the body, then folds the prelude (-> prelude CRC) and continues over the headers
-// and payload (-> message CRC, the running form of CRC32 over [0, total - 4)), and compares both
-// with the big-endian values stored at offset 8 and total - 4.
+// [16, limit - offset] and headers longer than total - 16 before touching the body, then folds the
+// prelude (-> prelude CRC) and continues over the headers and payload (-> message CRC, the running
+// form of CRC32 over [0, total - 4)), and compares both with the big-endian values stored at offset 8
+// and total - 4.  Folds on the conflict-free tables (LaneW8).
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
-#ifndef AMDCRC_ES_QUAD  // compile-time only (A/B builds): 0 keeps the one-lane-per-message kernel
-#define AMDCRC_ES_QUAD 0
-#endif
 
-#if !AMDCRC_ES_QUAD
 __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
-    __shared__ uint32_t tab[8][256];
-    lane_tables<uint32_t, kPoly32>(tab);
+    __shared__ __attribute__((aligned(16))) char lds[kLaneW8Lds];
+    lane_w8_tables<kPoly32>(lds);
+    LaneW8 f;
+    f.init(lds, threadIdx.x & 63u);
     const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= p.count) return;
     const uint64_t off = p.d_offsets[m];
@@ -3577,9 +3655,9 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
         // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
         // (headers_length > total_length - 16): malformed, whatever the CRCs say
         if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
-            uint32_t s = lane_scan<uint32_t>(~0u, q, 8, tab);
+            uint32_t s = lane_scan<uint32_t>(~0u, q, 8, f);
             pre = ~s;
-            s = lane_scan<uint32_t>(s, q + 8, total - 12, tab);
+            s = lane_scan<uint32_t>(s, q + 8, total - 12, f);
             msg = ~s;
             st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
         }
@@ -3588,7 +3666,6 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
     p.d_message_crc[m] = msg;
     p.d_status[m] = st;
 }
-#endif  // !AMDCRC_ES_QUAD
 
 }  // namespace
 
@@ -3750,123 +3827,10 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
     return (int)hipGetLastError();
 }
 
-// Event-stream framing check, four lanes per message (round 4; tests/test_eventstream_quad_model.py
-// restates it against zlib).  One lane per message read 64 messages per wave load -- 64 cache lines
-// per instruction, 16 bytes from each -- and a wave ran as long as the longest of its 64 messages
-// (profiles/r04: the software-pipelined form of that kernel still took 28.9 us per 65 MiB call, frac
-// 0.29).  Here a quad owns a message: lane j folds the body's words at 32 r + 8 j (r = row) with a
-// slice-by-8 step whose tables T'_t = T_(t+24) also skip the quad's other 24 bytes of the row; lane j's
-// share of the register is u_j * x^(-64 j) (byte tables per lane class), the quad XORs the shares, and
-// the last (body mod 32) bytes follow on the plain slice-by-8 path.  A wave load instruction reads 16
-// messages x 32 contiguous bytes, and a wave lasts as long as the longest of 16 messages at a quarter
-// of the steps.  Bodies start at any alignment: each lane reads the two aligned words around its word
-// (only when the message is unaligned), never past the aligned word holding the message's last byte.
-constexpr uint32_t kEsSkip = 24;  // bytes of a 32-byte row after a lane's word
-
-struct EsShareCols {  // column b of x^(-64 j), j = 1..3: (1 << b) * K_j
-    uint32_t c[3][32];
-    constexpr EsShareCols() : c() {
-        for (int j = 1; j <= 3; ++j) {
-            uint32_t k = 0x80000000u;  // x^0
-            for (int i = 0; i < 64 * j; ++i) k = (k & 0x80000000u) ? (((k ^ kPoly32) << 1) | 1u) : (k << 1);  // * x^-1
-            for (int b = 0; b < 32; ++b) c[j - 1][b] = (uint32_t)gf2_mulmod(1ull << b, k, kPoly32, 32);
-        }
-    }
-};
-
-__device__ __forceinline__ uint64_t es_word(const uint64_t *a, uint32_t o) {  // 8 bytes at (uint8*)a + o
-    const uint64_t lo = a[0];
-    if (!o) return lo;
-    const uint64_t hi = a[1];
-    return (lo >> (8 * o)) | (hi << (64 - 8 * o));
-}
-
-__global__ __launch_bounds__(256) void eventstream_quad_kernel(const EventStreamParams p) {
-    __shared__ uint32_t sd[8][256];     // standard slice-by-8 (prelude, tail)
-    __shared__ uint32_t tp[8][256];     // T'_t = T_(t+24): the row step
-    __shared__ uint32_t mj[3][4][256];  // lane shares of classes 1..3: (e << 8k) * x^(-64 j)
-    {
-        const uint32_t e = threadIdx.x;
-        uint32_t c = e;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? kPoly32 : 0u);
-        sd[0][e] = c;
-        __syncthreads();
-        for (int t = 1; t < 8 + (int)kEsSkip; ++t) {  // c = T_t[e] = e * x^(8(t+1))
-            c = (c >> 8) ^ sd[0][c & 0xff];
-            if (t < 8) sd[t][e] = c;
-            if (t >= (int)kEsSkip) tp[t - kEsSkip][e] = c;
-        }
-        constexpr EsShareCols C{};
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? C.c[j][8 * k + i] : 0u;
-                mj[j][k][e] = v;
-            }
-        __syncthreads();
-    }
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t m = gid >> 2;
-    const uint32_t j = (uint32_t)gid & 3u;
-    if (m >= p.count) return;  // whole quads: count messages x 4 lanes
-    const uint64_t off = p.d_offsets[m];
-    uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
-    if (off <= p.limit && p.limit - off >= 16) {
-        const uint8_t *q = p.base + off;
-        const uint64_t total = be32(q), headers = be32(q + 4);
-        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
-            const uint32_t s8 = lane_scan<uint32_t>(~0u, q, 8, sd);  // the prelude's register
-            pre = ~s8;
-            const uint8_t *body = q + 8;
-            const uint64_t nb = total - 12, R = nb >> 5;
-            const uint32_t o = (uint32_t)((uintptr_t)body & 7u);
-            const uint64_t *a = (const uint64_t *)((uintptr_t)body - o) + j;  // this lane's aligned word of row 0
-            uint32_t s = s8;
-            if (R) {
-                uint32_t u = 0;
-                uint64_t w = es_word(a, o);
-                if (j == 0) w ^= s8;  // the prelude state enters lane 0's first word
-                for (uint64_t r = 1; r < R; ++r) {
-                    const uint64_t wn = es_word(a + 4 * r, o);  // next row's word, in flight during this step
-                    u = lane_word<uint32_t>(u, w, tp);
-                    w = wn;
-                }
-                u = lane_word<uint32_t>(u, w, tp);
-                // lane j's share u * x^(-64 j), then the quad's XOR
-                uint32_t sh = u;
-                if (j) {
-                    const uint32_t (*t)[256] = mj[j - 1];
-                    sh = t[0][u & 0xff] ^ t[1][(u >> 8) & 0xff] ^ t[2][(u >> 16) & 0xff] ^ t[3][u >> 24];
-                }
-                sh ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sh, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-                sh ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)sh, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-                s = sh;
-            }
-            s = lane_scan<uint32_t>(s, body + 32 * R, nb - 32 * R, sd);  // the last (body mod 32) bytes
-            msg = ~s;
-            st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
-        }
-    }
-    if (j == 0) {
-        p.d_prelude_crc[m] = pre;
-        p.d_message_crc[m] = msg;
-        p.d_status[m] = st;
-    }
-}
-
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
     if (p->count == 0) return 0;
-#if AMDCRC_ES_QUAD
-    const uint64_t blocks = (p->count * 4 + 255) / 256;
-    launch(eventstream_quad_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
-#else
     const uint64_t blocks = (p->count + 255) / 256;
     launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
-#endif
     return (int)hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ constexpr int kW64StreamBlock = AMDCRC_W64_BLOCK;
 #define AMDCRC_XCD_CHUNK_GROUPS 4
 #endif
 constexpr uint64_t kXcdChunkBytes = (uint64_t)AMDCRC_XCD_CHUNK_GROUPS * 4096;
-#ifndef AMDCRC_XCD_BLOCK  // compile-time only (A/B builds): crc64_xcd_kernel workgroup size, 512 (two per CU) or 1024
+#ifndef AMDCRC_XCD_BLOCK  // compile-time only (A/B builds): crc64_xcd_kernel workgroup size: 512 or 640 (two per CU) or 1024
 #define AMDCRC_XCD_BLOCK 512
 #endif
 constexpr int kXcdBlock = AMDCRC_XCD_BLOCK;

@@ -192,6 +192,7 @@ void lane_free(Lane &L) {
 constexpr size_t kHybridPiece = 8u << 20;  // piece size of hybrid jobs (host threads claim whole pieces)
 constexpr uint64_t kMinDevClaim = 1u << 20;
 constexpr uint64_t kHostClaim = 1u << 20;
+constexpr uint64_t kHostClaimMax = 64u << 20;
 
 // Claim the next run of pieces [*a, *b): at least one, at most max_pieces, at most `budget` bytes
 // past the first.  false when the job has no unclaimed piece left.
@@ -257,7 +258,9 @@ void device_worker_body(JobImpl *job, int dev) {
             LANE_TRY(hipHostMalloc(&L.hres[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
             LANE_TRY(hipHostMalloc(&L.hseed[k], kMaxPiecesPerSlot * 8, hipHostMallocDefault));
             LANE_TRY(hipEventCreateWithFlags(&L.copied[k], hipEventDisableTiming));
-            LANE_TRY(hipEventCreateWithFlags(&L.done[k], hipEventDisableTiming));
+            // the lane thread waits on done[k] (harvest): blocking, so it sleeps instead of spinning on
+            // a CPU of the share the host threads run on
+            LANE_TRY(hipEventCreateWithFlags(&L.done[k], hipEventDisableTiming | hipEventBlockingSync));
         }
     }
     std::vector<const void *> dptrs;
@@ -364,7 +367,9 @@ void crc_host_worker(JobImpl *job) noexcept {
     while (job->rc.load() == 0) {
         const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
         const uint64_t rem = job->piece_start.back() - job->piece_start[c];
-        const uint64_t budget = std::min<uint64_t>(kHostClaim, std::max<uint64_t>(rem / (4 * (job->hthreads + (size_t)job->ndev)), 1));
+        // guided: a quarter of an even share of what is left, at least kHostClaim (one shared cursor
+        // claimed in 1 MiB runs cost a C2 job ~4,000 contended claims)
+        const uint64_t budget = std::min<uint64_t>(kHostClaimMax, std::max<uint64_t>(rem / (4 * (job->hthreads + (size_t)job->ndev)), kHostClaim));
         if (!claim(job, budget, SIZE_MAX, &a, &b)) return;
         for (size_t q = a; q < b; ++q) {
             const Piece &pc = job->pieces[q];
@@ -539,6 +544,7 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
         // pieces, buffer by buffer, in job order
+        J.pieces.reserve(count + (size_t)(total / piece));
         for (size_t i = 0; i < count; ++i) {
             size_t off = 0;
             do {
@@ -593,7 +599,16 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
             const uint64_t poly = alg_poly(J.alg);
             const int w = alg_width(J.alg);
             size_t p = 0;
-            for (size_t i = 0; i < J.count; ++i) {
+            if (J.pieces.size() == J.count) {  // no buffer was cut: the pieces are the buffers
+                for (size_t i = 0; i < J.count; ++i) {
+                    if (w == 64)
+                        ((uint64_t *)J.h_out)[i] = J.piece_val[i];
+                    else
+                        ((uint32_t *)J.h_out)[i] = (uint32_t)J.piece_val[i];
+                }
+                p = J.count;
+            }
+            for (size_t i = p; i < J.count; ++i) {
                 uint64_t acc = J.piece_val[p++];
                 while (p < J.pieces.size() && J.pieces[p].buf == i) {
                     acc = gf2_mulmod(acc, gf2_xpow8n(J.pieces[p].len, poly, w), poly, w) ^ J.piece_val[p];

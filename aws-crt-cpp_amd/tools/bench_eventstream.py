@@ -105,6 +105,15 @@ def main():
     torch.cuda.synchronize()
     kms = sum(A.event_ms(s, e) for s, e in zip(starts, ends)) / nt
     nbytes = fbs[0].payload_bytes
+    if a.device_frames:
+        # spot check of batch 0 against zlib (the library build under test may be an A/B variant)
+        import zlib
+        host_b = data[:pos].cpu().numpy().tobytes()
+        pre_d, msg_d = (res[0][k].cpu().numpy().view("uint32") for k in (0, 1))
+        for m in rng.sample(range(a.messages), min(4096, a.messages)):
+            o, n = offs[m], lens[m]
+            if (zlib.crc32(host_b[o:o + 8]) != int(pre_d[m]) or zlib.crc32(host_b[o:o + n - 4]) != int(msg_d[m])):
+                raise SystemExit(f"event-stream CRC mismatch at message {m} (offset {o}, {n} bytes)")
     print(json.dumps({
         "workload": f"event-stream framing: {a.messages} messages of {a.min_bytes}..{a.max_bytes} B "
                     f"({pos / 2**20:.1f} MiB), {fbs[0].n} CRC32 spans per call, "
