@@ -246,28 +246,30 @@ __device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typena
         asm volatile("global_store_dwordx2 %0, %1, off" : : "v"((uint64_t *)out + oi), "v"((uint64_t)fin) : "memory");
 }
 
-// r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time
+// r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, sixteen per round trip
+// (two s_load_dwordx16, 32 SGPRs; round 4: eight per trip made a W = 64 product eight dependent
+// L2 round trips)
 template <class T, int W>
 __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
+    typedef uint32_t s16u __attribute__((ext_vector_type(16)));
     T acc = 0;
 #pragma unroll
-    for (int c = 0; c < W; c += 8) {
-        uint64_t k0, k1, k2, k3, k4, k5, k6, k7;
+    for (int c = 0; c < W; c += 16) {
+        s16u k0, k1;
         const uint64_t a = rfl64((uint64_t)(cols + c));  // the table address must live in SGPRs
         asm volatile(
-            "s_load_dwordx2 %0, %8, 0x0\n\ts_load_dwordx2 %1, %8, 0x8\n\t"
-            "s_load_dwordx2 %2, %8, 0x10\n\ts_load_dwordx2 %3, %8, 0x18\n\t"
-            "s_load_dwordx2 %4, %8, 0x20\n\ts_load_dwordx2 %5, %8, 0x28\n\t"
-            "s_load_dwordx2 %6, %8, 0x30\n\ts_load_dwordx2 %7, %8, 0x38\n\t"
-            "s_waitcnt lgkmcnt(0)"
+            "s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
             // early-clobber: a returning load must never overwrite the shared address operand
-            : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
+            : "=&s"(k0), "=&s"(k1)
             : "s"(a)
             : "memory");
-        const uint64_t k[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if ((r >> (W - 1 - (c + j))) & 1) acc ^= (T)k[j];
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t lo = j < 8 ? k0[2 * j] : k1[2 * (j - 8)];
+            const uint32_t hi = j < 8 ? k0[2 * j + 1] : k1[2 * (j - 8) + 1];
+            const T col = W == 64 ? (T)(((uint64_t)hi << 32) | lo) : (T)lo;
+            if ((r >> (W - 1 - (c + j))) & 1) acc ^= col;
+        }
     }
     return acc;
 }
@@ -1694,6 +1696,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
     const uint64_t *xinv = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidXinvWord);
     const uint64_t *gsh = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGshiftWord);
+    const uint64_t *gmc = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGmWord);
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;  // b0 < nbuf then (the host's wbuf is nbuf only past the groups)
@@ -1797,8 +1800,13 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         return;
 #endif
         uint32_t r = wave_xor_s(eng.mulK(u, lane));
-        for (uint32_t m = sc.vg - g, i = 0; m; m >>= 1, ++i)
-            if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
+        const uint32_t mg = sc.vg - g;  // groups after the part
+        if (mg && mg < (uint32_t)kBraidGmCount) {
+            r = mul_pcols<uint32_t, 32>(r, gmc + 32 * mg);
+        } else {
+            for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
+                if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
+        }
         if (lane != 0) return;
         if (ga == 0 && g == sc.vg) {
             finalize<true>(p, sc.b, r, eng);
@@ -2671,7 +2679,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     B eng;
     eng.init(lds, lane);
     eng.kl = kl;
-    const uint64_t *shcols = p.d_pcols + 256;        // columns of x^(8 * chunk * 2^i), i < 40
     const uint64_t *bytecols = p.d_pcols + 256 + 40 * 64;  // [level][v][j]: x^(8 * chunk * v * 256^level) * x^j
     uint64_t pb = ~0ull, pk = 0;  // the open part: buffer, last chunk
     uint32_t pn = 0;              // chunks in the part
@@ -2696,10 +2703,13 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
         }
         return r;
     };
-    // the same product on the scalar unit (columns by SMEM): inside the scan, rarely
+    // the same product on the scalar unit (columns by SMEM): a part ending inside the scan (one per
+    // buffer a wave leaves: multi-batch launches cross many).  One product per nonzero byte of m --
+    // m < nwx, so one or two -- not one per set bit (round 4: up to twelve products of eight L2 round
+    // trips each made a 20-batch C5 launch 0.63 of the HBM peak)
     auto shift_scalar = [&](uint64_t r, uint64_t m) -> uint64_t {
-        for (int i = 0; m; ++i, m >>= 1)
-            if (m & 1) r = mul_pcols<uint64_t, 64>(r, shcols + 64 * i);
+        for (int L = 0; m; ++L, m >>= 8)
+            if (m & 255u) r = mul_pcols<uint64_t, 64>(r, bytecols + (256u * L + (m & 255u)) * 64);
         return r;
     };
     // value r of n chunks of buffer b into the buffer's accumulator; the part completing the count
@@ -2837,6 +2847,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
 // = engine.cpp get_xcd_consts (the X^(-j) and x^(8*4096*2^i) columns).
 constexpr uint32_t kXcdXinvU64 = 256 + 40 * 64 + 4 * 256 * 64;  // get_xcd_consts: X^(-j) columns, j < 32
 constexpr uint32_t kXcdGshiftU64 = kXcdXinvU64 + 32 * 64;        // x^(8*4096*2^i) columns, i < 40
+constexpr uint32_t kXcdGmU64 = kXcdGshiftU64 + 40 * 64;            // x^(8*4096*m) columns, m < kBraidGmCount
 
 template <uint64_t POLY>
 __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanParams p) {
@@ -2854,6 +2865,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
     const uint64_t *xinv = p.d_pcols + kXcdXinvU64;
     const uint64_t *gsh = p.d_pcols + kXcdGshiftU64;
+    const uint64_t *gmc = p.d_pcols + kXcdGmU64;
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;
@@ -2929,8 +2941,13 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     };
     auto part_finish = [&]() {
         uint64_t r = wave_xor64_s(eng.mulK(u));
-        for (uint32_t m = sc.vg - g, i = 0; m; m >>= 1, ++i)
-            if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
+        const uint32_t mg = sc.vg - g;  // groups after the part
+        if (mg && mg < (uint32_t)kBraidGmCount) {
+            r = mul_pcols<uint64_t, 64>(r, gmc + 64 * mg);
+        } else {
+            for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
+                if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
+        }
         if (lane != 0) return;
         if (ga == 0 && g == sc.vg) {
             finalize<true>(p, sc.b, r, eng);

@@ -296,6 +296,17 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
             }
             sq = gf2_mulmod(sq, sq, poly, 32);
         }
+        // columns of x^(8*4096*m), m < kBraidGmCount
+        const uint64_t g1 = gf2_xpow8n(4096, poly, 32);
+        uint64_t gm = 0x80000000u;  // x^0
+        for (int m = 0; m < kBraidGmCount; ++m) {
+            uint32_t col = (uint32_t)gm;
+            for (int j = 0; j < 32; ++j) {
+                c[kBraidGmWord + 2 * (32 * m + j)] = col;
+                col = (uint32_t)gf2_mulx(col, poly);
+            }
+            gm = gf2_mulmod(gm, g1, poly, 32);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
@@ -329,14 +340,14 @@ int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
 // crc64_xcd_kernel constants for nwx waves per XCD (u64): [0, 256) the nibble tables of the chunk
 // jump J = x^(8 * chunk * (nwx - 1)), entry 16 n + v = (v << 4n) * J; then 40 x 64 columns of
 // x^(8 * chunk * 2^i) * x^j; then [level < 4][v < 256] x 64 columns of x^(8 * chunk * v * 256^level) * x^j
-// (a part's shift to its buffer end: bit by bit on the scalar unit, or a byte of the distance per
-// lane-parallel product)
+// (a part's shift to its buffer end: a byte of the distance per product); then the list scan's X^(-j)
+// columns, x^(8*4096*2^i) columns and x^(8*4096*m) columns (m < kBraidGmCount)
 int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
     const auto key = std::make_pair(alg, nwx);
     auto it = d->xcd.find(key);
     if (it == d->xcd.end()) {
         const uint64_t poly = alg_poly(alg);
-        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64, 0);
+        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64, 0);
         const uint64_t J = gf2_xpow8n((uint64_t)kXcdChunkBytes * (nwx - 1), poly, 64);
         for (int n = 0; n < 16; ++n)
             for (uint64_t v = 0; v < 16; ++v) c[16 * n + v] = gf2_mulmod(v << (4 * n), J, poly, 64);
@@ -381,6 +392,17 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
                 col = gf2_mulx(col, poly);
             }
             gq = gf2_mulmod(gq, gq, poly, 64);
+        }
+        // columns of x^(8*4096*m), m < kBraidGmCount: the same shifts in one product (round 4)
+        const uint64_t g1 = gf2_xpow8n(4096, poly, 64);
+        uint64_t gm = 1ull << 63;  // x^0
+        for (int m = 0; m < kBraidGmCount; ++m) {
+            uint64_t col = gm;
+            for (int j = 0; j < 64; ++j) {
+                c[256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + 64 * m + j] = col;
+                col = gf2_mulx(col, poly);
+            }
+            gm = gf2_mulmod(gm, g1, poly, 64);
         }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 8);

@@ -111,12 +111,15 @@ struct ScanParams {
 //   [7424, 7936)  columns (u64) of X^(-j), X = x^(8*512), j < 8: the list streaming scan's head-state
 //                 entry (crc32_list_stream_kernel)
 //   [7936, 9984)  columns (u64) of x^(8*4096*2^i), i < 32: the list streaming scan's part shifts
+//   [9984, 14080) columns (u64) of x^(8*4096*m), m < 64: the same shifts in one product (round 4)
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 9984;
+constexpr int kBraidConstWords = 14080;
 constexpr int kBraidXinvWord = 7424;    // first word of the X^(-j) columns
 constexpr int kBraidGshiftWord = 7936;  // first word of the x^(8*4096*2^i) columns
+constexpr int kBraidGmWord = 9984;      // first word of the x^(8*4096*m) columns, m < kBraidGmCount
+constexpr int kBraidGmCount = 64;
 constexpr int kBraidK64Word = 3328;   // first word of the x^(-64 l) K image
 constexpr int kBraidK128Word = 5376;  // first word of the x^(-128 l) K image
 
