@@ -1793,6 +1793,19 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
+    // value r of n groups of a buffer of vg groups into its accumulator; the part completing the count
+    // finishes it (lane 0)
+    auto publish = [&](uint64_t b, uint32_t r, uint32_t n, uint32_t vg) {
+        (void)sx_xor64_ret(&p.d_acc[b], (unsigned long long)r);  // performed before it is counted
+        const uint32_t c = sx_add32_ret(&p.d_cnt[b], n);
+        if (c + n == vg) {
+            const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[b], 0ull);
+            sx_store32(&p.d_cnt[b], 0u);
+            finalize<true>(p, b, fin, eng);
+        }
+    };
+    uint64_t hb = ~0ull;  // the held part: buffer, value, groups, the buffer's groups
+    uint32_t hr = 0, hn = 0, hvg = 0;
     // the part [ga, g) ends: its share, moved to the buffer's end, finishes the buffer or joins it
     auto part_finish = [&]() {
 #ifdef AMDCRC_XP_LIST_NOFINISH  // experiment builds only (timing; results wrong): a part stores its lane-0 braid
@@ -1807,18 +1820,18 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
                 if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
         }
-        if (lane != 0) return;
         if (ga == 0 && g == sc.vg) {
-            finalize<true>(p, sc.b, r, eng);
+            if (lane == 0) finalize<true>(p, sc.b, r, eng);
             return;
         }
-        (void)sx_xor64_ret(&p.d_acc[sc.b], (unsigned long long)r);  // performed before it is counted
-        const uint32_t n = g - ga, c = sx_add32_ret(&p.d_cnt[sc.b], n);
-        if (c + n == sc.vg) {
-            const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[sc.b], 0ull);
-            sx_store32(&p.d_cnt[sc.b], 0u);
-            finalize<true>(p, sc.b, fin, eng);
+        // a buffer cut between waves: its parts meet in the accumulator through returning atomics,
+        // whose wait would drain the payload ring -- so a part ending inside the scan (the wave's first,
+        // the tail of a buffer begun by the wave before) is held and published after the scan
+        if (q < nq && hb == ~0ull) {
+            hb = sc.b, hr = r, hn = g - ga, hvg = sc.vg;
+            return;
         }
+        if (lane == 0) publish(sc.b, r, g - ga, sc.vg);
     };
     part_begin();
     auto step = [&](W8Group &cur, W8Group &nxt, bool first) {
@@ -1854,6 +1867,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (q < nq) step(rc, rb, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
+    if (hb != ~0ull && lane == 0) publish(hb, hr, hn, hvg);
     // trailing buffers without a main region
     while (sc.b + 1 < b_end) {
         sc = lbuf_at(p, sc.b + 1);
@@ -2731,10 +2745,12 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     uint32_t hn = 0;
     auto part_finish = [&]() {
         const uint64_t r = part_raw();
+#ifndef AMDCRC_XP_XCD_NOPUB  // experiment builds only (timing; results wrong): mid-scan parts dropped
         if (hb != ~0ull) {
             const uint64_t v = shift_scalar(hr, CPB - 1 - hk);
             if (lane == 0) publish(hb, v, hn);
         }
+#endif
         hb = pb, hr = r, hk = pk, hn = pn;
     };
     // every wave's held and last parts go through LDS: wave 0 joins the parts of one buffer, so the
@@ -2939,6 +2955,17 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
+    auto publish = [&](uint64_t b, uint64_t r, uint32_t n, uint32_t vg) {  // lane 0
+        (void)sx_xor64_ret(&p.d_acc[b], (unsigned long long)r);  // performed before it is counted
+        const uint32_t c = sx_add32_ret(&p.d_cnt[b], n);
+        if (c + n == vg) {
+            const uint64_t fin = sx_swap64_ret(&p.d_acc[b], 0ull);
+            sx_store32(&p.d_cnt[b], 0u);
+            finalize<true>(p, b, fin, eng);
+        }
+    };
+    uint64_t hb = ~0ull, hr = 0;  // the held part: buffer, value, groups, the buffer's groups
+    uint32_t hn = 0, hvg = 0;
     auto part_finish = [&]() {
         uint64_t r = wave_xor64_s(eng.mulK(u));
         const uint32_t mg = sc.vg - g;  // groups after the part
@@ -2948,18 +2975,17 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
                 if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
         }
-        if (lane != 0) return;
         if (ga == 0 && g == sc.vg) {
-            finalize<true>(p, sc.b, r, eng);
+            if (lane == 0) finalize<true>(p, sc.b, r, eng);
             return;
         }
-        (void)sx_xor64_ret(&p.d_acc[sc.b], (unsigned long long)r);  // performed before it is counted
-        const uint32_t n = g - ga, c = sx_add32_ret(&p.d_cnt[sc.b], n);
-        if (c + n == sc.vg) {
-            const uint64_t fin = sx_swap64_ret(&p.d_acc[sc.b], 0ull);
-            sx_store32(&p.d_cnt[sc.b], 0u);
-            finalize<true>(p, sc.b, fin, eng);
+        // a cut buffer's part ending inside the scan is held until the scan ends (see
+        // crc32_list_stream_kernel: the returning atomics' wait would drain the payload ring)
+        if (q < nq && hb == ~0ull) {
+            hb = sc.b, hr = r, hn = g - ga, hvg = sc.vg;
+            return;
         }
+        if (lane == 0) publish(sc.b, r, g - ga, sc.vg);
     };
     part_begin();
     auto step = [&](B64Group &cur, B64Group &nxt) {
@@ -2992,6 +3018,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         if (q < nq) step(rc, rb);
     }
     drain();
+    if (hb != ~0ull && lane == 0) publish(hb, hr, hn, hvg);
     while (sc.b + 1 < b_end) {  // trailing buffers without a main region
         sc = lbuf_at(p, sc.b + 1);
         finish_empty();
@@ -3467,9 +3494,7 @@ __device__ __forceinline__ void lane_tables(T (*tab)[256]) {
 // eight lookups of a word meet random banks, about 3.5-way conflicted per half-wave.  LaneW8 (W = 32,
 // round 4): the same tables T_t[e] = e * x^(8(t+1)) in crc32_stream_kernel's 8-copy layout (64 KiB,
 // one 256-byte row per entry: table t at 32 t, copy c at 4 c), looked up with its per-lane byte
-// rotation, so each ds_read_b32 half-wave meets 32 distinct banks whatever the data.  With one lane
-// per buffer the lookups' LDS cycles bound the scan (event-stream framing: 28.3 us per 65 MiB call on
-// the random-bank tables against ~9 us of HBM time).
+// rotation, so each ds_read_b32 half-wave meets 32 distinct banks whatever the data.
 template <class T>
 struct TabFold {
     const T (*tab)[256];
@@ -3499,19 +3524,28 @@ struct LaneW8Basis {
             for (int i = 0; i < 8; ++i) b[t][i] = (uint32_t)gf2_table_entry(1u << i, t, POLY);
     }
 };
-// the 64 KiB table image from a 256-thread workgroup: thread e writes entry e's row (8 tables x 8 copies)
+// the 64 KiB table image from a 256-thread workgroup, 16 ds_write_b128 per thread.  Store k of thread
+// i writes entry e = (i >> 3) + 32 (k >> 1), table t = ((i & 7) >> 1) + 4 (k & 1), copies 4 (i & 1)..+3,
+// so the eight lanes of each ds_write_b128 lane group cover the 128 bytes of all 32 banks once (16
+// bytes at (2 t + (i & 1)) mod 8 of a 128-byte line).  Round 4: thread e writing its own row made
+// every group 8-way conflicted -- 8,000 conflict cycles per CU before the first message.
 template <uint32_t POLY>
 __device__ __forceinline__ void lane_w8_tables(char *lds) {
     constexpr LaneW8Basis<POLY> B{};
-    const uint32_t e = threadIdx.x;
+    const uint32_t i = threadIdx.x, tl = (i & 7u) >> 1, half = i & 1u;
+    uint32_t bl[8], bh[8];  // the bases of T_tl and T_(tl + 4)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
+    for (int b = 0; b < 8; ++b) {
+        bl[b] = tl == 0 ? B.b[0][b] : tl == 1 ? B.b[1][b] : tl == 2 ? B.b[2][b] : B.b[3][b];
+        bh[b] = tl == 0 ? B.b[4][b] : tl == 1 ? B.b[5][b] : tl == 2 ? B.b[6][b] : B.b[7][b];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t e = (i >> 3) + 32u * (uint32_t)(k >> 1), t = tl + 4u * (uint32_t)(k & 1);
         uint32_t v = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[t][i] : 0u;
-        const uint4 q = make_uint4(v, v, v, v);
-        *(uint4 *)(lds + (e << 8) + (t << 5)) = q;
-        *(uint4 *)(lds + (e << 8) + (t << 5) + 16) = q;
+        for (int b = 0; b < 8; ++b) v ^= ((e >> b) & 1u) ? ((k & 1) ? bh[b] : bl[b]) : 0u;
+        *(uint4 *)(lds + (e << 8) + (t << 5) + (half << 4)) = make_uint4(v, v, v, v);
     }
     __syncthreads();
 }
@@ -3647,37 +3681,96 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
     ((T *)out)[ix] = (T)~s;
 }
 
-// Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads
-// total_length and headers_length from the message's prelude (big-endian), refuses lengths outside
-// [16, limit - offset] and headers longer than total - 16 before touching the body, then folds the
-// prelude (-> prelude CRC) and continues over the headers and payload (-> message CRC, the running
-// form of CRC32 over [0, total - 4)), and compares both with the big-endian values stored at offset 8
-// and total - 4.  Folds on the conflict-free tables (LaneW8).
+// Event-stream framing check, a lane pair per message (aws_crt_amd_eventstream_crcs).  Both lanes read
+// total_length and headers_length from the message's prelude (big-endian), refuse lengths outside
+// [16, limit - offset] and headers longer than total - 16 before touching the body.  The message CRC
+// spans n = total - 4 bytes: the pair's second lane folds the last h = 64 floor(n / 128) bytes from 0
+// and the first lane the prelude (-> prelude CRC) and the bytes up to n - h from ~0, its register then
+// moved past the second lane's bytes (times x^(8h): eight nibble lookups, h < 1 KiB; longer messages
+// stay on the first lane); the pair XORs its registers (DPP) and compares both CRCs with the big-endian
+// values stored at offset 8 and total - 4.  Both lanes run one code path with their own (state, span),
+// so a wave holds 32 messages at half the longest chain of one lane per message (round 4; the
+// one-lane kernel took 28.3-29.4 us per 65 MiB call, profiles/r04/f-h).  Folds on LaneW8.
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
+constexpr uint32_t kEsShiftOff = kLaneW8Lds;                  // [m < 16][nibble k < 8][v < 16]: (v << 4k) * x^(512 m)
+constexpr uint32_t kEsSplitMax = 16;                          // second lane for h = 64 m, m < 16
+constexpr uint32_t kEsLds = kEsShiftOff + kEsSplitMax * 8 * 16 * 4;
+static_assert(2 * kEsLds <= 160 * 1024, "two eventstream_kernel workgroups per CU");
+
+template <uint32_t POLY>
+struct EsX512 {  // column b of x^512 (64 bytes): (1 << b) * x^512
+    uint32_t c[32];
+    constexpr EsX512() : c() {
+        const uint64_t k = gf2_xpow8n(64, POLY, 32);
+        for (int b = 0; b < 32; ++b) c[b] = (uint32_t)gf2_mulmod(1ull << b, k, POLY, 32);
+    }
+};
+// threads < 128: entry (k, v) = i for every m, each m the previous times x^512 (the caller syncs)
+template <uint32_t POLY>
+__device__ __forceinline__ void es_shift_tables(char *lds) {
+    constexpr EsX512<POLY> X{};
+    const uint32_t i = threadIdx.x;
+    if (i >= 128) return;
+    uint32_t *t = (uint32_t *)(lds + kEsShiftOff);
+    uint32_t val = (i & 15u) << (4 * (i >> 4));
+    t[i] = val;
+    for (uint32_t m = 1; m < kEsSplitMax; ++m) {
+        uint32_t nv = 0;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) nv ^= ((val >> b) & 1u) ? X.c[b] : 0u;
+        val = nv;
+        t[128 * m + i] = val;
+    }
+}
+__device__ __forceinline__ uint32_t es_shift(const char *lds, uint32_t r, uint32_t m) {
+    const uint32_t *t = (const uint32_t *)(lds + kEsShiftOff) + 128 * m;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc ^= t[16 * k + ((r >> (4 * k)) & 15u)];
+    return acc;
+}
 
 __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
-    __shared__ __attribute__((aligned(16))) char lds[kLaneW8Lds];
-    lane_w8_tables<kPoly32>(lds);
+    __shared__ __attribute__((aligned(16))) char lds[kEsLds];
+    es_shift_tables<kPoly32>(lds);
+    lane_w8_tables<kPoly32>(lds);  // ends with the workgroup barrier
     LaneW8 f;
     f.init(lds, threadIdx.x & 63u);
-    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= p.count) return;
-    const uint64_t off = p.d_offsets[m];
-    uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
-    if (off <= p.limit && p.limit - off >= 16) {
-        const uint8_t *q = p.base + off;
-        const uint64_t total = be32(q), headers = be32(q + 4);
-        // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
-        // (headers_length > total_length - 16): malformed, whatever the CRCs say
-        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
-            uint32_t s = lane_scan<uint32_t>(~0u, q, 8, f);
-            pre = ~s;
-            s = lane_scan<uint32_t>(s, q + 8, total - 12, f);
-            msg = ~s;
-            st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = gid >> 1;
+    const uint32_t second = (uint32_t)gid & 1u;
+    const bool live = m < p.count;
+    bool ok = false;
+    const uint8_t *q = p.base;
+    uint64_t total = 0, h = 0;
+    if (live) {
+        const uint64_t off = p.d_offsets[m];
+        if (off <= p.limit && p.limit - off >= 16) {
+            q = p.base + off;
+            total = be32(q);
+            const uint64_t headers = be32(q + 4);
+            // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
+            // (headers_length > total_length - 16): malformed, whatever the CRCs say
+            ok = total >= 16 && total <= p.limit - off && headers <= total - 16;
         }
+    }
+    const uint64_t n = ok ? total - 4 : 0;
+    h = 64 * (n / 128);
+    if (h >= 64 * (uint64_t)kEsSplitMax) h = 0;
+    uint32_t pre = 0, s = 0;
+    if (ok) pre = ~lane_scan<uint32_t>(~0u, q, 8, f);
+    const uint8_t *ps = second ? q + (n - h) : q + 8;
+    const uint64_t pn = !ok ? 0 : second ? h : n - 8 - h;
+    s = lane_scan<uint32_t>(second ? 0u : ~pre, ps, pn, f);
+    const uint32_t part = es_shift(lds, s, second ? 0u : (uint32_t)(h / 64));
+    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    if (!live || second) return;
+    uint32_t msg = 0, st = 4u;  // bit 2: malformed
+    if (ok) {
+        msg = ~(part ^ other);
+        st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
     }
     p.d_prelude_crc[m] = pre;
     p.d_message_crc[m] = msg;
@@ -3846,7 +3939,7 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
 
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
     if (p->count == 0) return 0;
-    const uint64_t blocks = (p->count + 255) / 256;
+    const uint64_t blocks = (2 * p->count + 255) / 256;  // a lane pair per message
     launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
     return (int)hipGetLastError();
 }

@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -107,11 +109,32 @@ struct JobImpl {
     int ndev = 0;                       // device lanes of the job
     size_t hthreads = 0;                // host threads taking pieces beside them
     std::atomic<uint64_t> dev_bytes{0};
+    // AWS_CRT_AMD_INGEST_TRACE=1: one stderr line per job (claims and when each side ran out of work)
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    std::atomic<uint64_t> lane_claims{0}, lane_end_ns{0}, host_end_ns{0}, host_claims{0};
+    uint64_t since_ns() const {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    }
+    static void atomic_max(std::atomic<uint64_t> &a, uint64_t v) {
+        uint64_t c = a.load(std::memory_order_relaxed);
+        while (c < v && !a.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
+        }
+    }
     uint64_t *dev_bytes_out = nullptr;  // options: bytes the devices scanned, set by job_wait
     std::vector<std::thread> workers;
     std::atomic<int> rc{0};
     std::string err;
     std::mutex err_mu;
+    // back to a fresh job, keeping the vectors' storage (a C2 job's 20,480 pieces are ~1 MiB of
+    // vectors: fresh pages on every job cost ~0.3 ms of faults)
+    void reset() {
+        alg = 0, ptrs = nullptr, lens = nullptr, count = 0, h_out = nullptr;
+        seeds.clear(), pieces.clear(), piece_val.clear(), piece_start.clear();
+        cursor.store(0), ndev = 0, hthreads = 0, dev_bytes.store(0), dev_bytes_out = nullptr;
+        workers.clear(), rc.store(0), err.clear();
+        t0 = std::chrono::steady_clock::now();
+        lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
+    }
     void set_error(int code, const char *m) noexcept {
         std::lock_guard<std::mutex> g(err_mu);
         if (rc.load() == 0) {
@@ -285,6 +308,7 @@ void device_worker_body(JobImpl *job, int dev) {
         // claim a run of pieces for slot k: contiguous in the slot, in order (pieces are at most a slot)
         size_t a, b;
         if (!claim(job, dev_budget(job), kMaxPiecesPerSlot, &a, &b)) break;
+        job->lane_claims.fetch_add(1, std::memory_order_relaxed);
         std::vector<size_t> &ps = slot_pieces[k];
         ps.clear();
         for (size_t q = a; q < b; ++q) ps.push_back(q);
@@ -359,6 +383,7 @@ void device_worker_body(JobImpl *job, int dev) {
     }
     for (int j = 0; j < kSlots; ++j)
         if (!harvest(j)) job->set_error(AWS_CRT_AMD_ERR_HIP, "slot results");
+    JobImpl::atomic_max(job->lane_end_ns, job->since_ns());
 }
 
 // A hybrid CRC job's host thread: claimed runs of pieces on the host path, into piece_val like a lane
@@ -367,10 +392,14 @@ void crc_host_worker(JobImpl *job) noexcept {
     while (job->rc.load() == 0) {
         const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
         const uint64_t rem = job->piece_start.back() - job->piece_start[c];
-        // guided: a quarter of an even share of what is left, at least kHostClaim (one shared cursor
-        // claimed in 1 MiB runs cost a C2 job ~4,000 contended claims)
-        const uint64_t budget = std::min<uint64_t>(kHostClaimMax, std::max<uint64_t>(rem / (4 * (job->hthreads + (size_t)job->ndev)), kHostClaim));
-        if (!claim(job, budget, SIZE_MAX, &a, &b)) return;
+        // guided: a quarter of an even share of what is left, at least kHostClaim or an eighth of an
+        // even share of the job (one shared cursor claimed in 1 MiB runs cost a C2 job ~4,000
+        // contended claims; a 1 MiB floor left a 1 MiB job to one thread)
+        const uint64_t workers = job->hthreads + (size_t)job->ndev;
+        const uint64_t floor = std::min<uint64_t>(kHostClaim, std::max<uint64_t>(job->piece_start.back() / (8 * workers), 1));
+        const uint64_t budget = std::min<uint64_t>(kHostClaimMax, std::max<uint64_t>(rem / (4 * workers), floor));
+        if (!claim(job, budget, SIZE_MAX, &a, &b)) break;
+        job->host_claims.fetch_add(1, std::memory_order_relaxed);
         for (size_t q = a; q < b; ++q) {
             const Piece &pc = job->pieces[q];
             const uint8_t *p = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
@@ -381,6 +410,7 @@ void crc_host_worker(JobImpl *job) noexcept {
             }
         }
     }
+    JobImpl::atomic_max(job->host_end_ns, job->since_ns());
 }
 
 // A job's buffers on the host path (xxHash, or no device): buffers round-robin over `threads`
@@ -481,6 +511,38 @@ struct aws_crt_amd_job {
     JobImpl impl;
 };
 
+namespace {
+// finished jobs kept for reuse (their vectors' storage), at most 4, none over 1 Mi pieces
+std::mutex g_job_mu;
+std::vector<aws_crt_amd_job *> g_job_free;
+aws_crt_amd_job *job_take() {
+    {
+        std::lock_guard<std::mutex> g(g_job_mu);
+        if (!g_job_free.empty()) {
+            aws_crt_amd_job *j = g_job_free.back();
+            g_job_free.pop_back();
+            return j;
+        }
+    }
+    return new (std::nothrow) aws_crt_amd_job;
+}
+void job_give(aws_crt_amd_job *j) noexcept {
+    if (!j) return;
+    if (j->impl.pieces.capacity() <= ((size_t)1 << 20)) {
+        try {
+            j->impl.reset();
+            std::lock_guard<std::mutex> g(g_job_mu);
+            if (g_job_free.size() < 4) {
+                g_job_free.push_back(j);
+                return;
+            }
+        } catch (...) {
+        }
+    }
+    delete j;
+}
+}  // namespace
+
 extern "C" {
 
 AWS_CRT_AMD_API int aws_crt_amd_register_host(void *p, size_t n) {
@@ -507,7 +569,7 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
             if (lens[i] && !h_ptrs[i]) return AWS_CRT_AMD_ERR_INVALID_ARG;
         const int ndevices = opt ? opt->ndevices : 0;
         const int want_host = opt ? opt->host_threads : -1;
-        std::unique_ptr<aws_crt_amd_job> job(new (std::nothrow) aws_crt_amd_job);
+        std::unique_ptr<aws_crt_amd_job, void (*)(aws_crt_amd_job *)> job(job_take(), job_give);
         if (!job) return AWS_CRT_AMD_ERR_OOM;
         JobImpl &J = job->impl;
         J.alg = alg;
@@ -521,7 +583,7 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         J.seeds.assign(count, 0);
         for (size_t i = 0; h_seeds && i < count; ++i)
             J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
-        const int vis = visible_devices();
+        const int vis = ndevices < 0 ? 0 : visible_devices();
         int G = ndevices < 0 ? 0 : ndevices == 0 ? vis : std::min(ndevices, vis);  // < 0: the host path only
         if (is_crc(alg) && G > 0 && !amdcrc_gpu_usable()) {
             amdcrc_note_fallback();  // a visible device the engine cannot use (not gfx950, HIP error)
@@ -620,8 +682,16 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
                     ((uint32_t *)J.h_out)[i] = (uint32_t)acc;
             }
         }
+        const char *trace = std::getenv("AWS_CRT_AMD_INGEST_TRACE");
+        if (trace && *trace && *trace != '0')
+            std::fprintf(stderr,
+                         "{\"ingest_trace\": 1, \"pieces\": %zu, \"host_threads\": %zu, \"lanes\": %d, \"device_bytes\": %llu, "
+                         "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f}\n",
+                         J.pieces.size(), J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
+                         (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
+                         J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6);
         if (rc) t_err = J.err;
-        delete job;
+        job_give(job);
         return rc;
     });
 }
