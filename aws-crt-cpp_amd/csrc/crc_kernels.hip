@@ -246,30 +246,29 @@ __device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typena
         asm volatile("global_store_dwordx2 %0, %1, off" : : "v"((uint64_t *)out + oi), "v"((uint64_t)fin) : "memory");
 }
 
-// r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, sixteen per round trip
-// (two s_load_dwordx16, 32 SGPRs; round 4: eight per trip made a W = 64 product eight dependent
-// L2 round trips)
+// r * x^(8*TILE*kk) for a wave-uniform r: the 32/64 columns come in by SMEM, eight at a time (sixteen
+// per round trip, 32 SGPRs live, made the compiler spill 100-2000 SGPRs in the scans: round 4)
 template <class T, int W>
 __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
-    typedef uint32_t s16u __attribute__((ext_vector_type(16)));
     T acc = 0;
 #pragma unroll
-    for (int c = 0; c < W; c += 16) {
-        s16u k0, k1;
+    for (int c = 0; c < W; c += 8) {
+        uint64_t k0, k1, k2, k3, k4, k5, k6, k7;
         const uint64_t a = rfl64((uint64_t)(cols + c));  // the table address must live in SGPRs
         asm volatile(
-            "s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+            "s_load_dwordx2 %0, %8, 0x0\n\ts_load_dwordx2 %1, %8, 0x8\n\t"
+            "s_load_dwordx2 %2, %8, 0x10\n\ts_load_dwordx2 %3, %8, 0x18\n\t"
+            "s_load_dwordx2 %4, %8, 0x20\n\ts_load_dwordx2 %5, %8, 0x28\n\t"
+            "s_load_dwordx2 %6, %8, 0x30\n\ts_load_dwordx2 %7, %8, 0x38\n\t"
+            "s_waitcnt lgkmcnt(0)"
             // early-clobber: a returning load must never overwrite the shared address operand
-            : "=&s"(k0), "=&s"(k1)
+            : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
             : "s"(a)
             : "memory");
+        const uint64_t k[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t lo = j < 8 ? k0[2 * j] : k1[2 * (j - 8)];
-            const uint32_t hi = j < 8 ? k0[2 * j + 1] : k1[2 * (j - 8) + 1];
-            const T col = W == 64 ? (T)(((uint64_t)hi << 32) | lo) : (T)lo;
-            if ((r >> (W - 1 - (c + j))) & 1) acc ^= col;
-        }
+        for (int j = 0; j < 8; ++j)
+            if ((r >> (W - 1 - (c + j))) & 1) acc ^= (T)k[j];
     }
     return acc;
 }
@@ -1623,6 +1622,22 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
 //    holds their place in the sequence.
 // Host side: engine.cpp list_stream (d_wave_buf = start buffer per wave, nw + 1; d_tile_prefix = start
 // group within it, nw + 1; then the group prefix wq, nw + 1; ntiles = groups in the list).
+// A part of a buffer cut between waves joins the buffer's other parts in this workgroup in an LDS
+// slot (engine.cpp list_stream's join descriptor d: slot d & 15, d >> 4 & 15 parts expected):
+// value XOR, then parts and groups counted in one add; the part completing the count gets the
+// slot's value and group count (lane 0).  LDS atomics: no device round trip and no wait on the
+// payload ring (round 4: returning device atomics for every cut part cost ragged lists ~6 us).
+constexpr uint32_t kListJoinSlots = 9;
+static_assert(kLocalOff + 16 * kListJoinSlots <= kStreamLds, "list join slots");
+template <class T, class F>
+__device__ __forceinline__ void list_join(uint64_t *slot, uint32_t d, T r, uint32_t groups, F &&done) {
+    __hip_atomic_fetch_xor(slot, (uint64_t)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t add = (1ull << 32) | groups;
+    const uint64_t now = __hip_atomic_fetch_add(slot + 1, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP) + add;
+    if ((uint32_t)(now >> 32) != ((d >> 4) & 15u)) return;
+    done(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), (uint32_t)now);
+}
+
 struct LBuf {        // the cursor's buffer (wave-uniform)
     uint64_t b;      // buffer index
     uint64_t vb;     // virtual start of group 0 (main start - pad)
@@ -1697,6 +1712,9 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     const uint64_t *xinv = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidXinvWord);
     const uint64_t *gsh = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGshiftWord);
     const uint64_t *gmc = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGmWord);
+    const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
+    uint64_t *const jslots = (uint64_t *)(cb + (kLocalOff - kBKOff));  // 9 x {value, parts << 32 | groups}
+    if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;  // b0 < nbuf then (the host's wbuf is nbuf only past the groups)
@@ -1804,8 +1822,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             finalize<true>(p, b, fin, eng);
         }
     };
-    uint64_t hb = ~0ull;  // the held part: buffer, value, groups, the buffer's groups
-    uint32_t hr = 0, hn = 0, hvg = 0;
+    uint32_t nparts = 0;  // parts this wave has finished
     // the part [ga, g) ends: its share, moved to the buffer's end, finishes the buffer or joins it
     auto part_finish = [&]() {
 #ifdef AMDCRC_XP_LIST_NOFINISH  // experiment builds only (timing; results wrong): a part stores its lane-0 braid
@@ -1820,18 +1837,23 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
                 if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
         }
+        const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
+        ++nparts;
         if (ga == 0 && g == sc.vg) {
             if (lane == 0) finalize<true>(p, sc.b, r, eng);
             return;
         }
-        // a buffer cut between waves: its parts meet in the accumulator through returning atomics,
-        // whose wait would drain the payload ring -- so a part ending inside the scan (the wave's first,
-        // the tail of a buffer begun by the wave before) is held and published after the scan
-        if (q < nq && hb == ~0ull) {
-            hb = sc.b, hr = r, hn = g - ga, hvg = sc.vg;
+        if (lane != 0) return;
+        if (!(d & 0x8000u)) {  // (no descriptor: the device accumulator directly)
+            publish(sc.b, r, g - ga, sc.vg);
             return;
         }
-        if (lane == 0) publish(sc.b, r, g - ga, sc.vg);
+        list_join(jslots + 2 * (d & 15u), d, r, g - ga, [&](uint64_t v, uint32_t groups) {
+            if (d & 0x100u)
+                publish(sc.b, (uint32_t)v, groups, sc.vg);
+            else
+                finalize<true>(p, sc.b, (uint32_t)v, eng);
+        });
     };
     part_begin();
     auto step = [&](W8Group &cur, W8Group &nxt, bool first) {
@@ -1867,7 +1889,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (q < nq) step(rc, rb, false);
     }
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
-    if (hb != ~0ull && lane == 0) publish(hb, hr, hn, hvg);
     // trailing buffers without a main region
     while (sc.b + 1 < b_end) {
         sc = lbuf_at(p, sc.b + 1);
@@ -2882,6 +2903,9 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     const uint64_t *xinv = p.d_pcols + kXcdXinvU64;
     const uint64_t *gsh = p.d_pcols + kXcdGshiftU64;
     const uint64_t *gmc = p.d_pcols + kXcdGmU64;
+    const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
+    __shared__ uint64_t jslots[2 * kListJoinSlots];   // {value, parts << 32 | groups}
+    if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;
@@ -2964,8 +2988,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             finalize<true>(p, b, fin, eng);
         }
     };
-    uint64_t hb = ~0ull, hr = 0;  // the held part: buffer, value, groups, the buffer's groups
-    uint32_t hn = 0, hvg = 0;
+    uint32_t nparts = 0;  // parts this wave has finished
     auto part_finish = [&]() {
         uint64_t r = wave_xor64_s(eng.mulK(u));
         const uint32_t mg = sc.vg - g;  // groups after the part
@@ -2975,17 +2998,24 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
                 if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
         }
+        const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
+        ++nparts;
         if (ga == 0 && g == sc.vg) {
             if (lane == 0) finalize<true>(p, sc.b, r, eng);
             return;
         }
-        // a cut buffer's part ending inside the scan is held until the scan ends (see
-        // crc32_list_stream_kernel: the returning atomics' wait would drain the payload ring)
-        if (q < nq && hb == ~0ull) {
-            hb = sc.b, hr = r, hn = g - ga, hvg = sc.vg;
+        if (lane != 0) return;
+        if (!(d & 0x8000u)) {  // (no descriptor: the device accumulator directly)
+            publish(sc.b, r, g - ga, sc.vg);
             return;
         }
-        if (lane == 0) publish(sc.b, r, g - ga, sc.vg);
+        // a buffer cut between waves: its parts in this workgroup join in LDS (list_join)
+        list_join(jslots + 2 * (d & 15u), d, r, g - ga, [&](uint64_t v, uint32_t groups) {
+            if (d & 0x100u)
+                publish(sc.b, v, groups, sc.vg);
+            else
+                finalize<true>(p, sc.b, v, eng);
+        });
     };
     part_begin();
     auto step = [&](B64Group &cur, B64Group &nxt) {
@@ -3018,7 +3048,6 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         if (q < nq) step(rc, rb);
     }
     drain();
-    if (hb != ~0ull && lane == 0) publish(hb, hr, hn, hvg);
     while (sc.b + 1 < b_end) {  // trailing buffers without a main region
         sc = lbuf_at(p, sc.b + 1);
         finish_empty();
@@ -3681,96 +3710,40 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
     ((T *)out)[ix] = (T)~s;
 }
 
-// Event-stream framing check, a lane pair per message (aws_crt_amd_eventstream_crcs).  Both lanes read
-// total_length and headers_length from the message's prelude (big-endian), refuse lengths outside
-// [16, limit - offset] and headers longer than total - 16 before touching the body.  The message CRC
-// spans n = total - 4 bytes: the pair's second lane folds the last h = 64 floor(n / 128) bytes from 0
-// and the first lane the prelude (-> prelude CRC) and the bytes up to n - h from ~0, its register then
-// moved past the second lane's bytes (times x^(8h): eight nibble lookups, h < 1 KiB; longer messages
-// stay on the first lane); the pair XORs its registers (DPP) and compares both CRCs with the big-endian
-// values stored at offset 8 and total - 4.  Both lanes run one code path with their own (state, span),
-// so a wave holds 32 messages at half the longest chain of one lane per message (round 4; the
-// one-lane kernel took 28.3-29.4 us per 65 MiB call, profiles/r04/f-h).  Folds on LaneW8.
+// Event-stream framing check, one lane per message (aws_crt_amd_eventstream_crcs): the lane reads
+// total_length and headers_length from the message's prelude (big-endian), refuses lengths outside
+// [16, limit - offset] and headers longer than total - 16 before touching the body, then folds the
+// prelude (-> prelude CRC) and continues over the headers and payload (-> message CRC, the running
+// form of CRC32 over [0, total - 4)), and compares both with the big-endian values stored at offset 8
+// and total - 4.  Folds on the conflict-free tables (LaneW8).  Measured and dropped in round 4
+// (profiles/r04/f-i): deeper load rings (2-8 blocks of 64 bytes in flight: 37-39 us against 28-29),
+// four lanes per message on a quad braid (52-54 us), a lane pair per message (the second lane
+// folding the message tail: 42 us, twice the VALU instructions).
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
-constexpr uint32_t kEsShiftOff = kLaneW8Lds;                  // [m < 16][nibble k < 8][v < 16]: (v << 4k) * x^(512 m)
-constexpr uint32_t kEsSplitMax = 16;                          // second lane for h = 64 m, m < 16
-constexpr uint32_t kEsLds = kEsShiftOff + kEsSplitMax * 8 * 16 * 4;
-static_assert(2 * kEsLds <= 160 * 1024, "two eventstream_kernel workgroups per CU");
-
-template <uint32_t POLY>
-struct EsX512 {  // column b of x^512 (64 bytes): (1 << b) * x^512
-    uint32_t c[32];
-    constexpr EsX512() : c() {
-        const uint64_t k = gf2_xpow8n(64, POLY, 32);
-        for (int b = 0; b < 32; ++b) c[b] = (uint32_t)gf2_mulmod(1ull << b, k, POLY, 32);
-    }
-};
-// threads < 128: entry (k, v) = i for every m, each m the previous times x^512 (the caller syncs)
-template <uint32_t POLY>
-__device__ __forceinline__ void es_shift_tables(char *lds) {
-    constexpr EsX512<POLY> X{};
-    const uint32_t i = threadIdx.x;
-    if (i >= 128) return;
-    uint32_t *t = (uint32_t *)(lds + kEsShiftOff);
-    uint32_t val = (i & 15u) << (4 * (i >> 4));
-    t[i] = val;
-    for (uint32_t m = 1; m < kEsSplitMax; ++m) {
-        uint32_t nv = 0;
-#pragma unroll
-        for (int b = 0; b < 32; ++b) nv ^= ((val >> b) & 1u) ? X.c[b] : 0u;
-        val = nv;
-        t[128 * m + i] = val;
-    }
-}
-__device__ __forceinline__ uint32_t es_shift(const char *lds, uint32_t r, uint32_t m) {
-    const uint32_t *t = (const uint32_t *)(lds + kEsShiftOff) + 128 * m;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc ^= t[16 * k + ((r >> (4 * k)) & 15u)];
-    return acc;
-}
 
 __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
-    __shared__ __attribute__((aligned(16))) char lds[kEsLds];
-    es_shift_tables<kPoly32>(lds);
-    lane_w8_tables<kPoly32>(lds);  // ends with the workgroup barrier
+    __shared__ __attribute__((aligned(16))) char lds[kLaneW8Lds];
+    lane_w8_tables<kPoly32>(lds);
     LaneW8 f;
     f.init(lds, threadIdx.x & 63u);
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t m = gid >> 1;
-    const uint32_t second = (uint32_t)gid & 1u;
-    const bool live = m < p.count;
-    bool ok = false;
-    const uint8_t *q = p.base;
-    uint64_t total = 0, h = 0;
-    if (live) {
-        const uint64_t off = p.d_offsets[m];
-        if (off <= p.limit && p.limit - off >= 16) {
-            q = p.base + off;
-            total = be32(q);
-            const uint64_t headers = be32(q + 4);
-            // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
-            // (headers_length > total_length - 16): malformed, whatever the CRCs say
-            ok = total >= 16 && total <= p.limit - off && headers <= total - 16;
+    const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= p.count) return;
+    const uint64_t off = p.d_offsets[m];
+    uint32_t pre = 0, msg = 0, st = 4u;  // bit 2: malformed
+    if (off <= p.limit && p.limit - off >= 16) {
+        const uint8_t *q = p.base + off;
+        const uint64_t total = be32(q), headers = be32(q + 4);
+        // aws-c-event-stream's decoder refuses a prelude whose headers do not fit the message
+        // (headers_length > total_length - 16): malformed, whatever the CRCs say
+        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
+            uint32_t s = lane_scan<uint32_t>(~0u, q, 8, f);
+            pre = ~s;
+            s = lane_scan<uint32_t>(s, q + 8, total - 12, f);
+            msg = ~s;
+            st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
         }
-    }
-    const uint64_t n = ok ? total - 4 : 0;
-    h = 64 * (n / 128);
-    if (h >= 64 * (uint64_t)kEsSplitMax) h = 0;
-    uint32_t pre = 0, s = 0;
-    if (ok) pre = ~lane_scan<uint32_t>(~0u, q, 8, f);
-    const uint8_t *ps = second ? q + (n - h) : q + 8;
-    const uint64_t pn = !ok ? 0 : second ? h : n - 8 - h;
-    s = lane_scan<uint32_t>(second ? 0u : ~pre, ps, pn, f);
-    const uint32_t part = es_shift(lds, s, second ? 0u : (uint32_t)(h / 64));
-    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    if (!live || second) return;
-    uint32_t msg = 0, st = 4u;  // bit 2: malformed
-    if (ok) {
-        msg = ~(part ^ other);
-        st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
     }
     p.d_prelude_crc[m] = pre;
     p.d_message_crc[m] = msg;
@@ -3939,7 +3912,7 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
 
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
     if (p->count == 0) return 0;
-    const uint64_t blocks = (2 * p->count + 255) / 256;  // a lane pair per message
+    const uint64_t blocks = (p->count + 255) / 256;
     launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
     return (int)hipGetLastError();
 }

@@ -1060,7 +1060,7 @@ int list_stream(Device *d, int alg, const void *const *ptrs, const size_t *lens,
     for (size_t i = 0; i < count; ++i) gp[i + 1] = gp[i] + (mains[i] + gb - 1) / gb;
     const uint64_t ng = gp[count];
     const uint64_t blocks = list_stream_blocks(d, ng, total), nw = blocks * 8;
-    const size_t words = count * 2 + 3 * (nw + 1);
+    const size_t words = count * 2 + 4 * (nw + 1);
     uint64_t *h;
     int rc = stage_begin(d, s, words * 8, (void **)&h);
     if (rc) return rc;
@@ -1083,6 +1083,34 @@ int list_stream(Device *d, int alg, const void *const *ptrs, const size_t *lens,
         wq[w] = q0;
         woff[w] = b < count && gp[b + 1] > gp[b] ? q0 - gp[b] : 0;
         if (woff[w]) split = true;
+    }
+    // join descriptors of buffers cut between waves (crc32/64_list_stream_kernel): the parts of such a
+    // buffer inside one workgroup (8 waves) meet in an LDS slot -- slot = its first wave in the
+    // workgroup, or 8 when it began in an earlier workgroup -- and the last of the `expected` parts
+    // to arrive finishes the buffer, or publishes the workgroup's share when the buffer also lies in
+    // another workgroup.  Word w: bits 0-15 the descriptor of wave w's first part, 16-31 of its last
+    // (bit 15 valid, 0-3 slot, 4-7 expected, 8 global).
+    uint64_t *wjoin = wq + nw + 1;
+    std::fill(wjoin, wjoin + nw + 1, 0ull);
+    if (split) {
+        auto wave_of = [&](uint64_t q) {  // the wave whose group range holds group q
+            return (uint64_t)(std::upper_bound(wq, wq + nw + 1, q) - wq) - 1;
+        };
+        for (size_t i = 0; i < count; ++i) {
+            if (gp[i + 1] == gp[i]) continue;
+            const uint64_t ws = wave_of(gp[i]), we = wave_of(gp[i + 1] - 1);
+            if (ws == we) continue;  // whole inside one wave
+            for (uint64_t w = ws; w <= we; ++w) {
+                if (wq[w + 1] == wq[w]) continue;  // a wave without groups holds no part
+                const uint64_t wg0 = w & ~7ull, r0 = std::max(ws, wg0), r1 = std::min(we, wg0 + 7);
+                uint64_t parts = 0;
+                for (uint64_t v = r0; v <= r1; ++v) parts += wq[v + 1] > wq[v] ? 1 : 0;
+                const uint64_t desc = 0x8000u | (ws >= wg0 ? ws - wg0 : 8u) | (parts << 4) |
+                                      ((ws < wg0 || we > wg0 + 7) ? 0x100u : 0u);
+                if (wq[w] >= gp[i]) wjoin[w] |= desc;              // the buffer is wave w's first part
+                if (wq[w + 1] <= gp[i + 1]) wjoin[w] |= desc << 16;  // ... and/or its last part
+            }
+        }
     }
     const uint64_t *dd;
     if ((rc = stage_end(d, s, words * 8, (const void **)&dd))) return rc;

@@ -112,6 +112,7 @@ struct JobImpl {
     // AWS_CRT_AMD_INGEST_TRACE=1: one stderr line per job (claims and when each side ran out of work)
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::atomic<uint64_t> lane_claims{0}, lane_end_ns{0}, host_end_ns{0}, host_claims{0};
+    std::atomic<uint64_t> lane_wait_ns{0}, lane_issue_ns{0}, lane_first_ns{0};
     uint64_t since_ns() const {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -134,6 +135,7 @@ struct JobImpl {
         workers.clear(), rc.store(0), err.clear();
         t0 = std::chrono::steady_clock::now();
         lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
+        lane_wait_ns.store(0), lane_issue_ns.store(0), lane_first_ns.store(0);
     }
     void set_error(int code, const char *m) noexcept {
         std::lock_guard<std::mutex> g(err_mu);
@@ -292,7 +294,9 @@ void device_worker_body(JobImpl *job, int dev) {
     // copy a slot's results back into the job once its scan has completed
     auto harvest = [&](int k) {
         if (!L.used[k]) return true;
+        const uint64_t w0 = job->since_ns();
         if (hipEventSynchronize(L.done[k]) != hipSuccess) return false;
+        job->lane_wait_ns.fetch_add(job->since_ns() - w0, std::memory_order_relaxed);
         const std::vector<size_t> &ps = slot_pieces[k];
         for (size_t j = 0; j < ps.size(); ++j)
             job->piece_val[ps[j]] = osz == 8 ? ((const uint64_t *)L.hres[k])[j] : ((const uint32_t *)L.hres[k])[j];
@@ -308,7 +312,8 @@ void device_worker_body(JobImpl *job, int dev) {
         // claim a run of pieces for slot k: contiguous in the slot, in order (pieces are at most a slot)
         size_t a, b;
         if (!claim(job, dev_budget(job), kMaxPiecesPerSlot, &a, &b)) break;
-        job->lane_claims.fetch_add(1, std::memory_order_relaxed);
+        const uint64_t i0 = job->since_ns();
+        if (job->lane_claims.fetch_add(1, std::memory_order_relaxed) == 0) job->lane_first_ns.store(i0);
         std::vector<size_t> &ps = slot_pieces[k];
         ps.clear();
         for (size_t q = a; q < b; ++q) ps.push_back(q);
@@ -368,7 +373,12 @@ void device_worker_body(JobImpl *job, int dev) {
         LANE_TRY(hipMemcpyAsync(L.dseed[k], L.hseed[k], ps.size() * osz, hipMemcpyHostToDevice, L.copy));
         LANE_TRY(hipEventRecord(L.copied[k], L.copy));
         LANE_TRY(hipStreamWaitEvent(L.comp, L.copied[k], 0));
-        const int rc = aws_crt_amd_checksum_list(job->alg, dptrs.data(), dlens.data(), ps.size(), L.dseed[k], L.dres[k], L.comp);
+        // pieces of one length (part buffers of one size) lie back to back in the slot: a strided
+        // batch, with no per-buffer descriptors to build and stage
+        bool uniform = dlens[0] % 16 == 0 || ps.size() == 1;
+        for (size_t j = 1; uniform && j < dlens.size(); ++j) uniform = dlens[j] == dlens[0];
+        const int rc = uniform ? aws_crt_amd_checksum_strided(job->alg, dptrs[0], dlens[0], dlens[0], ps.size(), L.dseed[k], L.dres[k], L.comp)
+                               : aws_crt_amd_checksum_list(job->alg, dptrs.data(), dlens.data(), ps.size(), L.dseed[k], L.dres[k], L.comp);
         if (rc) {
             job->set_error(rc, aws_crt_amd_last_error());
             return;
@@ -378,6 +388,7 @@ void device_worker_body(JobImpl *job, int dev) {
         // the slot's copy stream must not overwrite it before the scan has read it: the next use of
         // slot k waits on done[k] in harvest(); the copy stream also waits for it explicitly
         L.used[k] = true;
+        job->lane_issue_ns.fetch_add(job->since_ns() - i0, std::memory_order_relaxed);
         k = (k + 1) % kSlots;
         LANE_TRY(hipStreamWaitEvent(L.copy, L.done[k], 0));  // slot k (next) free on the device side
     }
@@ -602,7 +613,11 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         uint64_t total = 0;
         for (size_t i = 0; i < count; ++i) total += lens[i];
         const size_t share = host_threads(SIZE_MAX);
-        size_t H = want_host < 0 || G == 0 ? (share > (size_t)G ? share - (size_t)G : 1) : (size_t)want_host;
+        // (auto: one CPU of the share per lane for its thread, and one for the HIP runtime's own
+        // threads while lanes run -- a share run full by host threads delayed the lane's HIP calls:
+        // profiles/r04/i, a lane at 15 GiB/s beside 15 host threads)
+        const size_t reserve = G ? (size_t)G + 1 : 0;
+        size_t H = want_host < 0 || G == 0 ? (share > reserve ? share - reserve : 1) : (size_t)want_host;
         if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
         // pieces, buffer by buffer, in job order
@@ -686,10 +701,12 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
         if (trace && *trace && *trace != '0')
             std::fprintf(stderr,
                          "{\"ingest_trace\": 1, \"pieces\": %zu, \"host_threads\": %zu, \"lanes\": %d, \"device_bytes\": %llu, "
-                         "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f}\n",
+                         "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f, "
+                         "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_wait_ms\": %.3f}\n",
                          J.pieces.size(), J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
                          (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
-                         J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6);
+                         J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6, J.lane_first_ns.load() * 1e-6,
+                         J.lane_issue_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6);
         if (rc) t_err = J.err;
         job_give(job);
         return rc;

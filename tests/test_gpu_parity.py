@@ -414,6 +414,32 @@ def test_list_long_buffers_cut_over_all_waves(engine, alg):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("alg", ["crc32c", "crc64nvme"])
+@pytest.mark.parametrize("nbuf,lo,hi", [(1024, 32 << 10, 96 << 10), (3000, 4097, 40000), (200, 200 << 10, 1 << 20)])
+def test_ragged_list_workgroup_joins(engine, alg, nbuf, lo, hi):
+    """Ragged lists on the list streaming scans where most buffers are cut between waves (the
+    list probe's shape, scaled): a cut buffer's parts inside one workgroup join in LDS slots and
+    finish there, or publish the workgroup's share when the buffer continues into another
+    workgroup (slot 8 for a buffer begun in an earlier one); buffers over one, two and many waves.
+    Random starts and lengths, seeds on all."""
+    import torch
+
+    rng = random.Random(nbuf + lo + ALG[alg])
+    lens = [rng.randrange(lo, hi) for _ in range(nbuf)]
+    offs, pos = [], 5
+    for ln in lens:
+        offs.append(pos)
+        pos += ln + rng.randrange(0, 64)
+    d = dev_random(pos + 64, nbuf + 0x70)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_fuzz_lengths_alignments_seeds(engine, alg):
     """GPU-vs-oracle differential fuzzing: 2000 buffers of uniformly random length
