@@ -112,7 +112,7 @@ struct JobImpl {
     // AWS_CRT_AMD_INGEST_TRACE=1: one stderr line per job (claims and when each side ran out of work)
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::atomic<uint64_t> lane_claims{0}, lane_end_ns{0}, host_end_ns{0}, host_claims{0};
-    std::atomic<uint64_t> lane_wait_ns{0}, lane_issue_ns{0}, lane_first_ns{0};
+    std::atomic<uint64_t> lane_wait_ns{0}, lane_issue_ns{0}, lane_first_ns{0}, lane_stage_ns{0};
     uint64_t since_ns() const {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -135,7 +135,7 @@ struct JobImpl {
         workers.clear(), rc.store(0), err.clear();
         t0 = std::chrono::steady_clock::now();
         lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
-        lane_wait_ns.store(0), lane_issue_ns.store(0), lane_first_ns.store(0);
+        lane_wait_ns.store(0), lane_issue_ns.store(0), lane_first_ns.store(0), lane_stage_ns.store(0);
     }
     void set_error(int code, const char *m) noexcept {
         std::lock_guard<std::mutex> g(err_mu);
@@ -370,6 +370,7 @@ void device_worker_body(JobImpl *job, int dev) {
             job->set_error(AWS_CRT_AMD_ERR_HIP, "host-to-device copy");
             return;
         }
+        job->lane_stage_ns.fetch_add(job->since_ns() - i0, std::memory_order_relaxed);
         LANE_TRY(hipMemcpyAsync(L.dseed[k], L.hseed[k], ps.size() * osz, hipMemcpyHostToDevice, L.copy));
         LANE_TRY(hipEventRecord(L.copied[k], L.copy));
         LANE_TRY(hipStreamWaitEvent(L.comp, L.copied[k], 0));
@@ -613,10 +614,11 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         uint64_t total = 0;
         for (size_t i = 0; i < count; ++i) total += lens[i];
         const size_t share = host_threads(SIZE_MAX);
-        // (auto: one CPU of the share per lane for its thread, and one for the HIP runtime's own
-        // threads while lanes run -- a share run full by host threads delayed the lane's HIP calls:
-        // profiles/r04/i, a lane at 15 GiB/s beside 15 host threads)
-        const size_t reserve = G ? (size_t)G + 1 : 0;
+        // (auto: one CPU of the share per lane for its thread and three for the HIP runtime's own
+        // threads while lanes run -- a share run full by host threads stalled the lane's staging of a
+        // 32 MiB claim for ~1 ms: C2 parts from pinned memory at 116 GiB/s with 14 host threads, 191
+        // with 12, profiles/r04/l)
+        const size_t reserve = G ? (size_t)G + 3 : 0;
         size_t H = want_host < 0 || G == 0 ? (share > reserve ? share - reserve : 1) : (size_t)want_host;
         if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
@@ -702,11 +704,11 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
             std::fprintf(stderr,
                          "{\"ingest_trace\": 1, \"pieces\": %zu, \"host_threads\": %zu, \"lanes\": %d, \"device_bytes\": %llu, "
                          "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f, "
-                         "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_wait_ms\": %.3f}\n",
+                         "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_stage_ms\": %.3f, \"lane_wait_ms\": %.3f}\n",
                          J.pieces.size(), J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
                          (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
                          J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6, J.lane_first_ns.load() * 1e-6,
-                         J.lane_issue_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6);
+                         J.lane_issue_ns.load() * 1e-6, J.lane_stage_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6);
         if (rc) t_err = J.err;
         job_give(job);
         return rc;

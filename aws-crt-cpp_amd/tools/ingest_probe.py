@@ -47,11 +47,13 @@ def main(total_mib=1280, reps=3):
             row = {"memory": mem, "part_bytes": part, "parts": n}
             cb = eng.CpuBatch(eng.CRC32C, ptrs, lens, threads=threads)
             row["cpu_batch"] = round(total / best(cb.run, reps) / 2**30, 1)
-            for name, nd, ht in (("host_only", -1, -1), ("hybrid", 0, -1), ("devices_only", 0, 0)):
+            legs = [("host_only", -1, -1), ("hybrid", 0, -1), ("devices_only", 0, 0)]
+            legs += [(f"hybrid_h{h}", 0, h) for h in (int(x) for x in os.environ.get("INGEST_PROBE_H", "").split(",") if x)]
+            for name, nd, ht in legs:
                 job = eng.HostJob(eng.CRC32C, ptrs, lens, ndevices=nd, host_threads=ht)
                 row[name] = round(total / best(job.run, reps) / 2**30, 1)
-                if name == "hybrid":
-                    row["hybrid_device_share"] = round(job.device_bytes / total, 3)
+                if name.startswith("hybrid"):
+                    row[name + "_device_share"] = round(job.device_bytes / total, 3)
             res.append(row)
             print(json.dumps(row), flush=True)
     dev = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
