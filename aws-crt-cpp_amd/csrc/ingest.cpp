@@ -113,6 +113,7 @@ struct JobImpl {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::atomic<uint64_t> lane_claims{0}, lane_end_ns{0}, host_end_ns{0}, host_claims{0};
     std::atomic<uint64_t> lane_wait_ns{0}, lane_issue_ns{0}, lane_first_ns{0}, lane_stage_ns{0};
+    std::atomic<uint64_t> lane_mirror_bytes{0}, lane_pin_checks{0}, lane_pin_ns{0};
     uint64_t since_ns() const {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -136,6 +137,7 @@ struct JobImpl {
         t0 = std::chrono::steady_clock::now();
         lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
         lane_wait_ns.store(0), lane_issue_ns.store(0), lane_first_ns.store(0), lane_stage_ns.store(0);
+        lane_mirror_bytes.store(0), lane_pin_checks.store(0), lane_pin_ns.store(0);
     }
     void set_error(int code, const char *m) noexcept {
         std::lock_guard<std::mutex> g(err_mu);
@@ -218,6 +220,7 @@ constexpr size_t kHybridPiece = 8u << 20;  // piece size of hybrid jobs (host th
 constexpr uint64_t kMinDevClaim = 1u << 20;
 constexpr uint64_t kHostClaim = 1u << 20;
 constexpr uint64_t kHostClaimMax = 64u << 20;
+constexpr size_t kAutoLanesMaxShare = 12;  // auto jobs use device lanes below this many host threads
 
 // Claim the next run of pieces [*a, *b): at least one, at most max_pieces, at most `budget` bytes
 // past the first.  false when the job has no unclaimed piece left.
@@ -338,7 +341,12 @@ void device_worker_body(JobImpl *job, int dev) {
         for (size_t j = 0; j < ps.size(); ++j) {
             const Piece &pc = job->pieces[ps[j]];
             const uint8_t *src = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
-            if (src != src_end) cur_pinned = pc.len && host_pinned(src);
+            if (src != src_end) {
+                const uint64_t c0 = job->since_ns();
+                cur_pinned = pc.len && host_pinned(src);
+                job->lane_pin_checks.fetch_add(1, std::memory_order_relaxed);
+                job->lane_pin_ns.fetch_add(job->since_ns() - c0, std::memory_order_relaxed);
+            }
             src_end = src + pc.len;
             const uint8_t *from = src;
             if (pc.len && !cur_pinned) {
@@ -347,6 +355,7 @@ void device_worker_body(JobImpl *job, int dev) {
                     mir = (uint8_t *)L.hmirror[k];
                 }
                 std::memcpy(mir + off, src, pc.len);
+                job->lane_mirror_bytes.fetch_add(pc.len, std::memory_order_relaxed);
                 from = mir + off;
             }
             if (run_len && run_src + run_len == from && run_dev + run_len == off) {
@@ -614,11 +623,17 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         uint64_t total = 0;
         for (size_t i = 0; i < count; ++i) total += lens[i];
         const size_t share = host_threads(SIZE_MAX);
+        // Auto (ndevices 0, host_threads -1): device lanes only for a CPU-poor share.  A lane moves
+        // ~50 GiB/s over PCIe, about what 2.5 host threads fold (~20 GiB/s each, AVX-512 VPCLMULQDQ),
+        // and takes a thread plus headroom for the HIP runtime beside it; on the pool's 16-CPU share
+        // the hybrid job measured 107-306 GiB/s against 284-348 host-only (profiles/r04/m-o), so the
+        // default there is the host path.  Lanes stay on when asked for explicitly.
+        if (ndevices == 0 && want_host < 0 && share >= kAutoLanesMaxShare) G = 0;
         // (auto: one CPU of the share per lane for its thread and three for the HIP runtime's own
         // threads while lanes run -- a share run full by host threads stalled the lane's staging of a
         // 32 MiB claim for ~1 ms: C2 parts from pinned memory at 116 GiB/s with 14 host threads, 191
         // with 12, profiles/r04/l)
-        const size_t reserve = G ? (size_t)G + 3 : 0;
+        const size_t reserve = G ? 4 * (size_t)G : 0;
         size_t H = want_host < 0 || G == 0 ? (share > reserve ? share - reserve : 1) : (size_t)want_host;
         if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
@@ -704,11 +719,14 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
             std::fprintf(stderr,
                          "{\"ingest_trace\": 1, \"pieces\": %zu, \"host_threads\": %zu, \"lanes\": %d, \"device_bytes\": %llu, "
                          "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f, "
-                         "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_stage_ms\": %.3f, \"lane_wait_ms\": %.3f}\n",
+                         "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_stage_ms\": %.3f, \"lane_wait_ms\": %.3f, "
+                         "\"lane_mirror_bytes\": %llu, \"lane_pin_checks\": %llu, \"lane_pin_ms\": %.3f}\n",
                          J.pieces.size(), J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
                          (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
                          J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6, J.lane_first_ns.load() * 1e-6,
-                         J.lane_issue_ns.load() * 1e-6, J.lane_stage_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6);
+                         J.lane_issue_ns.load() * 1e-6, J.lane_stage_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6,
+                         (unsigned long long)J.lane_mirror_bytes.load(), (unsigned long long)J.lane_pin_checks.load(),
+                         J.lane_pin_ns.load() * 1e-6);
         if (rc) t_err = J.err;
         job_give(job);
         return rc;

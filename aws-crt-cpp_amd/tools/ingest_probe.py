@@ -49,6 +49,8 @@ def main(total_mib=1280, reps=3):
             row["cpu_batch"] = round(total / best(cb.run, reps) / 2**30, 1)
             legs = [("host_only", -1, -1), ("hybrid", 0, -1), ("devices_only", 0, 0)]
             legs += [(f"hybrid_h{h}", 0, h) for h in (int(x) for x in os.environ.get("INGEST_PROBE_H", "").split(",") if x)]
+            if os.environ.get("INGEST_PROBE_AGAIN"):
+                legs.append(("hybrid_again", 0, -1))  # the default once more, after the other legs
             for name, nd, ht in legs:
                 job = eng.HostJob(eng.CRC32C, ptrs, lens, ndevices=nd, host_threads=ht)
                 row[name] = round(total / best(job.run, reps) / 2**30, 1)

@@ -298,8 +298,9 @@ AWS_CRT_AMD_API int aws_crt_amd_checksum_host(
  * to the HOST array h_out (u32 CRC32/32C, u64 CRC64NVME/XXH64/XXH3_64, two u64 {high, low}
  * XXH3_128) once aws_crt_amd_job_wait(job) returns 0.  Buffers, seeds and h_out must stay valid
  * until then.  CRCs are split between the host threads of the process's CPU share and `ndevices`
- * GPUs (0 = all visible): both take runs of pieces from one cursor over the job (work stealing), so
- * a job is never slower than the host path alone.  Each device runs a three-slot pipeline (H2D on a
+ * GPUs (0 = all visible; by default only when the CPU share is under 12 threads -- on a larger share
+ * the host path alone is faster than a PCIe lane plus the threads it displaces): both take runs of
+ * pieces from one cursor over the job (work stealing).  Each device runs a three-slot pipeline (H2D on a
  * copy stream overlapping the scans; 32 MiB slots); buffers longer than a piece (8 MiB, or a slot
  * when no host thread takes part) are cut into pieces folded with Combine.  Registered / pinned
  * memory is DMA'd in place; pageable memory goes through pinned mirrors.  xxHash (a serial chain per
@@ -317,11 +318,13 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(
     int ndevices,
     struct aws_crt_amd_job **job);
 /*
- * aws_crt_amd_host_submit with options.  ndevices: 0 = every visible device, n = the first n, < 0 =
- * none (the host path alone, on the CPU share).  host_threads: -1 = the CPU share less one thread per
- * device lane (what aws_crt_amd_host_submit does), 0 = devices only (the PCIe-bound pipeline), n = n
- * host threads beside the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the
- * devices checksummed.
+ * aws_crt_amd_host_submit with options.  ndevices: 0 = every visible device (with host_threads -1:
+ * only when the CPU share is under 12 threads), n > 0 = the first n, < 0 = none (the host path alone,
+ * on the CPU share).  host_threads: -1 = the CPU share less four threads per device lane (the lane's
+ * own and the HIP runtime's), 0 = devices only (the PCIe-bound pipeline), n = n host threads beside
+ * the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the devices
+ * checksummed.  AWS_CRT_AMD_INGEST_TRACE=1 prints one JSON line per job to stderr (claims, when each
+ * side ran out of work, the lanes' staging / issue / wait times).
  */
 struct aws_crt_amd_ingest_options {
     int ndevices;

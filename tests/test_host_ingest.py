@@ -58,8 +58,9 @@ def test_host_job_pageable(engine, alg, host_threads):
 @pytest.mark.parametrize("alg", ["crc32c", "crc64nvme"])
 def test_host_job_hybrid_split(engine, alg):
     """A hybrid job's pieces go to the host threads and the device lane (both take some), a
-    devices-only job's all to the lane, a host-threads-only split with a fixed thread count; buffers
-    cut into 8 MiB pieces at odd offsets join with Combine."""
+    devices-only job's all to the lane, a split with a fixed thread count beside the lane, and the
+    default policy (host path alone on a CPU share of 12+ threads); buffers cut into 8 MiB pieces at
+    odd offsets join with Combine."""
     import torch
 
     rng = random.Random(0x4B + ALG[alg])
@@ -74,13 +75,18 @@ def test_host_job_hybrid_split(engine, alg):
     ptrs = [host.data_ptr() + o for o in offs]
     seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
     want = [oracle.checksum(alg, a[o:o + n], s) for o, n, s in zip(offs, lens, seeds)]
-    for ht, check in ((-1, lambda d: 0 < d < total), (0, lambda d: d == total), (3, lambda d: 0 < d < total)):
-        job = engine.HostJob(ALG[alg], ptrs, lens, seeds, host_threads=ht)
+    import os
+    share = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    # (ndevices, host_threads): hybrid asked for, devices only, a fixed thread count beside the lane,
+    # and the default -- device lanes only for a CPU share under 12 threads (ingest.cpp)
+    for nd, ht, check in ((1, -1, lambda d: 0 < d < total), (0, 0, lambda d: d == total), (0, 3, lambda d: 0 < d < total),
+                          (0, -1, (lambda d: d == 0) if share >= 12 else (lambda d: 0 <= d <= total))):
+        job = engine.HostJob(ALG[alg], ptrs, lens, seeds, ndevices=nd, host_threads=ht)
         job.run()  # the first job may find the lane still being set up (it claims once it is ready)
         assert job.results() == want, ht
         job.run()
         assert job.results() == want, ht
-        assert check(job.device_bytes), (ht, job.device_bytes, total)
+        assert check(job.device_bytes), (nd, ht, job.device_bytes, total)
 
 
 @pytest.mark.gpu
