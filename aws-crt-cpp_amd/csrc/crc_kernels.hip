@@ -3526,7 +3526,6 @@ __device__ __forceinline__ void lane_tables(T (*tab)[256]) {
 // rotation, so each ds_read_b32 half-wave meets 32 distinct banks whatever the data.
 template <class T>
 struct TabFold {
-    static constexpr bool kPairs = false;
     const T (*tab)[256];
     __device__ __forceinline__ T word(T s, uint64_t v) const {
         if (sizeof(T) == 4) {
@@ -3580,7 +3579,6 @@ __device__ __forceinline__ void lane_w8_tables(char *lds) {
     __syncthreads();
 }
 struct LaneW8 {
-    static constexpr bool kPairs = false;
     const char *L;
     uint32_t cst8[8], sel8[8], c4;
     __device__ void init(const char *lds, uint32_t lane) {  // Braid32W8::init's schedule
@@ -3610,48 +3608,6 @@ struct LaneW8 {
         return s;
     }
 };
-
-// Slice-by-16 on plain tables T_0..T_15 (16 KiB, lane_tables16): a pair of words takes one step of 16
-// independent lookups, so a lane's dependent chain over a message is half as long as slice-by-8's
-// (event-stream framing: the chain, not bandwidth, bounds the one-lane-per-message scan, §3.5).
-struct Tab16Fold {
-    static constexpr bool kPairs = true;
-    const uint32_t (*tab)[256];
-    __device__ __forceinline__ uint32_t word(uint32_t s, uint64_t v) const {
-        const uint32_t lo = (uint32_t)v ^ s, hi = (uint32_t)(v >> 32);
-        return xor3(xor3(tab[7][lo & 0xff], tab[6][(lo >> 8) & 0xff], tab[5][(lo >> 16) & 0xff]),
-                    xor3(tab[4][lo >> 24], tab[3][hi & 0xff], tab[2][(hi >> 8) & 0xff]),
-                    tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24]);
-    }
-    __device__ __forceinline__ uint32_t word2(uint32_t s, uint64_t v0, uint64_t v1) const {
-        const uint32_t a = (uint32_t)v0 ^ s, b = (uint32_t)(v0 >> 32), c = (uint32_t)v1, d = (uint32_t)(v1 >> 32);
-        const uint32_t x0 = xor3(tab[15][a & 0xff], tab[14][(a >> 8) & 0xff], tab[13][(a >> 16) & 0xff]);
-        const uint32_t x1 = xor3(tab[12][a >> 24], tab[11][b & 0xff], tab[10][(b >> 8) & 0xff]);
-        const uint32_t x2 = xor3(tab[9][(b >> 16) & 0xff], tab[8][b >> 24], tab[7][c & 0xff]);
-        const uint32_t x3 = xor3(tab[6][(c >> 8) & 0xff], tab[5][(c >> 16) & 0xff], tab[4][c >> 24]);
-        const uint32_t x4 = xor3(tab[3][d & 0xff], tab[2][(d >> 8) & 0xff], tab[1][(d >> 16) & 0xff]);
-        return xor3(xor3(x0, x1, x2), xor3(x3, x4, tab[0][d >> 24]), 0u);
-    }
-    __device__ __forceinline__ uint32_t bytes(uint32_t s, uint64_t v, uint32_t nb) const {
-        for (uint32_t j = 0; j < nb; ++j, v >>= 8) s = (s >> 8) ^ tab[0][(s ^ (uint32_t)v) & 0xff];
-        return s;
-    }
-};
-template <uint32_t POLY>
-__device__ __forceinline__ void lane_tables16(uint32_t (*tab)[256]) {  // 256 threads
-    const uint32_t i = threadIdx.x;
-    uint32_t c = i;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? POLY : 0u);
-    tab[0][i] = c;
-    __syncthreads();
-#pragma unroll
-    for (int t = 1; t < 16; ++t) {
-        c = (c >> 8) ^ tab[0][c & 0xff];
-        tab[t][i] = c;
-    }
-    __syncthreads();
-}
 
 // register s advanced over [ptr, ptr + n).  All loads are aligned 8-byte words: the unaligned head
 // and the tail come from the aligned words that contain them (never past their page), so a short
@@ -3688,13 +3644,8 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
         w += 8;
         k -= 8;
         auto fold8 = [&](const uint64_t *x) {
-            if constexpr (F::kPairs) {
 #pragma unroll
-                for (int j = 0; j < 8; j += 2) s = f.word2(s, x[j], x[j + 1]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) s = f.word(s, x[j]);
-            }
+            for (int j = 0; j < 8; ++j) s = f.word(s, x[j]);
         };
         for (; k >= 8; k -= 8, w += 8) {
             load8(w, nv);
@@ -3706,71 +3657,15 @@ __device__ __forceinline__ T lane_scan(T s, const uint8_t *ptr, uint64_t n, cons
     }
     if (k >= 4) {
         const uint64_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
-        if constexpr (F::kPairs) {
-            s = f.word2(s, v0, v1);
-            s = f.word2(s, v2, v3);
-        } else {
-            s = f.word(s, v0);
-            s = f.word(s, v1);
-            s = f.word(s, v2);
-            s = f.word(s, v3);
-        }
+        s = f.word(s, v0);
+        s = f.word(s, v1);
+        s = f.word(s, v2);
+        s = f.word(s, v3);
         k -= 4;
         w += 4;
     }
-    if constexpr (F::kPairs) {
-        if (k >= 2) {
-            const uint64_t v0 = w[0], v1 = w[1];
-            s = f.word2(s, v0, v1);
-            k -= 2;
-            w += 2;
-        }
-    }
     for (; k; --k) s = f.word(s, *w++);
     if (n & 7) s = f.bytes(s, *w, (uint32_t)(n & 7));
-    return s;
-}
-
-// lane_scan over whole 128-byte lines: every line a lane touches is loaded at once (eight 16-byte
-// loads, the next line in flight while this one is folded), so each line is requested from L2 once.
-// With one lane per buffer the lanes of a CU stream ~500 lines at a time, more than the L1 holds; the
-// half-line batches of lane_scan came back for the second half after it had been evicted (2-4 L2
-// requests per line: TCP_TCC_READ_REQ, profiles/r04/h).  Words outside [ptr, ptr + n) in the first
-// and last line are loaded (same line, same page) and skipped.
-template <class T, class F>
-__device__ __forceinline__ T lane_scan_lines(T s, const uint8_t *ptr, uint64_t n, const F &f) {
-    const uintptr_t a = (uintptr_t)ptr, e = a + n;
-    const uintptr_t p8 = (a + 7) & ~(uintptr_t)7, e8 = e & ~(uintptr_t)7;
-    if (n < 256 || p8 >= e8) return lane_scan<T>(s, ptr, n, f);
-    if (p8 > a) s = f.bytes(s, *(const uint64_t *)(a & ~(uintptr_t)7) >> (8 * (a & 7)), (uint32_t)(p8 - a));
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(16)));
-    auto load16 = [](uintptr_t L, uint64_t *v) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const u64x2 x = *(const __attribute__((address_space(1))) u64x2 *)(L + 16 * j);
-            v[2 * j] = x.x;
-            v[2 * j + 1] = x.y;
-        }
-    };
-    uintptr_t line = p8 & ~(uintptr_t)127;
-    uint64_t v[16], nv[16];
-    load16(line, v);
-    uint32_t j0 = (uint32_t)((p8 - line) >> 3);
-    for (;;) {
-        const uintptr_t nl = line + 128;
-        const bool next = nl < e8;
-        if (next) load16(nl, nv);
-        const uint32_t j1 = nl <= e8 ? 16u : (uint32_t)((e8 - line) >> 3);
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if ((uint32_t)j >= j0 && (uint32_t)j < j1) s = f.word(s, v[j]);
-        if (!next) break;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = nv[j];
-        line = nl;
-        j0 = 0;
-    }
-    if (e > e8) s = f.bytes(s, *(const uint64_t *)e8, (uint32_t)(e - e8));
     return s;
 }
 
@@ -3823,30 +3718,18 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
 // prelude (-> prelude CRC) and continues over the headers and payload (-> message CRC, the running
 // form of CRC32 over [0, total - 4)), and compares both with the big-endian values stored at offset 8
 // and total - 4.  Folds on the conflict-free tables (LaneW8).  Measured and dropped in round 4
-// (profiles/r04/f-i): deeper load rings (2-8 blocks of 64 bytes in flight: 37-39 us against 28-29),
-// four lanes per message on a quad braid (52-54 us), a lane pair per message (the second lane
-// folding the message tail: 42 us, twice the VALU instructions).
+// (profiles/r04/f-s; the code is in git history, commit baaa268): deeper load rings
+// (37-39 us against 28-29), four lanes per message on a quad braid (52-54 us), a lane pair per message
+// (42 us; 35 us with 512-thread workgroups), slice-by-16 (30 us), whole 128-byte line batches (35 us).
 __device__ __forceinline__ uint32_t be32(const uint8_t *q) {
     return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
 }
 
-#ifndef AMDCRC_ES_S16  // compile-time only (A/B builds): 1 = slice-by-16 on plain tables
-#define AMDCRC_ES_S16 0
-#endif
-#ifndef AMDCRC_ES_LINES  // compile-time only (A/B builds): 1 = whole 128-byte lines per load batch
-#define AMDCRC_ES_LINES 0
-#endif
 __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParams p) {
-#if AMDCRC_ES_S16
-    __shared__ uint32_t tab16[16][256];
-    lane_tables16<kPoly32>(tab16);
-    const Tab16Fold f{(const uint32_t (*)[256])tab16};
-#else
     __shared__ __attribute__((aligned(16))) char lds[kLaneW8Lds];
     lane_w8_tables<kPoly32>(lds);
     LaneW8 f;
     f.init(lds, threadIdx.x & 63u);
-#endif
     const uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= p.count) return;
     const uint64_t off = p.d_offsets[m];
@@ -3859,11 +3742,7 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
         if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
             uint32_t s = lane_scan<uint32_t>(~0u, q, 8, f);
             pre = ~s;
-#if AMDCRC_ES_LINES
-            s = lane_scan_lines<uint32_t>(s, q + 8, total - 12, f);
-#else
             s = lane_scan<uint32_t>(s, q + 8, total - 12, f);
-#endif
             msg = ~s;
             st = (be32(q + 8) == pre ? 1u : 0u) | (be32(q + total - 4) == msg ? 2u : 0u);
         }
