@@ -30,6 +30,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -100,11 +103,29 @@ struct JobImpl {
     const void *const *ptrs = nullptr;
     const size_t *lens = nullptr;
     size_t count = 0;
-    std::vector<uint64_t> seeds;  // per buffer (0 when none)
+    const void *h_seeds = nullptr;  // the caller's seeds (u32 or u64 per buffer) or null
+    bool seed64 = false;
+    uint64_t seed_of(size_t i) const {
+        return !h_seeds ? 0 : seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+    }
     void *h_out = nullptr;
+    // Pieces: with no buffer cut (every buffer within a piece) piece q is buffer q and its value goes
+    // straight to h_out (`direct`: no piece records, no join pass -- a C4-shard job of 131,072 parts
+    // spent ~20 % of its time building and folding them); otherwise the records below.
+    bool direct = false;
+    size_t npieces = 0;
     std::vector<Piece> pieces;
-    std::vector<uint64_t> piece_val;    // per piece (CRC jobs)
-    std::vector<uint64_t> piece_start;  // byte offset of each piece in the job (pieces.size() + 1)
+    std::vector<uint64_t> piece_val;    // per piece (CRC jobs, not direct)
+    std::vector<uint64_t> piece_start;  // byte offset of each piece in the job (npieces + 1)
+    Piece piece(size_t q) const { return direct ? Piece{q, 0, lens[q], seed_of(q)} : pieces[q]; }
+    void put(size_t q, uint64_t v) {
+        if (!direct)
+            piece_val[q] = v;
+        else if (alg == AWS_CRT_AMD_CRC64NVME)
+            ((uint64_t *)h_out)[q] = v;
+        else
+            ((uint32_t *)h_out)[q] = (uint32_t)v;
+    }
     std::atomic<size_t> cursor{0};      // the next unclaimed piece
     int ndev = 0;                       // device lanes of the job
     size_t hthreads = 0;                // host threads taking pieces beside them
@@ -124,6 +145,14 @@ struct JobImpl {
     }
     uint64_t *dev_bytes_out = nullptr;  // options: bytes the devices scanned, set by job_wait
     std::vector<std::thread> workers;
+    // the host coordinator posted to the runner: done when it has returned
+    std::mutex host_mu;
+    std::condition_variable host_cv;
+    bool host_running = false;
+    void host_wait() {
+        std::unique_lock<std::mutex> g(host_mu);
+        host_cv.wait(g, [this] { return !host_running; });
+    }
     std::atomic<int> rc{0};
     std::string err;
     std::mutex err_mu;
@@ -131,9 +160,10 @@ struct JobImpl {
     // vectors: fresh pages on every job cost ~0.3 ms of faults)
     void reset() {
         alg = 0, ptrs = nullptr, lens = nullptr, count = 0, h_out = nullptr;
-        seeds.clear(), pieces.clear(), piece_val.clear(), piece_start.clear();
+        h_seeds = nullptr, seed64 = false, direct = false, npieces = 0;
+        pieces.clear(), piece_val.clear(), piece_start.clear();
         cursor.store(0), ndev = 0, hthreads = 0, dev_bytes.store(0), dev_bytes_out = nullptr;
-        workers.clear(), rc.store(0), err.clear();
+        workers.clear(), rc.store(0), err.clear(), host_running = false;
         t0 = std::chrono::steady_clock::now();
         lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
         lane_wait_ns.store(0), lane_issue_ns.store(0), lane_first_ns.store(0), lane_stage_ns.store(0);
@@ -216,6 +246,55 @@ void lane_free(Lane &L) {
     if (L.comp) (void)hipStreamDestroy(L.comp);
 }
 
+// Threads that run jobs' host-side coordinators, kept for reuse (a std::thread per job cost its
+// creation, ~0.1 ms, on every job); one more is started when none is idle, so concurrent jobs still
+// run concurrently.
+class Runner {
+  public:
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu_);
+        q_.push_back(std::move(f));
+        if (idle_ == 0)
+            ts_.emplace_back([this] { loop(); });
+        else
+            cv_.notify_one();
+    }
+    ~Runner() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : ts_) t.join();
+    }
+
+  private:
+    void loop() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            ++idle_;
+            cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+            --idle_;
+            if (q_.empty()) return;  // stopping
+            std::function<void()> f = std::move(q_.front());
+            q_.pop_front();
+            g.unlock();
+            f();
+            g.lock();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    std::vector<std::thread> ts_;
+    size_t idle_ = 0;
+    bool stop_ = false;
+};
+Runner &runner() {
+    static Runner r;
+    return r;
+}
+
 constexpr size_t kHybridPiece = 8u << 20;  // piece size of hybrid jobs (host threads claim whole pieces)
 constexpr uint64_t kMinDevClaim = 1u << 20;
 constexpr uint64_t kHostClaim = 1u << 20;
@@ -225,7 +304,7 @@ constexpr size_t kAutoLanesMaxShare = 12;  // auto jobs use device lanes below t
 // Claim the next run of pieces [*a, *b): at least one, at most max_pieces, at most `budget` bytes
 // past the first.  false when the job has no unclaimed piece left.
 bool claim(JobImpl *job, uint64_t budget, size_t max_pieces, size_t *a, size_t *b) {
-    const size_t n = job->pieces.size();
+    const size_t n = job->npieces;
     size_t cur = job->cursor.load(std::memory_order_relaxed);
     for (;;) {
         if (cur >= n) return false;
@@ -248,7 +327,7 @@ bool claim(JobImpl *job, uint64_t budget, size_t max_pieces, size_t *a, size_t *
 // profiles/r04/e).  Devices alone: a whole slot.
 uint64_t dev_budget(const JobImpl *job) {
     if (!job->hthreads) return kSlotBytes;
-    const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
+    const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->npieces);
     const uint64_t rem = job->piece_start.back() - job->piece_start[c];
     const uint64_t share = rem * 3 / ((3 * (uint64_t)job->ndev + (uint64_t)job->hthreads) * kSlots);
     return std::min<uint64_t>(kSlotBytes, std::max(kMinDevClaim, share));
@@ -302,7 +381,7 @@ void device_worker_body(JobImpl *job, int dev) {
         job->lane_wait_ns.fetch_add(job->since_ns() - w0, std::memory_order_relaxed);
         const std::vector<size_t> &ps = slot_pieces[k];
         for (size_t j = 0; j < ps.size(); ++j)
-            job->piece_val[ps[j]] = osz == 8 ? ((const uint64_t *)L.hres[k])[j] : ((const uint32_t *)L.hres[k])[j];
+            job->put(ps[j], osz == 8 ? ((const uint64_t *)L.hres[k])[j] : ((const uint32_t *)L.hres[k])[j]);
         L.used[k] = false;
         return true;
     };
@@ -339,7 +418,7 @@ void device_worker_body(JobImpl *job, int dev) {
         bool cur_pinned = false;
         const uint8_t *src_end = nullptr;
         for (size_t j = 0; j < ps.size(); ++j) {
-            const Piece &pc = job->pieces[ps[j]];
+            const Piece pc = job->piece(ps[j]);
             const uint8_t *src = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
             if (src != src_end) {
                 const uint64_t c0 = job->since_ns();
@@ -411,7 +490,7 @@ void device_worker_body(JobImpl *job, int dev) {
 void crc_host_worker(JobImpl *job) noexcept {
     size_t a, b;
     while (job->rc.load() == 0) {
-        const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->pieces.size());
+        const size_t c = std::min(job->cursor.load(std::memory_order_relaxed), job->npieces);
         const uint64_t rem = job->piece_start.back() - job->piece_start[c];
         // guided: a quarter of an even share of what is left, at least kHostClaim or an eighth of an
         // even share of the job (one shared cursor claimed in 1 MiB runs cost a C2 job ~4,000
@@ -422,12 +501,12 @@ void crc_host_worker(JobImpl *job) noexcept {
         if (!claim(job, budget, SIZE_MAX, &a, &b)) break;
         job->host_claims.fetch_add(1, std::memory_order_relaxed);
         for (size_t q = a; q < b; ++q) {
-            const Piece &pc = job->pieces[q];
+            const Piece pc = job->piece(q);
             const uint8_t *p = (const uint8_t *)job->ptrs[pc.buf] + pc.off;
             switch (job->alg) {
-                case AWS_CRT_AMD_CRC32: job->piece_val[q] = cpu::crc32(p, pc.len, (uint32_t)pc.seed); break;
-                case AWS_CRT_AMD_CRC32C: job->piece_val[q] = cpu::crc32c(p, pc.len, (uint32_t)pc.seed); break;
-                default: job->piece_val[q] = cpu::crc64nvme(p, pc.len, pc.seed); break;
+                case AWS_CRT_AMD_CRC32: job->put(q, cpu::crc32(p, pc.len, (uint32_t)pc.seed)); break;
+                case AWS_CRT_AMD_CRC32C: job->put(q, cpu::crc32c(p, pc.len, (uint32_t)pc.seed)); break;
+                default: job->put(q, cpu::crc64nvme(p, pc.len, pc.seed)); break;
             }
         }
     }
@@ -440,7 +519,7 @@ void host_worker(JobImpl *job, size_t t, size_t threads) {
         uint64_t r[2] = {0, 0};
         const uint8_t *p = (const uint8_t *)job->ptrs[i];
         const size_t n = job->lens[i];
-        const uint64_t sd = job->seeds[i];
+        const uint64_t sd = job->seed_of(i);
         switch (job->alg) {
             case AWS_CRT_AMD_CRC32: ((uint32_t *)job->h_out)[i] = cpu::crc32(p, n, (uint32_t)sd); continue;
             case AWS_CRT_AMD_CRC32C: ((uint32_t *)job->h_out)[i] = cpu::crc32c(p, n, (uint32_t)sd); continue;
@@ -601,9 +680,8 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         J.dev_bytes_out = opt ? opt->device_bytes : nullptr;
         if (J.dev_bytes_out) *J.dev_bytes_out = 0;
         const bool seed64 = alg != AWS_CRT_AMD_CRC32 && alg != AWS_CRT_AMD_CRC32C;
-        J.seeds.assign(count, 0);
-        for (size_t i = 0; h_seeds && i < count; ++i)
-            J.seeds[i] = seed64 ? ((const uint64_t *)h_seeds)[i] : ((const uint32_t *)h_seeds)[i];
+        J.h_seeds = h_seeds;
+        J.seed64 = seed64;
         const int vis = ndevices < 0 ? 0 : visible_devices();
         int G = ndevices < 0 ? 0 : ndevices == 0 ? vis : std::min(ndevices, vis);  // < 0: the host path only
         if (is_crc(alg) && G > 0 && !amdcrc_gpu_usable()) {
@@ -637,20 +715,31 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         size_t H = want_host < 0 || G == 0 ? (share > reserve ? share - reserve : 1) : (size_t)want_host;
         if (G == 0) H = std::max<size_t>(H, 1);
         const size_t piece = H ? kHybridPiece : kSlotBytes;
-        // pieces, buffer by buffer, in job order
-        J.pieces.reserve(count + (size_t)(total / piece));
-        for (size_t i = 0; i < count; ++i) {
-            size_t off = 0;
-            do {
-                const size_t n = std::min(piece, lens[i] - off);
-                J.pieces.push_back({i, off, n, off == 0 ? J.seeds[i] : 0});
-                off += n;
-            } while (off < lens[i]);
+        // pieces, buffer by buffer, in job order (none recorded when no buffer is cut)
+        size_t maxlen = 0;
+        for (size_t i = 0; i < count; ++i) maxlen = std::max(maxlen, lens[i]);
+        J.direct = maxlen <= piece;
+        if (J.direct) {
+            J.npieces = count;
+            J.piece_start.resize(count + 1);
+            J.piece_start[0] = 0;
+            for (size_t i = 0; i < count; ++i) J.piece_start[i + 1] = J.piece_start[i] + lens[i];
+        } else {
+            J.pieces.reserve(count + (size_t)(total / piece));
+            for (size_t i = 0; i < count; ++i) {
+                size_t off = 0;
+                do {
+                    const size_t n = std::min(piece, lens[i] - off);
+                    J.pieces.push_back({i, off, n, off == 0 ? J.seed_of(i) : 0});
+                    off += n;
+                } while (off < lens[i]);
+            }
+            J.npieces = J.pieces.size();
+            J.piece_start.resize(J.npieces + 1, 0);
+            for (size_t q = 0; q < J.npieces; ++q) J.piece_start[q + 1] = J.piece_start[q] + J.pieces[q].len;
+            J.piece_val.assign(J.npieces, 0);
         }
-        J.piece_start.resize(J.pieces.size() + 1, 0);
-        for (size_t q = 0; q < J.pieces.size(); ++q) J.piece_start[q + 1] = J.piece_start[q] + J.pieces[q].len;
-        J.piece_val.assign(J.pieces.size(), 0);
-        H = std::min(H, J.pieces.size());
+        H = std::min(H, J.npieces);
         if (G) G = (int)std::min<size_t>((size_t)G, std::max<size_t>(1, (size_t)(total / kMinDevClaim)));  // tiny jobs: fewer lanes
         // a hybrid job smaller than one slot finishes on the host threads before a lane's first copy
         // and launch would (tens of microseconds): no lane
@@ -660,7 +749,16 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         for (int g = 0; g < G; ++g) J.spawn(device_worker, &J, g);
         // the host threads: the host path's persistent pool (a std::thread per job thread cost its
         // creation on every job), driven by one coordinator thread the job joins
-        if (H) J.spawn([](JobImpl *j, size_t h) { cpu::parallel(h, [j](size_t) { crc_host_worker(j); }); }, &J, H);
+        if (H) {
+            J.host_running = true;
+            JobImpl *jp = &J;
+            runner().post([jp, H] {
+                cpu::parallel(H, [jp](size_t) { crc_host_worker(jp); });
+                std::lock_guard<std::mutex> g(jp->host_mu);
+                jp->host_running = false;
+                jp->host_cv.notify_all();
+            });
+        }
         *job_out = job.release();
         return 0;
     });
@@ -678,6 +776,7 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
         JobImpl &J = job->impl;
         for (auto &t : J.workers) t.join();
         J.workers.clear();
+        J.host_wait();
         int rc = J.rc.load();
         if ((rc == AWS_CRT_AMD_ERR_HIP || rc == AWS_CRT_AMD_ERR_NO_DEVICE) && is_crc(J.alg)) {
             // a device worker failed: the whole job on the host path instead, as the single-buffer ABI
@@ -687,22 +786,15 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
             for (auto &t : J.workers) t.join();
             amdcrc_note_fallback();
             rc = 0;
-        } else if (rc == 0 && is_crc(J.alg) && !J.pieces.empty()) {
-            if (J.dev_bytes_out) *J.dev_bytes_out = J.dev_bytes.load();
+        } else if (rc == 0 && is_crc(J.alg) && J.dev_bytes_out) {
+            *J.dev_bytes_out = J.dev_bytes.load();
+        }
+        if (rc == 0 && is_crc(J.alg) && !J.direct && !J.pieces.empty() && J.workers.empty()) {
             // fold each buffer's pieces: crc = Combine(crc, piece, |piece|)
             const uint64_t poly = alg_poly(J.alg);
             const int w = alg_width(J.alg);
             size_t p = 0;
-            if (J.pieces.size() == J.count) {  // no buffer was cut: the pieces are the buffers
-                for (size_t i = 0; i < J.count; ++i) {
-                    if (w == 64)
-                        ((uint64_t *)J.h_out)[i] = J.piece_val[i];
-                    else
-                        ((uint32_t *)J.h_out)[i] = (uint32_t)J.piece_val[i];
-                }
-                p = J.count;
-            }
-            for (size_t i = p; i < J.count; ++i) {
+            for (size_t i = 0; i < J.count; ++i) {
                 uint64_t acc = J.piece_val[p++];
                 while (p < J.pieces.size() && J.pieces[p].buf == i) {
                     acc = gf2_mulmod(acc, gf2_xpow8n(J.pieces[p].len, poly, w), poly, w) ^ J.piece_val[p];
@@ -721,7 +813,7 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
                          "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f, "
                          "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_stage_ms\": %.3f, \"lane_wait_ms\": %.3f, "
                          "\"lane_mirror_bytes\": %llu, \"lane_pin_checks\": %llu, \"lane_pin_ms\": %.3f}\n",
-                         J.pieces.size(), J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
+                         J.npieces, J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
                          (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
                          J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6, J.lane_first_ns.load() * 1e-6,
                          J.lane_issue_ns.load() * 1e-6, J.lane_stage_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6,
