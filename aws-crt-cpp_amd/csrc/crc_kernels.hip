@@ -135,19 +135,30 @@ __device__ __forceinline__ BatchPos batch_pos(const ScanParams &p, uint64_t b) {
 // the compiler emits scalar loads; the build checks that no kernel uses scratch)
 __device__ __forceinline__ uint64_t karg64(const uint64_t *a, uint64_t j) { return a[j]; }
 
+__device__ __forceinline__ Edges edges_of(uint64_t ptr, uint64_t n) {
+    const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
+    return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
+}
+// a list buffer's address and length: both scalar loads in flight together, one wait
+__device__ __forceinline__ void list_desc(const ScanParams &p, uint64_t b, uint64_t &ptr, uint64_t &n) {
+    const uint64_t pa = rfl64((uint64_t)(p.d_ptrs + b)), la = rfl64((uint64_t)(p.d_lens + b));
+    asm volatile("s_load_dwordx2 %0, %2, 0x0\n\ts_load_dwordx2 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(ptr), "=&s"(n)
+                 : "s"(pa), "s"(la)
+                 : "memory");
+}
+
 template <bool LIST>
 __device__ __forceinline__ Edges buffer_edges(const ScanParams &p, uint64_t b) {
     uint64_t ptr, n;
     if (LIST) {
-        ptr = sload64(p.d_ptrs + b);
-        n = sload64(p.d_lens + b);
+        list_desc(p, b, ptr, n);
     } else {
         const BatchPos bp = batch_pos(p, b);
         ptr = karg64(p.bbase, bp.j) + bp.i * p.stride;
         n = p.len;
     }
-    const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
-    return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
+    return edges_of(ptr, n);
 }
 
 template <bool LIST>
@@ -205,6 +216,24 @@ __device__ __forceinline__ typename E::T fold_bytes(typename E::T s, uint64_t a,
     return s;
 }
 
+// head state of buffer b with edges e: ~seed advanced over the unaligned head bytes [ptr, headend)
+template <bool LIST, class E>
+__device__ __forceinline__ typename E::T head_state_e(const ScanParams &p, uint64_t b, const Edges &e, const E &eng) {
+    using T = typename E::T;
+    uint64_t seed = p.seed_all;
+    const void *seeds = p.d_seeds;
+    uint64_t si = b;
+    if (!LIST) {
+        const BatchPos bp = batch_pos(p, b);
+        seeds = (const void *)karg64(p.bseed, bp.j);
+        si = bp.i;
+    }
+    if (seeds)
+        seed = E::W == 32 ? (uint64_t)sload32((const uint32_t *)seeds + si) : sload64((const uint64_t *)seeds + si);
+    T s = (T)~seed;
+    if (e.headend > e.ptr) s = fold_bytes(s, e.ptr, e.headend, eng);
+    return s;
+}
 // head state of buffer b: ~seed advanced over the unaligned head bytes [ptr, headend)
 template <bool LIST, class E>
 __device__ __forceinline__ typename E::T head_state(const ScanParams &p, uint64_t b, const E &eng) {
@@ -227,8 +256,13 @@ __device__ __forceinline__ typename E::T head_state(const ScanParams &p, uint64_
 
 // buffer b's register after its main region -> tail bytes, complement, store
 template <bool LIST, class E>
+__device__ __forceinline__ void finalize_e(const ScanParams &p, uint64_t b, const Edges &e, typename E::T fin, const E &eng);
+template <bool LIST, class E>
 __device__ __forceinline__ void finalize(const ScanParams &p, uint64_t b, typename E::T fin, const E &eng) {
-    const Edges e = buffer_edges<LIST>(p, b);
+    finalize_e<LIST>(p, b, buffer_edges<LIST>(p, b), fin, eng);
+}
+template <bool LIST, class E>
+__device__ __forceinline__ void finalize_e(const ScanParams &p, uint64_t b, const Edges &e, typename E::T fin, const E &eng) {
     if (e.end > e.tail) fin = fold_bytes(fin, e.tail, e.end, eng);
     fin = ~fin;
     void *out = p.d_out;
@@ -1643,13 +1677,17 @@ struct LBuf {        // the cursor's buffer (wave-uniform)
     uint64_t vb;     // virtual start of group 0 (main start - pad)
     uint32_t vg;     // groups (0: no main region)
     uint32_t pad;    // virtual zero bytes in front of main (< 4096)
+    uint64_t ptr, n; // the buffer (its head and tail folds need no second descriptor load)
+    __device__ __forceinline__ Edges edges() const { return edges_of(ptr, n); }
 };
 __device__ __forceinline__ LBuf lbuf_at(const ScanParams &p, uint64_t b) {
-    const Edges e = buffer_edges<true>(p, b);
+    uint64_t ptr, n;
+    list_desc(p, b, ptr, n);
+    const Edges e = edges_of(ptr, n);
     const uint64_t m = e.tail - e.headend;
     const uint64_t vg = (m + kWaveGroupBytes - 1) / kWaveGroupBytes;
     const uint32_t pad = (uint32_t)(vg * kWaveGroupBytes - m);
-    return LBuf{b, e.headend - pad, (uint32_t)vg, pad};
+    return LBuf{b, e.headend - pad, (uint32_t)vg, pad, ptr, n};
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint64_t base, uint32_t nrec) {
@@ -1718,7 +1756,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;  // b0 < nbuf then (the host's wbuf is nbuf only past the groups)
-    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0};
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0, 0, 0};
     uint32_t fq = 0, fg = g0;
     if (nq)
         while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
@@ -1779,8 +1817,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     if (owns) sc = lbuf_at(p, b0);
     // a buffer without a main region: its head fold is the whole CRC
     auto finish_empty = [&]() {
-        const uint32_t s_h = head_state<true>(p, sc.b, eng);
-        if (lane == 0) finalize<true>(p, sc.b, s_h, eng);
+        const uint32_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
+        if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), s_h, eng);
     };
     // leading buffers without a main region (with groups to scan, the first buffer that has some may
     // lie past b_end: the next wave then starts inside it)
@@ -1804,7 +1842,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
 #ifdef AMDCRC_XP_LIST_NOHEAD  // experiment builds only (timing; results wrong): no head fold, no seed read
             uint32_t s_h = ~0u;
 #else
-            uint32_t s_h = head_state<true>(p, sc.b, eng);
+            uint32_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
 #endif
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
@@ -1819,7 +1857,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (c + n == vg) {
             const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[b], 0ull);
             sx_store32(&p.d_cnt[b], 0u);
-            finalize<true>(p, b, fin, eng);
+            finalize_e<true>(p, b, sc.edges(), fin, eng);  // (b is sc.b at every call)
         }
     };
     uint32_t nparts = 0;  // parts this wave has finished
@@ -1840,7 +1878,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;
         if (ga == 0 && g == sc.vg) {
-            if (lane == 0) finalize<true>(p, sc.b, r, eng);
+            if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), r, eng);
             return;
         }
         if (lane != 0) return;
@@ -1852,7 +1890,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             if (d & 0x100u)
                 publish(sc.b, (uint32_t)v, groups, sc.vg);
             else
-                finalize<true>(p, sc.b, (uint32_t)v, eng);
+                finalize_e<true>(p, sc.b, sc.edges(), (uint32_t)v, eng);
         });
     };
     part_begin();
@@ -2909,7 +2947,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;
-    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0};
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0, 0, 0};
     uint32_t fq = 0, fg = g0;
     if (nq)
         while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
@@ -2954,8 +2992,8 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     LBuf sc = fc;
     if (owns) sc = lbuf_at(p, b0);
     auto finish_empty = [&]() {  // a buffer without a main region: its head fold is the whole CRC
-        const uint64_t s_h = head_state<true>(p, sc.b, eng);
-        if (lane == 0) finalize<true>(p, sc.b, s_h, eng);
+        const uint64_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
+        if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), s_h, eng);
     };
     if (owns)
         while (sc.vg == 0) {
@@ -2973,7 +3011,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         ga = g;
         u = 0;
         if (g == 0) {
-            uint64_t s_h = head_state<true>(p, sc.b, eng);
+            uint64_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
@@ -2985,7 +3023,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         if (c + n == vg) {
             const uint64_t fin = sx_swap64_ret(&p.d_acc[b], 0ull);
             sx_store32(&p.d_cnt[b], 0u);
-            finalize<true>(p, b, fin, eng);
+            finalize_e<true>(p, b, sc.edges(), fin, eng);  // (b is sc.b at every call)
         }
     };
     uint32_t nparts = 0;  // parts this wave has finished
@@ -3001,7 +3039,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;
         if (ga == 0 && g == sc.vg) {
-            if (lane == 0) finalize<true>(p, sc.b, r, eng);
+            if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), r, eng);
             return;
         }
         if (lane != 0) return;
@@ -3014,7 +3052,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             if (d & 0x100u)
                 publish(sc.b, v, groups, sc.vg);
             else
-                finalize<true>(p, sc.b, v, eng);
+                finalize_e<true>(p, sc.b, sc.edges(), v, eng);
         });
     };
     part_begin();
