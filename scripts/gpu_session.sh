@@ -28,6 +28,10 @@ for s in "$@"; do
     probe) for v in ${PROBE_ENVS:-""}; do
              step 120 $O/probe.log.tmp env $v python -u aws-crt-cpp_amd/tools/overhead_probe.py 20 40; rc=$?; cat $O/probe.log.tmp >> $O/probe.log
              [ $rc -ne 0 ] && break; done; grep '^{' $O/probe.log | cut -c1-600 ;;
+    # kernel traces of the event-stream bench and of the ragged-list probe
+    esprof) (cd /tmp && step 180 $O/esprof.log rocprofv3 --kernel-trace --stats -d $O/esprof -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames); rc=$? ;;
+    listprof) (cd /tmp && step 180 $O/listprof.log rocprofv3 --kernel-trace --stats -d $O/listprof -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/list_probe.py ${LIST_ALG:-crc32c}); rc=$? ;;
+    sq)    step 300 $O/sq.log env TAG=${TAG}/sq bash scripts/pmc_sq.sh; rc=$?; tail -1 $O/sq.log ;;
     es)    step 180 $O/es.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames; rc=$?; grep '^{' $O/es.log | cut -c1-500 ;;
     # SQ issue / stall / LDS counters of the event-stream framing kernel (one pass)
     sqes)  (cd /tmp && step 120 $O/sqes.log timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $O/sqes -o run --output-format csv -- python3 $R/aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames --steps 12 --timing-launches 4); rc=$? ;;
