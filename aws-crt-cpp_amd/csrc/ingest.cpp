@@ -752,12 +752,21 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         if (H) {
             J.host_running = true;
             JobImpl *jp = &J;
-            runner().post([jp, H] {
-                cpu::parallel(H, [jp](size_t) { crc_host_worker(jp); });
-                std::lock_guard<std::mutex> g(jp->host_mu);
-                jp->host_running = false;
-                jp->host_cv.notify_all();
-            });
+            try {
+                runner().post([jp, H] {
+                    cpu::parallel(H, [jp](size_t) { crc_host_worker(jp); });
+                    std::lock_guard<std::mutex> g(jp->host_mu);
+                    jp->host_running = false;
+                    jp->host_cv.notify_all();
+                });
+            } catch (...) {
+                // no runner thread: the job must not be released under the lanes already started
+                J.host_running = false;
+                J.set_error(AWS_CRT_AMD_ERR_OOM, "no host thread for the job");
+                for (auto &t : J.workers) t.join();
+                J.workers.clear();
+                throw;
+            }
         }
         *job_out = job.release();
         return 0;
