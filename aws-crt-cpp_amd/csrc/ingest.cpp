@@ -612,15 +612,25 @@ struct aws_crt_amd_job {
 };
 
 namespace {
-// finished jobs kept for reuse (their vectors' storage), at most 4, none over 1 Mi pieces
-std::mutex g_job_mu;
-std::vector<aws_crt_amd_job *> g_job_free;
+// finished jobs kept for reuse (their vectors' storage), at most 4, none over 1 Mi pieces; freed at exit
+struct JobCache {
+    std::mutex mu;
+    std::vector<aws_crt_amd_job *> v;
+    ~JobCache() {
+        for (aws_crt_amd_job *j : v) delete j;
+    }
+};
+JobCache &job_cache() {
+    static JobCache c;
+    return c;
+}
 aws_crt_amd_job *job_take() {
     {
-        std::lock_guard<std::mutex> g(g_job_mu);
-        if (!g_job_free.empty()) {
-            aws_crt_amd_job *j = g_job_free.back();
-            g_job_free.pop_back();
+        JobCache &c = job_cache();
+        std::lock_guard<std::mutex> g(c.mu);
+        if (!c.v.empty()) {
+            aws_crt_amd_job *j = c.v.back();
+            c.v.pop_back();
             return j;
         }
     }
@@ -631,9 +641,10 @@ void job_give(aws_crt_amd_job *j) noexcept {
     if (j->impl.pieces.capacity() <= ((size_t)1 << 20)) {
         try {
             j->impl.reset();
-            std::lock_guard<std::mutex> g(g_job_mu);
-            if (g_job_free.size() < 4) {
-                g_job_free.push_back(j);
+            JobCache &c = job_cache();
+            std::lock_guard<std::mutex> g(c.mu);
+            if (c.v.size() < 4) {
+                c.v.push_back(j);
                 return;
             }
         } catch (...) {

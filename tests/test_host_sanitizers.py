@@ -10,6 +10,8 @@ stand-ins in tests/cpp/host_only_stubs.cpp report "no usable device"):
   * TSan: eight threads racing on first use and then checksumming concurrently.
 """
 import os
+
+import pytest
 import subprocess
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,6 +40,20 @@ def test_concurrent_callers_under_tsan():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "[PASS] ConcurrentCallers" in r.stdout, r.stdout
     assert "ThreadSanitizer" not in r.stderr, r.stderr
+
+
+@pytest.mark.parametrize("target,opts", [("build/ingest_tsan", {"TSAN_OPTIONS": "halt_on_error=1"}),
+                                         ("build/ingest_asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})])
+def test_concurrent_host_jobs_under_sanitizers(target, opts):
+    """Host-ingest jobs from six threads at once on the host path (tests/cpp/ingest_host_test.cpp):
+    uncut jobs writing results directly, cut jobs joined with Combine, jobs and their vectors reused
+    across threads, coordinators on the shared runner threads -- under TSan and under ASan."""
+    _build(target)
+    env = dict(os.environ, **opts)
+    r = subprocess.run([os.path.join(CPP, target)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "[PASS] ConcurrentHostJobs" in r.stdout, r.stdout
+    assert "ThreadSanitizer" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr
 
 
 def test_unreadable_device_buffer_raises():
