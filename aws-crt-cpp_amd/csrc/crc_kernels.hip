@@ -23,9 +23,6 @@
 
 #include <type_traits>
 
-#ifndef AMDCRC_XCD_TWO  // compile-time only (A/B builds): 1 = two chains per lane in crc64_xcd_kernel (whole chunks)
-#define AMDCRC_XCD_TWO 0
-#endif
 #ifndef AMDCRC_R16_XCD  // compile-time only: crc64_rows16_kernel's sets in XCD-window order (1) or contiguous (0)
 #define AMDCRC_R16_XCD 1
 #endif
@@ -2622,13 +2619,13 @@ constexpr uint32_t kXcdSlotOff = kXcdJumpOff + 16 * 16 * 8;  // two held parts p
 constexpr uint32_t kXcdLds = kXcdSlotOff + 32 * 32;           // up to 16 waves
 static_assert(2 * kXcdLds <= 160 * 1024, "two crc64_xcd_kernel workgroups per CU");
 
-__device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u, uint32_t off = kXcdJumpOff) {
+__device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u) {
     const uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
     uint64_t v[16];
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-        v[n] = lds64(lds, off + 128u * n + 8u * ((lo >> (4 * n)) & 15u));
-        v[8 + n] = lds64(lds, off + 128u * (8 + n) + 8u * ((hi >> (4 * n)) & 15u));
+        v[n] = lds64(lds, kXcdJumpOff + 128u * n + 8u * ((lo >> (4 * n)) & 15u));
+        v[8 + n] = lds64(lds, kXcdJumpOff + 128u * (8 + n) + 8u * ((hi >> (4 * n)) & 15u));
     }
     uint32_t rl = 0, rh = 0;
 #pragma unroll
@@ -2673,43 +2670,12 @@ __device__ __forceinline__ void xcd_issue(B64Group &g, __amdgpu_buffer_rsrc_t rs
     }
 }
 
-// Two chains per lane (TWO, round-4 experiment build AMDCRC_XCD_TWO): a group's eight 512-byte rows
-// are four 1024-byte super-rows; chain E folds lane l's words of the even rows, chain O those of the
-// odd rows, each stepping over a super-row (tables T'_t with the skip over 127 words), so a lane's two
-// dependent chains are half as long and interleave.  At a part's end the shares join as
-// (uE * x^4096 ^ uO) * x^(-64 (64 + l)) (braid j of a super-row at 8 j, share x^(-64 j)).
-template <int R, class B>
-__device__ __forceinline__ void stream64_rows2(uint64_t &xe, uint64_t &xo, B64Group &cur, B64Group &nxt, uint32_t voff,
-                                               uint64_t snext, const B &eng) {
-    if constexpr (R < kB64RowsPerGroup) {
-        nxt.w[R] = gld_row64<R>(voff, snext);
-        if constexpr (R < 2) {
-            if constexpr (R == 0) xe ^= cur.w[0];
-            else xo ^= cur.w[1];
-        } else if constexpr (R % 2 == 0) {
-            xe = eng.step_x(xe, cur.w[R]);
-        } else {
-            xo = eng.step_x(xo, cur.w[R]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        stream64_rows2<R + 1>(xe, xo, cur, nxt, voff, snext, eng);
-    } else {
-        xe = eng.step(xe);
-        xo = eng.step(xo);
-    }
-}
-constexpr uint32_t kXcdX2U64 = 256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64;  // get_xcd_consts: nibble tables of x^4096
-constexpr uint32_t kXcdK2U64 = kXcdX2U64 + 256;                 // x^(-64 (64 + l)), l < 64
-constexpr uint32_t kXcdX2Off = kXcdLds;                         // the x^4096 nibble tables in LDS (TWO)
-static_assert(2 * (kXcdLds + 2048) <= 160 * 1024, "two two-chain crc64_xcd_kernel workgroups per CU");
-
 // PADDED: some main regions hold no whole number of chunks (ScanParams::xcd_pad != 0): every group
 // reads through a buffer resource.  Otherwise plain global loads (1-2 % shorter C5 launches).
-template <uint64_t POLY, int BLOCK, bool PADDED, bool TWO = false>
+template <uint64_t POLY, int BLOCK, bool PADDED>
 __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p) {
-    static_assert(!(PADDED && TWO), "two chains: whole-chunk main regions only");
     using B = Braid64<POLY, 4>;
-    __shared__ __attribute__((aligned(16))) char lds[kXcdLds + (TWO ? 2048 : 0)];
+    __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
     constexpr int kWaves = BLOCK / 64;
     static_assert(kWaves <= 16, "two held-part slots per wave, 32 entries");
     const int lane = threadIdx.x & 63;
@@ -2772,18 +2738,16 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
             if (fq < nq) cur_next(fc);
         }
     };
-    const uint64_t kl = TWO ? *(gu64 *)(p.d_pcols + kXcdK2U64 + lane) : *(gu64 *)(p.d_kvals + lane);
+    const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
     const uint64_t jt = threadIdx.x < 256 ? *(gu64 *)(p.d_pcols + threadIdx.x) : 0ull;
-    const uint64_t xt = TWO && threadIdx.x < 256 ? *(gu64 *)(p.d_pcols + kXcdX2U64 + threadIdx.x) : 0ull;
     B64Group ra, rb, rc;
     if (nq) {
         issue(ra);
         f_next();
     }
-    b64x4_build_tables<POLY, TWO ? 2 * kB64Row : kB64Row>(lds);
+    b64x4_build_tables<POLY>(lds);
     b64x4_build_nib<POLY>(lds, kl);
     if (threadIdx.x < 256) *(uint64_t *)(lds + kXcdJumpOff + 8u * threadIdx.x) = jt;
-    if (TWO && threadIdx.x < 256) *(uint64_t *)(lds + kXcdX2Off + 8u * threadIdx.x) = xt;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
@@ -2791,12 +2755,9 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint64_t *bytecols = p.d_pcols + 256 + 40 * 64;  // [level][v][j]: x^(8 * chunk * v * 256^level) * x^j
     uint64_t pb = ~0ull, pk = 0;  // the open part: buffer, last chunk
     uint32_t pn = 0;              // chunks in the part
-    uint64_t u = 0, uo = 0;  // (TWO: u is chain E, uo chain O)
+    uint64_t u = 0;
     // the open part's register (lane shares joined), at the end of its last chunk
-    auto part_raw = [&]() -> uint64_t {
-        if constexpr (TWO) return wave_xor64_s(eng.mulK(xcd_jump(lds, u, kXcdX2Off) ^ uo));
-        return wave_xor64_s(eng.mulK(u));
-    };
+    auto part_raw = [&]() -> uint64_t { return wave_xor64_s(eng.mulK(u)); };
     // r * x^(8 * chunk * m): one 64-column product per nonzero byte of m, the columns spread over the
     // lanes (lane c holds column c, a coalesced 512-byte load; the four loads issue together) and the
     // selected columns XORed across the wave.  Only where the payload ring is drained.
@@ -2902,11 +2863,10 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
         if (g == 0) {
             if (pn && sc.b == pb) {
                 u = xcd_jump(lds, u);
-                if constexpr (TWO) uo = xcd_jump(lds, uo);
             } else {
                 if (pn) part_finish();
                 pb = sc.b, pn = 0;
-                u = 0ull, uo = 0ull;
+                u = 0ull;
                 if (sc.k == 0) {
                     uint64_t s_h = head_state<false>(p, sc.b, eng);
                     if (jr) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * jr);
@@ -2920,10 +2880,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
             const uint32_t fo = f_off(), fl = f_lim();
             f_next();
             u = xcd_rows<0>(u, cur, nxt, rs, fo, fl, eng);
-        } else if constexpr (TWO) {
-            const uint64_t sn = f_addr();
-            f_next();
-            stream64_rows2<0>(u, uo, cur, nxt, voff, sn, eng);
         } else {
             const uint64_t sn = f_addr();
             f_next();
@@ -3966,7 +3922,7 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             else if (p->stream == 5 && !list && p->xcd_pad)  // long buffers: XCD-window chunks, front pads
                 launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, true>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream == 5 && !list)  // long buffers of whole chunks
-                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false, AMDCRC_XCD_TWO>, nblocks, kXcdBlock, s, p, ev);
+                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list && p->stream == 4)  // ragged lists: the list streaming scan

@@ -347,7 +347,7 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
     auto it = d->xcd.find(key);
     if (it == d->xcd.end()) {
         const uint64_t poly = alg_poly(alg);
-        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64 + 256 + 64, 0);
+        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64, 0);
         const uint64_t J = gf2_xpow8n((uint64_t)kXcdChunkBytes * (nwx - 1), poly, 64);
         for (int n = 0; n < 16; ++n)
             for (uint64_t v = 0; v < 16; ++v) c[16 * n + v] = gf2_mulmod(v << (4 * n), J, poly, 64);
@@ -403,18 +403,6 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
                 col = gf2_mulx(col, poly);
             }
             gm = gf2_mulmod(gm, g1, poly, 64);
-        }
-        // two-chain scans (1024-byte super-rows): nibble tables of x^(8*512), entry 16 n + v =
-        // (v << 4n) * x^4096, then the odd chain's lane shares x^(-64 (64 + l)), l < 64
-        const size_t x2 = 256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64;
-        const uint64_t X = gf2_xpow8n(512, poly, 64);
-        for (int n = 0; n < 16; ++n)
-            for (uint64_t v = 0; v < 16; ++v) c[x2 + 16 * n + v] = gf2_mulmod(v << (4 * n), X, poly, 64);
-        uint64_t k2 = 1ull << 63;  // x^0, then x^(-64 (64 + l))
-        for (int i = 0; i < 64 * 64; ++i) k2 = inv_mulx64(k2, poly);
-        for (int l = 0; l < 64; ++l) {
-            c[x2 + 256 + l] = k2;
-            for (int i = 0; i < 64; ++i) k2 = inv_mulx64(k2, poly);
         }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 8);
