@@ -88,8 +88,14 @@ void batch(int alg, const uint8_t *const *ptrs, const size_t *lens, const uint64
            int threads);
 
 // fn(0) .. fn(n - 1) on the host batch's persistent worker threads (fn(0) on the calling thread), or
-// on threads of their own when the pool is busy
-void parallel(size_t n, const std::function<void(size_t)> &fn);
+// on threads of their own when the pool is busy.  node >= 0 (from home_node): every index on pool
+// workers placed on that NUMA node's CPUs, the calling thread only waiting.
+void parallel(size_t n, const std::function<void(size_t)> &fn, int node = -1);
+
+// The NUMA node holding >= 3/4 of a job's bytes (64 pages sampled, move_pages), when the process's
+// CPU mask spans more than one node, that node has `threads` CPUs of it and the job is >= 16 MiB;
+// else -1.  AWS_CRT_AMD_NUMA=0: always -1; =force: one node counts too (tests).
+int home_node(const uint8_t *const *ptrs, const size_t *lens, size_t count, size_t threads);
 
 }  // namespace cpu
 }  // namespace amdcrc

@@ -129,6 +129,7 @@ struct JobImpl {
     std::atomic<size_t> cursor{0};      // the next unclaimed piece
     int ndev = 0;                       // device lanes of the job
     size_t hthreads = 0;                // host threads taking pieces beside them
+    int numa_node = -1;                 // the NUMA node the host threads run on (-1: not placed)
     std::atomic<uint64_t> dev_bytes{0};
     // AWS_CRT_AMD_INGEST_TRACE=1: one stderr line per job (claims and when each side ran out of work)
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
@@ -162,7 +163,7 @@ struct JobImpl {
         alg = 0, ptrs = nullptr, lens = nullptr, count = 0, h_out = nullptr;
         h_seeds = nullptr, seed64 = false, direct = false, npieces = 0;
         pieces.clear(), piece_val.clear(), piece_start.clear();
-        cursor.store(0), ndev = 0, hthreads = 0, dev_bytes.store(0), dev_bytes_out = nullptr;
+        cursor.store(0), ndev = 0, hthreads = 0, numa_node = -1, dev_bytes.store(0), dev_bytes_out = nullptr;
         workers.clear(), rc.store(0), err.clear(), host_running = false;
         t0 = std::chrono::steady_clock::now();
         lane_claims.store(0), lane_end_ns.store(0), host_end_ns.store(0), host_claims.store(0);
@@ -761,11 +762,13 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit_ex(int alg, const void *const *h_ptr
         // the host threads: the host path's persistent pool (a std::thread per job thread cost its
         // creation on every job), driven by one coordinator thread the job joins
         if (H) {
+            // the host threads on the NUMA node holding the job's bytes (cpu::home_node)
+            J.numa_node = cpu::home_node((const uint8_t *const *)h_ptrs, lens, count, H);
             J.host_running = true;
             JobImpl *jp = &J;
             try {
                 runner().post([jp, H] {
-                    cpu::parallel(H, [jp](size_t) { crc_host_worker(jp); });
+                    cpu::parallel(H, [jp](size_t) { crc_host_worker(jp); }, jp->numa_node);
                     std::lock_guard<std::mutex> g(jp->host_mu);
                     jp->host_running = false;
                     jp->host_cv.notify_all();
@@ -832,13 +835,13 @@ AWS_CRT_AMD_API int aws_crt_amd_job_wait(struct aws_crt_amd_job *job) {
                          "{\"ingest_trace\": 1, \"pieces\": %zu, \"host_threads\": %zu, \"lanes\": %d, \"device_bytes\": %llu, "
                          "\"lane_claims\": %llu, \"host_claims\": %llu, \"host_end_ms\": %.3f, \"lane_end_ms\": %.3f, \"wait_ms\": %.3f, "
                          "\"lane_first_ms\": %.3f, \"lane_issue_ms\": %.3f, \"lane_stage_ms\": %.3f, \"lane_wait_ms\": %.3f, "
-                         "\"lane_mirror_bytes\": %llu, \"lane_pin_checks\": %llu, \"lane_pin_ms\": %.3f}\n",
+                         "\"lane_mirror_bytes\": %llu, \"lane_pin_checks\": %llu, \"lane_pin_ms\": %.3f, \"numa_node\": %d}\n",
                          J.npieces, J.hthreads, J.ndev, (unsigned long long)J.dev_bytes.load(),
                          (unsigned long long)J.lane_claims.load(), (unsigned long long)J.host_claims.load(), J.host_end_ns.load() * 1e-6,
                          J.lane_end_ns.load() * 1e-6, J.since_ns() * 1e-6, J.lane_first_ns.load() * 1e-6,
                          J.lane_issue_ns.load() * 1e-6, J.lane_stage_ns.load() * 1e-6, J.lane_wait_ns.load() * 1e-6,
                          (unsigned long long)J.lane_mirror_bytes.load(), (unsigned long long)J.lane_pin_checks.load(),
-                         J.lane_pin_ns.load() * 1e-6);
+                         J.lane_pin_ns.load() * 1e-6, J.numa_node);
         if (rc) t_err = J.err;
         job_give(job);
         return rc;

@@ -7,7 +7,7 @@ pinned and pageable, through
   hybrid        aws_crt_amd_host_submit_ex (host threads beside the device lane; the default)
   devices_only  aws_crt_amd_host_submit_ex, host_threads 0
 
-best of `reps` after a warm-up each, and the plain H2D rate of the same bytes."""
+median of `reps` reps of >= 0.2 s after a warm-up each, and the plain H2D rate of the same bytes."""
 import json
 import os
 import sys
@@ -21,18 +21,24 @@ import torch  # noqa: E402
 import aws_crt_amd as eng  # noqa: E402
 
 
-def best(fn, reps):
+def best(fn, reps, secs=0.2):
+    """seconds per call: the median over `reps` reps of >= secs each (after a warm-up call)"""
     fn()
-    t = None
+    ts = []
     for _ in range(reps):
-        t0 = time.perf_counter()
-        fn()
-        el = time.perf_counter() - t0
-        t = el if t is None else min(t, el)
-    return t
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                break
+        ts.append(el / passes)
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
-def main(total_mib=1280, reps=3):
+def main(total_mib=1280, reps=5):
     eng.init()
     total = total_mib << 20
     threads = int(os.environ.get("OMP_NUM_THREADS", "16"))
@@ -40,7 +46,8 @@ def main(total_mib=1280, reps=3):
     pageable = torch.empty(total, dtype=torch.uint8)
     pageable.copy_(pinned)
     res = []
-    for mem, host in (("pinned", pinned), ("pageable", pageable)):
+    mems = os.environ.get("INGEST_PROBE_MEM", "pinned,pageable").split(",")
+    for mem, host in ((m, h) for m, h in (("pinned", pinned), ("pageable", pageable)) if m in mems):
         for part in (64 << 10, 8 << 20):
             n = total // part
             ptrs, lens = [host.data_ptr() + i * part for i in range(n)], [part] * n

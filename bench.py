@@ -136,11 +136,49 @@ def cpu_share():
     return threads, topo, limit
 
 
-def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5, step_buffers=None):
+def host_sample(dev_data, nbytes, pinned=None):
+    """The CPU baseline's bytes in host memory: the e2e leg's pinned copy of them when there is one
+    (the same pages the host-ingest legs read, so the two figures differ only by the path), else a
+    pageable copy written by this thread (its pages on one NUMA node, where the engine's host path
+    places its threads: cpu::home_node)."""
+    import numpy as np
+
+    if pinned is not None:
+        return pinned[:nbytes].numpy()
+    host = np.empty(nbytes, dtype=np.uint8)
+    np.copyto(host, dev_data[:nbytes].cpu().numpy())
+    return host
+
+
+def interleaved(legs, reps):
+    """Median GiB/s of each leg over `reps` reps; a leg's rep runs its callable until >= its seconds
+    have passed.  legs: (name, fn, nbytes, seconds).  Each leg is warmed up once; within a rep the
+    legs run one after another, the starting leg rotating with the rep."""
+    for _, fn, _, _ in legs:
+        fn()
+    rs = {name: [] for name, _, _, _ in legs}
+    for r in range(reps):
+        for k in range(len(legs)):
+            name, fn, nbytes, secs = legs[(r + k) % len(legs)]
+            passes, t0 = 0, time.perf_counter()
+            while True:
+                fn()
+                passes += 1
+                el = time.perf_counter() - t0
+                if el >= secs:
+                    break
+            rs[name].append(passes * nbytes / el / 2**30)
+    return {name: statistics.median(v) for name, v in rs.items()}
+
+
+def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5, step_buffers=None, paired=None):
     """Engine host path (kind "port") on a bounded sample: `count` buffers of L bytes from `host`
     (numpy), 1 thread and the box's CPU share, median of `reps` reps of >= rep_seconds each.
     gpu_results: the GPU's results for the first buffers.  step_buffers: also time the first
-    step_buffers buffers alone (one step, which may sit in the host's last-level cache) beside it."""
+    step_buffers buffers alone (one step, which may sit in the host's last-level cache) beside it.
+    paired: an IngestLegs whose host-ingest legs are timed in the same reps as the share-thread
+    figure (interleaved, order rotated per rep), so that `value` and the e2e legs see the same
+    state of the shared host (other tenants' memory traffic moves both by up to 2x between runs)."""
     from oracle import oracle  # checker and secondary figure only
 
     threads, topo, limit = cpu_share()
@@ -151,23 +189,16 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5, ste
     parity = first[:len(gpu_results)] == gpu_results[:count]
 
     def rate(fn, nbytes):
-        fn()  # warm-up
-        rs = []
-        for _ in range(reps):
-            passes, t0 = 0, time.perf_counter()
-            while True:
-                fn()
-                passes += 1
-                el = time.perf_counter() - t0
-                if el >= rep_seconds:
-                    break
-            rs.append(passes * nbytes / el / 2**30)
-        return statistics.median(rs)
+        return interleaved([("r", fn, nbytes, rep_seconds)], reps)["r"]
 
     n1 = count  # the same sample on one thread
     # argument arrays prepared once: the timed calls are the C calls alone
     many, one = eng.CpuBatch(ALG[alg], ptrs, lens, threads=threads), eng.CpuBatch(ALG[alg], ptrs[:n1], lens[:n1], threads=1)
-    v = rate(many.run, count * L)
+    legs = [("cpu", many.run, count * L, rep_seconds)] + (paired.legs() if paired is not None else [])
+    rates = interleaved(legs, reps)
+    if paired is not None:
+        paired.rates = rates
+    v = rates["cpu"]
     v1 = rate(one.run, n1 * L)
     ov = None
     if alg in oracle.ALG_INDEX:
@@ -181,8 +212,10 @@ def cpu_baseline(eng, alg, host, count, L, gpu_results, rep_seconds, reps=5, ste
     busy = min(threads, count) if hashed else threads
     return {"value": round(v, 2), "unit": "GiB/s", "cores": busy, "kind": "port",
             "impl": f"engine host path ({eng.cpu_tier()} tier)",
-            "sample": f"{count} x {L >> 10} KiB ({count * L >> 20} MiB) copied to host, median of {reps} reps "
-                      f"of >= {rep_seconds:g} s, {threads} persistent threads claiming work items "
+            "sample": f"{count} x {L >> 10} KiB ({count * L >> 20} MiB) in "
+                      f"{'the e2e legs pinned host pages' if paired is not None else 'pageable host memory'}, median of {reps} reps "
+                      f"of >= {rep_seconds:g} s{' interleaved with the e2e legs' if paired is not None else ''}, "
+                      f"{threads} persistent threads claiming work items "
                       + ("(one per buffer: a hash is one serial chain)" if hashed else
                          "(buffers cut into >= 1 MiB pieces folded with Combine, so every thread is busy)"),
             "threads_limit": limit, "single_thread_gibs": round(v1, 2), "topology": topo,
@@ -302,32 +335,40 @@ def kernel_name(alg, nbuf, L):
     return "xxh3_blocksum_kernel + xxh3_wave_kernel"
 
 
-def ingest_rates(eng, alg_id, ptrs, lens, reps=3):
-    """One host-ingest job over host buffers: the default (aws_crt_amd_host_submit with no options:
-    device lanes only for a CPU-poor share, the host path on the pool's 16-CPU share), hybrid asked for
-    explicitly (one lane beside the share less four threads), devices only (the PCIe-bound pipeline)
-    and the host path alone on the same bytes: GiB/s (best of `reps` after a warm-up), the devices'
-    share of the bytes, and the default job's results."""
-    nbytes = sum(lens)
-    share = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    out = {}
-    for name, nd, ht in (("default", 0, -1), ("hybrid", 1, max(1, share - 4)), ("devices_only", 0, 0), ("host_only", -1, -1)):
-        job = eng.HostJob(alg_id, ptrs, lens, ndevices=nd, host_threads=ht)
-        job.run()  # warm-up: device lanes, the first DMA touch of the pinned pages
-        best = None
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            job.run()
-            el = time.perf_counter() - t0
-            best = el if best is None else min(best, el)
-        out[name] = {"gibs": round(nbytes / best / 2**30, 2), "device_share": round(job.device_bytes / max(nbytes, 1), 4)}
-        if name == "default":
-            out["results"] = job.results()
-    return {"value": out["default"]["gibs"], "unit": "GiB/s", "device_share": out["default"]["device_share"],
-            "hybrid_gibs": out["hybrid"]["gibs"], "hybrid_device_share": out["hybrid"]["device_share"],
-            "devices_only_gibs": out["devices_only"]["gibs"], "host_only_gibs": out["host_only"]["gibs"],
-            "results": out["results"],
-            "api": "aws_crt_amd_host_submit (default policy) + aws_crt_amd_job_wait"}
+class IngestLegs:
+    """One host-ingest job over host buffers, four ways: the default (aws_crt_amd_host_submit with no
+    options: device lanes only for a CPU-poor share, the host path on the pool's 16-CPU share), hybrid
+    asked for explicitly (one lane beside the share less four threads), devices only (the PCIe-bound
+    pipeline) and the host path alone on the same bytes.  legs() are timed by interleaved() (beside
+    cpu_baseline's share-thread figure when paired with it, else alone): GiB/s is the median of the
+    reps, each rep re-running the job for >= `seconds`."""
+
+    def __init__(self, eng, alg_id, ptrs, lens, seconds=0.25):
+        self.nbytes = sum(lens)
+        share = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        self.jobs = {name: eng.HostJob(alg_id, ptrs, lens, ndevices=nd, host_threads=ht)
+                     for name, nd, ht in (("default", 0, -1), ("hybrid", 1, max(1, share - 4)),
+                                          ("devices_only", 0, 0), ("host_only", -1, -1))}
+        self.seconds = seconds
+        self.rates = None
+
+    def legs(self):
+        return [(name, job.run, self.nbytes, self.seconds) for name, job in self.jobs.items()]
+
+    def record(self, reps=5):
+        if self.rates is None:
+            self.rates = interleaved(self.legs(), reps)
+        share = {name: round(job.device_bytes / max(self.nbytes, 1), 4) for name, job in self.jobs.items()}
+        gibs = {name: round(self.rates[name], 2) for name in self.jobs}
+        return {"value": gibs["default"], "unit": "GiB/s", "device_share": share["default"],
+                "hybrid_gibs": gibs["hybrid"], "hybrid_device_share": share["hybrid"],
+                "devices_only_gibs": gibs["devices_only"], "host_only_gibs": gibs["host_only"],
+                "timing": f"median of reps of >= {self.seconds:g} s per leg"
+                          + (", interleaved with cpu_baseline's reps" if "cpu" in self.rates else ""),
+                "api": "aws_crt_amd_host_submit (default policy) + aws_crt_amd_job_wait"}
+
+    def results(self):
+        return self.jobs["default"].results()
 
 
 def config_label(alg, count, L):
@@ -343,30 +384,39 @@ def config_label(alg, count, L):
     return "custom"
 
 
-def e2e_step(eng, alg, dev_step, nbuf, L, gpu_results):
+class E2EStep:
     """One config step from pinned host memory through the host-ingest API (SURVEY.md §8(d)
     end-to-end row): results in host memory, checked against the device-resident results; beside it
-    the H2D-only rate of the same bytes (the PCIe ceiling)."""
-    import torch
+    the H2D-only rate of the same bytes (the PCIe ceiling).  `ingest` is timed by record() or,
+    paired, inside cpu_baseline."""
 
-    host = torch.empty(nbuf * L, dtype=torch.uint8, pin_memory=True)
-    host.copy_(dev_step[: nbuf * L])
-    ptrs = [host.data_ptr() + i * L for i in range(nbuf)]
-    hy = ingest_rates(eng, ALG[alg], ptrs, [L] * nbuf)
-    parity = hy.pop("results")[:nbuf] == gpu_results[:nbuf]
-    slot = torch.empty(min(nbuf * L, 256 << 20), dtype=torch.uint8, device=dev_step.device)
-    cs = torch.cuda.Stream(device=dev_step.device)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    with torch.cuda.stream(cs):
-        for off in range(0, nbuf * L, slot.numel()):
-            n = min(slot.numel(), nbuf * L - off)
-            slot[:n].copy_(host[off:off + n], non_blocking=True)
-    torch.cuda.synchronize()
-    el_h2d = time.perf_counter() - t1
-    del host
-    return dict(hy, h2d_only_gibs=round(nbuf * L / el_h2d / 2**30, 2), parity_with_device_path=parity,
-                sample=f"one step ({nbuf} x {L} B) from pinned host memory, results to host memory")
+    def __init__(self, eng, alg, dev_step, nbuf, L):
+        import torch
+
+        self.host = torch.empty(nbuf * L, dtype=torch.uint8, pin_memory=True)
+        self.host.copy_(dev_step[: nbuf * L])
+        self.dev, self.nbuf, self.L = dev_step.device, nbuf, L
+        self.ingest = IngestLegs(eng, ALG[alg], [self.host.data_ptr() + i * L for i in range(nbuf)], [L] * nbuf)
+
+    def record(self, gpu_results):
+        import torch
+
+        hy = self.ingest.record()
+        parity = self.ingest.results()[: self.nbuf] == gpu_results[: self.nbuf]
+        total = self.nbuf * self.L
+        slot = torch.empty(min(total, 256 << 20), dtype=torch.uint8, device=self.dev)
+        cs = torch.cuda.Stream(device=self.dev)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        with torch.cuda.stream(cs):
+            for off in range(0, total, slot.numel()):
+                n = min(slot.numel(), total - off)
+                slot[:n].copy_(self.host[off:off + n], non_blocking=True)
+        torch.cuda.synchronize()
+        el_h2d = time.perf_counter() - t1
+        self.host = None
+        return dict(hy, h2d_only_gibs=round(total / el_h2d / 2**30, 2), parity_with_device_path=parity,
+                    sample=f"one step ({self.nbuf} x {self.L} B) from pinned host memory, results to host memory")
 
 
 def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,
@@ -407,54 +457,70 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
     trf = pmc_traffic(alg, nbuf, L, per)
     if trf:
         rec["roofline"]["traffic"], rec["roofline"]["traffic_source"] = trf
+    e2e = None
+    if do_e2e and alg not in ("xxh64", "xxh3_64", "xxh3_128"):  # host-ingest hash jobs run on the host path
+        torch.cuda.synchronize()
+        e2e = E2EStep(eng, alg, data, nbuf, L)
     if do_cpu:
         # the whole step's buffers (buffers round-robin over the threads, so a sample
         # of fewer buffers than threads would leave cores idle)
         cpu_bufs = nbuf if cpu_bufs is None else cpu_bufs
         torch.cuda.synchronize()
         gpu0 = eng.as_unsigned(outs[0])
-        host = data[: cpu_bufs * L].cpu().numpy()
-        rec["cpu_baseline"] = cpu_baseline(eng, alg, host, cpu_bufs, L, gpu0, cpu_seconds)
-    if do_e2e and alg not in ("xxh64", "xxh3_64", "xxh3_128"):  # host-ingest hash jobs run on the host path
-        torch.cuda.synchronize()
-        rec["e2e_pinned"] = e2e_step(eng, alg, data, nbuf, L, eng.as_unsigned(outs[0]))
+        host = host_sample(data, cpu_bufs * L, e2e.host if e2e is not None else None)
+        rec["cpu_baseline"] = cpu_baseline(eng, alg, host, cpu_bufs, L, gpu0, cpu_seconds,
+                                           paired=e2e.ingest if e2e is not None else None)
+        del host
+    if e2e is not None:
+        rec["e2e_pinned"] = e2e.record(eng.as_unsigned(outs[0]))
     del data
     torch.cuda.empty_cache()
     return rec
 
 
-def e2e_pinned(eng, alg_id, dev_data, count, L, nb, iters, wide):
+class E2EPinned:
     """Pinned host memory -> results in host memory through the engine's host-ingest API
-    (aws_crt_amd_host_submit / aws_crt_amd_job_wait: per-device 3-slot pipeline, H2D on a copy stream
-    overlapping the scans, results D2H), `iters` C2 batches of parts in one job; checked against the
-    device-resident results of the same bytes.  Also the H2D-only rate of the same bytes (the PCIe
-    ceiling of the pipeline)."""
-    import torch
+    (aws_crt_amd_host_submit / aws_crt_amd_job_wait: device lanes with a 3-slot pipeline, H2D on a copy
+    stream overlapping the scans, results D2H, beside the host path), `iters` C2 batches of parts in
+    one job; checked against the device-resident results of the same bytes.  Also the H2D-only rate of
+    the same bytes (the PCIe ceiling of the pipeline).  `ingest` is timed by record() or, paired,
+    inside cpu_baseline."""
 
-    step = count * L
-    host = torch.empty(nb * step, dtype=torch.uint8, pin_memory=True)
-    host.copy_(dev_data[: nb * step])
-    base = host.data_ptr()
-    ptrs = [base + (i % nb) * step + j * L for i in range(iters) for j in range(count)]
-    lens = [L] * len(ptrs)
-    first = eng.host_job(alg_id, ptrs[:count], lens[:count])
-    hy = ingest_rates(eng, alg_id, ptrs, lens)
-    res = hy.pop("results")
-    dev_out = eng.checksum_strided(alg_id, dev_data, L, L, count)
-    torch.cuda.synchronize()
-    parity = first == eng.as_unsigned(dev_out) and res[:count] == first
-    slot = torch.empty(step, dtype=torch.uint8, device=dev_data.device)
-    cs = torch.cuda.Stream(device=dev_data.device)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    with torch.cuda.stream(cs):
-        for i in range(iters):
-            slot.copy_(host[(i % nb) * step:((i % nb) + 1) * step], non_blocking=True)
-    torch.cuda.synchronize()
-    el_h2d = time.perf_counter() - t1
-    return dict(hy, h2d_only_gibs=round(iters * step / el_h2d / 2**30, 2), parity_with_device_path=parity,
-                sample=f"{iters} C2 batches ({iters * count} parts of {L // 1024} KiB) from {nb * step >> 20} MiB pinned host "
-                       f"memory in one host job, results to host memory")
+    def __init__(self, eng, alg_id, dev_data, count, L, nb, iters):
+        import torch
+
+        self.eng, self.alg_id, self.dev_data, self.count, self.L, self.nb, self.iters = eng, alg_id, dev_data, count, L, nb, iters
+        step = count * L
+        self.host = torch.empty(nb * step, dtype=torch.uint8, pin_memory=True)
+        self.host.copy_(dev_data[: nb * step])
+        base = self.host.data_ptr()
+        self.ptrs = [base + (i % nb) * step + j * L for i in range(iters) for j in range(count)]
+        self.ingest = IngestLegs(eng, alg_id, self.ptrs, [L] * len(self.ptrs))
+
+    def record(self):
+        import torch
+
+        eng, count, L, nb, iters = self.eng, self.count, self.L, self.nb, self.iters
+        step = count * L
+        first = eng.host_job(self.alg_id, self.ptrs[:count], [L] * count)
+        hy = self.ingest.record()
+        res = self.ingest.results()
+        dev_out = eng.checksum_strided(self.alg_id, self.dev_data, L, L, count)
+        torch.cuda.synchronize()
+        parity = first == eng.as_unsigned(dev_out) and res[:count] == first
+        slot = torch.empty(step, dtype=torch.uint8, device=self.dev_data.device)
+        cs = torch.cuda.Stream(device=self.dev_data.device)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        with torch.cuda.stream(cs):
+            for i in range(iters):
+                slot.copy_(self.host[(i % nb) * step:((i % nb) + 1) * step], non_blocking=True)
+        torch.cuda.synchronize()
+        el_h2d = time.perf_counter() - t1
+        self.host = self.dev_data = None
+        return dict(hy, h2d_only_gibs=round(iters * step / el_h2d / 2**30, 2), parity_with_device_path=parity,
+                    sample=f"{iters} C2 batches ({iters * count} parts of {L // 1024} KiB) from {nb * step >> 20} MiB pinned host "
+                           f"memory in one host job, results to host memory")
 
 
 def main_inproc(args):
@@ -710,16 +776,19 @@ def main():
     cpu = e2e = None
     configs = {}
     if rank == 0 and world == 1:
+        e2e_legs = E2EPinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches) if args.e2e_batches > 0 else None
         if not args.no_cpu_baseline:
             # the sample: every resident batch (as many bytes as the timed region streams, more than
             # the host's last-level cache, as the GPU's reads are beyond its caches), with one step
             # alone (cache-resident on the host) reported beside it
             torch.cuda.synchronize()
-            host = data[:nb * step_bytes].cpu().numpy()
+            host = host_sample(data, nb * step_bytes, e2e_legs.host if e2e_legs is not None else None)
             cpu = cpu_baseline(eng, alg, host, nb * count, L, eng.as_unsigned(outs[0]), args.cpu_seconds,
-                               step_buffers=count)
-        if args.e2e_batches > 0:
-            e2e = e2e_pinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches, wide)
+                               step_buffers=count, paired=e2e_legs.ingest if e2e_legs is not None else None)
+            del host
+        if e2e_legs is not None:
+            e2e = e2e_legs.record()
+            del e2e_legs
         if not args.no_configs:
             del data
             torch.cuda.empty_cache()

@@ -324,7 +324,9 @@ AWS_CRT_AMD_API int aws_crt_amd_host_submit(
  * own and the HIP runtime's), 0 = devices only (the PCIe-bound pipeline), n = n host threads beside
  * the lanes.  device_bytes (optional): set by aws_crt_amd_job_wait to the bytes the devices
  * checksummed.  AWS_CRT_AMD_INGEST_TRACE=1 prints one JSON line per job to stderr (claims, when each
- * side ran out of work, the lanes' staging / issue / wait times).
+ * side ran out of work, the lanes' staging / issue / wait times, the NUMA node).  Host threads of a
+ * job >= 16 MiB whose bytes sit on one NUMA node run on that node's CPUs (as do
+ * aws_crt_amd_cpu_batch's); AWS_CRT_AMD_NUMA=0 turns that off.
  */
 struct aws_crt_amd_ingest_options {
     int ndevices;

@@ -145,3 +145,51 @@ def test_list_devices_and_devices_batches(engine):
     engine.checksum_devices(ALG["crc32c"], entries)
     for dev, (d, h) in enumerate(datas):
         assert engine.as_unsigned(outs[dev]) == [oracle.crc("crc32c", h[i * 65536:(i + 1) * 65536]) for i in range(64)]
+
+
+_NUMA_SCRIPT = r"""
+import json, random, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import aws_crt_amd as eng
+rng = random.Random(7)
+sizes = [3, 70000, (9 << 20) + 5, 1 << 20, (6 << 20) + 1] + [rng.randrange(1, 1 << 20) for _ in range(40)]
+bufs = [np.frombuffer(rng.randbytes(n), dtype=np.uint8) for n in sizes]
+ptrs, lens = [b.ctypes.data for b in bufs], [b.size for b in bufs]
+out = {}
+for alg in (0, 1, 2, 3):
+    out[alg] = {"batch": eng.cpu_batch(alg, ptrs, lens, threads=4),
+                "job": eng.host_job(alg, ptrs, lens, ndevices=-1, host_threads=4)}
+np.save(sys.argv[2], np.concatenate(bufs))
+print(json.dumps({"sizes": sizes, "out": out}))
+"""
+
+
+def test_numa_placed_host_path(tmp_path):
+    """Host-path jobs placed on a NUMA node (AWS_CRT_AMD_NUMA=force places them on a one-node host:
+    every index on pool workers moved onto the node's CPUs, the caller waiting) give the oracle's
+    values, for the batch call and the host-ingest job; the job's trace names the node."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aws-crt-cpp_amd")
+    env = dict(os.environ, AWS_CRT_AMD_NUMA="force", AWS_CRT_AMD_INGEST_TRACE="1", HIP_VISIBLE_DEVICES="")
+    blob = tmp_path / "bytes.npy"
+    r = subprocess.run([sys.executable, "-c", _NUMA_SCRIPT, pkg, str(blob)], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    data, off, bufs = np.load(blob), 0, []
+    for n in rec["sizes"]:
+        bufs.append(data[off:off + n])
+        off += n
+    names = {0: "crc32", 1: "crc32c", 2: "crc64nvme", 3: "xxh64"}
+    for alg, got in rec["out"].items():
+        want = [oracle.checksum(names[int(alg)], b, 0) for b in bufs]
+        assert got["batch"] == want and got["job"] == want, names[int(alg)]
+    # the CRC jobs' host threads (an xxHash job runs a thread per buffer outside the pool)
+    traces = [json.loads(l) for l in r.stderr.splitlines() if l.startswith('{"ingest_trace"')]
+    crc = [t for t in traces if t["host_threads"] > 0]
+    assert len(crc) == 3 and all(t["numa_node"] == 0 for t in crc), traces

@@ -42,14 +42,18 @@ def test_concurrent_callers_under_tsan():
     assert "ThreadSanitizer" not in r.stderr, r.stderr
 
 
+@pytest.mark.parametrize("numa", ["", "force"])
 @pytest.mark.parametrize("target,opts", [("build/ingest_tsan", {"TSAN_OPTIONS": "halt_on_error=1"}),
                                          ("build/ingest_asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})])
-def test_concurrent_host_jobs_under_sanitizers(target, opts):
+def test_concurrent_host_jobs_under_sanitizers(target, opts, numa):
     """Host-ingest jobs from six threads at once on the host path (tests/cpp/ingest_host_test.cpp):
     uncut jobs writing results directly, cut jobs joined with Combine, jobs and their vectors reused
-    across threads, coordinators on the shared runner threads -- under TSan and under ASan."""
+    across threads, coordinators on the shared runner threads -- under TSan and under ASan; with
+    AWS_CRT_AMD_NUMA=force the jobs of >= 16 MiB run on pool workers placed on the node."""
     _build(target)
     env = dict(os.environ, **opts)
+    if numa:
+        env["AWS_CRT_AMD_NUMA"] = numa
     r = subprocess.run([os.path.join(CPP, target)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "[PASS] ConcurrentHostJobs" in r.stdout, r.stdout
