@@ -3597,7 +3597,7 @@ struct LaneW8Basis {
 // bytes at (2 t + (i & 1)) mod 8 of a 128-byte line).  Round 4: thread e writing its own row made
 // every group 8-way conflicted -- 8,000 conflict cycles per CU before the first message.
 template <uint32_t POLY>
-__device__ __forceinline__ void lane_w8_fill(char *lds) {  // threads 0..255 of the workgroup
+__device__ __forceinline__ void lane_w8_tables(char *lds) {
     constexpr LaneW8Basis<POLY> B{};
     const uint32_t i = threadIdx.x, tl = (i & 7u) >> 1, half = i & 1u;
     uint32_t bl[8], bh[8];  // the bases of T_tl and T_(tl + 4)
@@ -3614,10 +3614,6 @@ __device__ __forceinline__ void lane_w8_fill(char *lds) {  // threads 0..255 of 
         for (int b = 0; b < 8; ++b) v ^= ((e >> b) & 1u) ? ((k & 1) ? bh[b] : bl[b]) : 0u;
         *(uint4 *)(lds + (e << 8) + (t << 5) + (half << 4)) = make_uint4(v, v, v, v);
     }
-}
-template <uint32_t POLY>
-__device__ __forceinline__ void lane_w8_tables(char *lds) {  // a 256-thread workgroup
-    lane_w8_fill<POLY>(lds);
     __syncthreads();
 }
 struct LaneW8 {
@@ -3794,272 +3790,6 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
     p.d_status[m] = st;
 }
 
-// Event-stream framing check, block-parallel (aws_crt_amd_eventstream_crcs when the bytes fit a
-// 32-bit buffer range).  The one-lane-per-message kernel above is bound by each lane's serial walk of
-// its own message: ~9 dependent 64-byte load rounds per message, one cache-line request per lane.
-// Here a wave takes 64 messages and cuts them into the aligned 64-byte blocks that hold them; in each
-// round lane l folds block 64 r + l (coalesced 4 x 16-byte loads: neighbouring lanes read
-// neighbouring blocks), bytes outside its message masked to zero.  The message register is then
-//   U(~0, m) = x^(-8 pad) * ( sum_i c_i X^(n-1-i)  ^  I[lo] X^(n-1) )
-// with c_i the zero-init register of block i (leading zeros are free), X = x^512, lo the message's
-// start in its first block (I[lo] = ~0 x^(8 (64 - lo)): the init entering at byte lo) and pad the
-// zeros after its end in its last block.  Within a round the blocks of one message form a segment of
-// lanes: each lane multiplies its c by X^(segment end - l) (nibble tables in LDS), an XOR scan over
-// the wave (DPP) sums the segments, and a message running on from the previous round enters as a
-// carry times X^(segment length).  LDS: LaneW8 (64 KiB), the X^e / x^(-8 p) / I tables (66 KiB,
-// engine.cpp get_es_consts), 1 KiB per wave of message prefix sums.
-#ifndef AMDCRC_ES_XP
-#define AMDCRC_ES_XP 0  // experiment builds (wrong results): 1 = no rounds, 2 = rounds load but fold nothing
-#endif
-constexpr int kEsBlock = 512;
-constexpr int kEsWaves = kEsBlock / 64;
-constexpr uint32_t kEsTabOff = kLaneW8Lds;
-constexpr uint32_t kEsWaveOff = kEsTabOff + kEsConstWords * 4;
-// per wave: block prefix [65] (padded), (first block | prelude ok, start, end), (message CRC, status),
-// and the message of each block when the wave has at most kEsMapBlocks
-constexpr uint32_t kEsMapBlocks = 1024;
-constexpr uint32_t kEsWaveBytes = 68 * 4 + 64 * 12 + 64 * 8 + kEsMapBlocks;
-constexpr uint32_t kEsNoRead = 0x80000000u;  // a buffer offset past any range the kernel takes (< 2 GiB)
-constexpr uint32_t kEsLds = kEsWaveOff + kEsWaves * kEsWaveBytes;
-
-__device__ __forceinline__ uint32_t es_mul(const char *L, uint32_t tab, uint32_t v) {  // v * K, K's nibble table at byte tab
-    uint32_t x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = lds32(L, tab + (((uint32_t)i << 6) | (((v >> (4 * i)) & 15u) << 2)));
-    return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
-}
-
-__device__ __forceinline__ uint32_t wave_xor_scan(uint32_t v) {  // inclusive, over the 64 lanes
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    return v;
-}
-
-// the dword at byte o (< 16 + 4 * (3 - i)) of x[0..7], i-th of consecutive ones
-// (selects by v_perm: written as ?: the compiler turned them into a scratch array lookup)
-__device__ __forceinline__ uint32_t es_dword(const uint32_t *x, uint32_t o, int i) {
-    const uint32_t s1 = (o & 4u) ? 0x07060504u : 0x03020100u, s2 = (o & 8u) ? 0x07060504u : 0x03020100u;
-    uint32_t y[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) y[j] = __builtin_amdgcn_perm(x[i + j + 1], x[i + j], s1);
-    const uint32_t lo = __builtin_amdgcn_perm(y[2], y[0], s2), hi = __builtin_amdgcn_perm(y[3], y[1], s2);
-    return __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
-}
-
-struct EsSlot {
-    v4u d[4];         // the block's 64 bytes
-    v4u t0, t1;       // final block: the 32 bytes holding the stored message CRC
-    uint64_t heads;   // the round's segment heads (wave-uniform)
-    uint32_t bs, lo, hi, ep, mi;
-    bool act, first, fin, pre_ok;
-};
-
-__global__ __launch_bounds__(kEsBlock) void eventstream_block_kernel(const EventStreamParams p) {
-    __shared__ __attribute__((aligned(16))) char lds[kEsLds];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t m0 = ((uint64_t)blockIdx.x * kEsWaves + wv) * 64, m = m0 + lane;
-    const uint64_t abase = (uint64_t)p.base & ~63ull;
-    const uint32_t shift0 = (uint32_t)((uint64_t)p.base & 63u);
-    const __amdgpu_buffer_rsrc_t rs = list_rsrc(abase, shift0 + (uint32_t)p.limit);
-    // phase 0: the prelude of message m (32 aligned bytes holding its first 12)
-    const bool have = m < p.count;
-    const uint64_t off = have ? p.d_offsets[m] : 0;
-    const bool inr = have && off <= p.limit && p.limit - off >= 16;
-    const uint32_t a = shift0 + (uint32_t)off;
-    v4u h0 = {0, 0, 0, 0}, h1 = {0, 0, 0, 0};
-    if (inr) {
-        h0 = __builtin_amdgcn_raw_buffer_load_b128(rs, a & ~15u, 0, 0);
-        h1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (a & ~15u) + 16u, 0, 0);
-    }
-    if (threadIdx.x < 256) {
-        lane_w8_fill<kPoly32>(lds);
-    } else {  // the constant image: every load issued before the first store (one L2 round trip)
-        constexpr uint32_t kN = kEsConstWords / 4, kPer = (kN + 255) / 256;
-        const v4u *src = (const v4u *)p.d_consts;
-        v4u *dst = (v4u *)(lds + kEsTabOff);
-        const uint32_t t = threadIdx.x - 256u;
-        v4u c[kPer];
-#pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i) c[i] = t + 256u * i < kN ? src[t + 256u * i] : v4u{0, 0, 0, 0};
-#pragma unroll
-        for (uint32_t i = 0; i < kPer; ++i)
-            if (t + 256u * i < kN) dst[t + 256u * i] = c[i];
-    }
-    __syncthreads();
-    LaneW8 f;
-    f.init(lds, lane);
-    uint32_t st = 4u, pre = 0, nblk = 0, ep = 0, fbp = 0;
-    if (inr) {
-        const uint32_t x[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-        const uint32_t o = a & 15u, d0 = es_dword(x, o, 0), d1 = es_dword(x, o, 1), d2 = es_dword(x, o, 2);
-        const uint32_t total = __builtin_bswap32(d0), headers = __builtin_bswap32(d1);
-        if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
-            pre = ~f.word(~0u, ((uint64_t)d1 << 32) | d0);
-            ep = a + total - 4;
-            fbp = (a >> 6) | (__builtin_bswap32(d2) == pre ? 0x80000000u : 0u);
-            nblk = ((ep + 63u) >> 6) - (a >> 6);
-            st = 0;
-        }
-    }
-    if (have) {
-        p.d_prelude_crc[m] = pre;
-        if (st) {
-            p.d_message_crc[m] = 0;
-            p.d_status[m] = st;
-        }
-    }
-    // the wave's block prefix sums
-    uint32_t inc = nblk;
-#pragma unroll
-    for (int dlt = 1; dlt < 64; dlt <<= 1) {
-        const uint32_t t = __shfl_up(inc, dlt, 64);
-        if (lane >= (uint32_t)dlt) inc += t;
-    }
-    const uint32_t B = __shfl(inc, 63, 64);
-    uint32_t *ws = (uint32_t *)(lds + kEsWaveOff + wv * kEsWaveBytes), *wi = ws + 68, *wo = wi + 192;
-    ws[lane] = inc - nblk;
-    if (lane == 63) ws[64] = B;
-    wi[3 * lane] = fbp;
-    wi[3 * lane + 1] = a;
-    wi[3 * lane + 2] = ep;
-    uint8_t *wmap = (uint8_t *)(wo + 128);
-    const bool mapped = B <= kEsMapBlocks;
-    if (mapped)
-        for (uint32_t i = inc - nblk; i < inc; ++i) wmap[i] = (uint8_t)lane;
-    __syncthreads();
-    auto prep = [&](EsSlot &S, uint32_t r) {
-        const uint32_t b = r * 64u + lane;
-        uint32_t mi = 0;
-        if (mapped) {
-            mi = b < B ? wmap[b] : 63u;
-        } else {
-#pragma unroll
-            for (uint32_t step = 32; step; step >>= 1)
-                if (ws[mi + step] <= b) mi += step;
-        }
-        const uint32_t s0 = ws[mi], n = ws[mi + 1] - s0, fb = wi[3 * mi], ia = wi[3 * mi + 1], iep = wi[3 * mi + 2];
-        const uint32_t k = b - s0, bs = ((fb & 0x7FFFFFFFu) + k) << 6;
-        S.act = b < B;
-        S.first = k == 0;
-        S.fin = k == n - 1;
-        S.pre_ok = fb >> 31;
-        S.mi = mi;
-        S.bs = bs;
-        S.ep = iep;
-        S.lo = ia > bs ? ia - bs : 0u;
-        S.hi = iep - bs < 64u ? iep - bs : 64u;
-        // the round's segments: a head at each message's first block, and at the lanes past the end
-        S.heads = __ballot(!S.act || S.first) | 1ull;
-        // no branch around the loads (rounds past the end and idle lanes read past the range: zeros,
-        // no traffic), so the waits before a fold count only the two rounds issued after it
-        const uint32_t vo = S.act ? bs : kEsNoRead, to = S.act && S.fin ? iep & ~15u : kEsNoRead;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) S.d[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 16u * i, 0, 0);
-        S.t0 = __builtin_amdgcn_raw_buffer_load_b128(rs, to, 0, 0);
-        S.t1 = __builtin_amdgcn_raw_buffer_load_b128(rs, to + 16u, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // the fold after it stays after the loads
-    };
-    // a block's register times X^(segment end - lane): two half-block chains (words 0-3, 4-7) joined
-    // by x^256, so that two rounds' four chains can interleave (the fold is LDS-latency bound)
-    auto blockv = [&](const EsSlot &S) -> uint32_t {
-        if (AMDCRC_ES_XP == 2) {  // consume the loads only
-            const v4u x = S.d[0] ^ S.d[1] ^ S.d[2] ^ S.d[3] ^ S.t0 ^ S.t1;
-            return x.x ^ x.y ^ x.z ^ x.w;
-        }
-        const uint32_t dw[16] = {S.d[0].x, S.d[0].y, S.d[0].z, S.d[0].w, S.d[1].x, S.d[1].y, S.d[1].z, S.d[1].w,
-                                 S.d[2].x, S.d[2].y, S.d[2].z, S.d[2].w, S.d[3].x, S.d[3].y, S.d[3].z, S.d[3].w};
-        const uint32_t wl = S.lo >> 3, wh = (S.hi - 1u) >> 3;
-        const uint64_t ml = ~0ull << (8u * (S.lo & 7u)), mh = (S.hi & 7u) ? (~0ull >> (8u * (8u - (S.hi & 7u)))) : ~0ull;
-        uint64_t x[8];
-#pragma unroll
-        for (uint32_t w = 0; w < 8; ++w) {
-            uint64_t v = ((uint64_t)dw[2 * w + 1] << 32) | dw[2 * w];
-            v = (w < wl || w > wh) ? 0ull : v;
-            v &= w == wl ? ml : ~0ull;
-            v &= w == wh ? mh : ~0ull;
-            x[w] = v;
-        }
-        uint32_t c1 = 0, c2 = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            c1 = f.word(c1, x[w]);
-            c2 = f.word(c2, x[w + 4]);
-        }
-        uint32_t c = es_mul(lds, kEsTabOff + kEsHalfWord * 4u, c1) ^ c2;
-        if (S.first) c ^= lds32(lds, kEsTabOff + (kEsInitWord + S.lo) * 4u);
-        c = S.act ? c : 0u;
-        const uint64_t above = S.heads & ~((2ull << lane) - 1ull);
-        const uint32_t send = above ? (uint32_t)__builtin_ctzll(above) - 1u : 63u;
-        return es_mul(lds, kEsTabOff + (kEsXeWord + 128u * (send - lane)) * 4u, c);
-    };
-    // the round's segment sums (XOR scan over the wave), the carry, and the finished messages
-    uint32_t carry = 0;
-    auto assemble = [&](const EsSlot &S, uint32_t v) {
-        if (AMDCRC_ES_XP == 2) {
-            if (v == 0x9E3779B9u) wo[2 * S.mi] = 1u;
-            return;
-        }
-        const uint64_t below = (2ull << lane) - 1ull;  // lanes 0..lane (all for lane 63)
-        const uint64_t above = S.heads & ~below;
-        const uint32_t send = above ? (uint32_t)__builtin_ctzll(above) - 1u : 63u;
-        const uint32_t sst = 63u - (uint32_t)__builtin_clzll(S.heads & below);
-        v = wave_xor_scan(v);
-        const uint32_t prev = __shfl(v, sst ? sst - 1u : 0u, 64);
-        uint32_t T = v ^ (sst ? prev : 0u);
-        if (carry && sst == 0) T ^= es_mul(lds, kEsTabOff + (kEsXeWord + 128u * (send + 1u)) * 4u, carry);
-        const uint32_t cont63 = (uint32_t)__builtin_amdgcn_readlane((int)(S.act && !S.fin), 63);
-        const uint32_t T63 = (uint32_t)__builtin_amdgcn_readlane((int)T, 63);
-        carry = cont63 ? T63 : 0u;
-        if (S.act && S.fin) {
-            const uint32_t pad = S.bs + 64u - S.ep;
-            const uint32_t msg = ~es_mul(lds, kEsTabOff + (kEsXiWord + 128u * pad) * 4u, T);
-            const uint32_t t[8] = {S.t0.x, S.t0.y, S.t0.z, S.t0.w, S.t1.x, S.t1.y, S.t1.z, S.t1.w};
-            const uint32_t stored = __builtin_bswap32(es_dword(t, S.ep & 15u, 0));
-            wo[2 * S.mi] = msg;  // to LDS: a global store here would sit in the load counter's count
-            wo[2 * S.mi + 1] = (S.pre_ok ? 1u : 0u) | (stored == msg ? 2u : 0u);
-        }
-    };
-    const uint32_t R = (B + 63u) >> 6;
-    // Six rounds per step in pairs: four slots, the next pair's loads in flight while a pair is folded,
-    // the slots rotating by unrolling (a register copy of a slot would wait for its loads).  Straight-
-    // line within a step: carried across the loop's back edge, the loads in flight made the compiler
-    // wait for all of them before every fold.  Rounds past R load nothing (kEsNoRead), fold to zero
-    // and are not assembled.
-    for (uint32_t r = 0; r < (AMDCRC_ES_XP == 1 ? 0u : R); r += 6) {
-        EsSlot sa, sb, sc, sd;
-        prep(sa, r);
-        prep(sb, r + 1);
-        prep(sc, r + 2);
-        prep(sd, r + 3);
-        {
-            const uint32_t va = blockv(sa), vb = blockv(sb);
-            assemble(sa, va);
-            if (r + 1 < R) assemble(sb, vb);
-        }
-        prep(sa, r + 4);
-        prep(sb, r + 5);
-        if (r + 2 < R) {
-            const uint32_t vc = blockv(sc), vd = blockv(sd);
-            assemble(sc, vc);
-            if (r + 3 < R) assemble(sd, vd);
-        }
-        if (r + 4 < R) {
-            const uint32_t va = blockv(sa), vb = blockv(sb);
-            assemble(sa, va);
-            if (r + 5 < R) assemble(sb, vb);
-        }
-    }
-    __syncthreads();
-    if (have && st == 0) {
-        p.d_message_crc[m] = wo[2 * lane];
-        p.d_status[m] = wo[2 * lane + 1];
-    }
-}
-
 }  // namespace
 
 #if AWS_CRT_AMD_DIAG  // diagnostic library only (lib/libaws-crt-cpp-amd-diag.so)
@@ -4222,10 +3952,6 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
 
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
     if (p->count == 0) return 0;
-    if (p->d_consts) {
-        launch(eventstream_block_kernel, (int)((p->count + kEsBlock - 1) / kEsBlock), kEsBlock, (hipStream_t)stream, p, ev);
-        return (int)hipGetLastError();
-    }
     const uint64_t blocks = (p->count + 255) / 256;
     launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
     return (int)hipGetLastError();

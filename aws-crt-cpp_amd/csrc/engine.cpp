@@ -146,7 +146,6 @@ struct Device {
     std::map<std::pair<int, uint64_t>, DevBuf> pcols;  // (alg, tile) -> tmax x W x u64
     std::map<std::pair<int, uint64_t>, uint64_t> pcols_tmax;
     std::map<std::pair<int, uint64_t>, DevBuf> xcd;    // (alg, waves per XCD) -> crc64_xcd_kernel constants
-    DevBuf es_consts;                                  // event-stream block kernel (kEsConstWords)
     std::vector<DevBuf> retired;                       // outgrown buffers queued kernels may still read
     StreamStates<hipStream_t, StreamState, StatePolicy> states{kMaxStreamStates};  // under mu
     // single path (GPU-dispatched host buffers, device buffers through the aws-checksums ABI)
@@ -243,38 +242,6 @@ int upload_new(DevBuf &b, const void *host, size_t bytes) {
 // x^-1 * t : inverse of gf2_mulx (the reflected polynomial's top bit is the x^0 coefficient, 1)
 inline uint32_t inv_mulx32(uint32_t t, uint32_t poly) { return (t & 0x80000000u) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 inline uint64_t inv_mulx64(uint64_t t, uint64_t poly) { return (t >> 63) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
-
-// Event-stream block kernel constants (engine.h kEsConstWords; CRC32): nibble tables of the block
-// shifts X^e = x^(512 e), e <= 64, of the pad removals x^(-8 p), p < 64, the init terms
-// ~0 * x^(8 (64 - l)) of a message starting at byte l of its first block, and the half-block shift
-// x^256.  Under d->mu.
-int get_es_consts(Device *d, const uint32_t **out) {
-    if (!d->es_consts.p) {
-        const uint32_t poly = kPoly32;
-        std::vector<uint32_t> c(kEsConstWords, 0);
-        auto nib = [&](uint32_t base, uint32_t k) {
-            for (int i = 0; i < 8; ++i)
-                for (uint32_t u = 0; u < 16; ++u) c[base + 16 * i + u] = (uint32_t)gf2_mulmod((uint64_t)u << (4 * i), k, poly, 32);
-        };
-        for (uint32_t e = 0; e <= 64; ++e) nib(kEsXeWord + 128 * e, (uint32_t)gf2_xpow8n(64ull * e, poly, 32));
-        uint32_t xi = 0x80000000u;  // x^0, then x^(-8 p)
-        for (uint32_t q = 0; q < 64; ++q) {
-            nib(kEsXiWord + 128 * q, xi);
-            for (int i = 0; i < 8; ++i) xi = inv_mulx32(xi, poly);
-        }
-        for (uint32_t l = 0; l < 64; ++l)
-            c[kEsInitWord + l] = (uint32_t)gf2_mulmod(0xFFFFFFFFu, gf2_xpow8n(64 - l, poly, 32), poly, 32);
-        nib(kEsHalfWord, (uint32_t)gf2_xpow8n(32, poly, 32));
-        int rc = upload_new(d->es_consts, c.data(), c.size() * sizeof(uint32_t));
-        if (rc) {
-            if (d->es_consts.p) (void)hipFree(d->es_consts.p);
-            d->es_consts = DevBuf{};
-            return rc;
-        }
-    }
-    *out = (const uint32_t *)d->es_consts.p;
-    return 0;
-}
 
 // W=32 braided-scan constants (layout: engine.h kBraidConstWords): the K image of x^(-32 l) (32 matrix
 // columns per lane), T' (the row step's slice-by-4 tables) and T0 (byte table)
@@ -1943,18 +1910,7 @@ AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(const void *base, uint64_t limi
         Device *d;
         int rc = get_device(&d);
         if (rc) return rc;
-        // the block kernel addresses the bytes through a buffer resource based at the 64-byte line
-        // holding base, with offsets under 2 GiB (kEsNoRead); larger ranges take one lane per message
-        const uint32_t *consts = nullptr;
-#ifndef AMDCRC_ES_LANES
-#define AMDCRC_ES_LANES 0  // experiment builds: 1 = one lane per message always
-#endif
-        if (!AMDCRC_ES_LANES && ((uintptr_t)base & 63) + limit < 0x80000000ull) {
-            std::lock_guard<std::mutex> g(d->mu);
-            rc = get_es_consts(d, &consts);
-            if (rc) return rc;
-        }
-        EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status, consts};
+        EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status};
         int e = amdcrc_launch_eventstream(&ep, hip_stream, g_time_events);
         g_time_events[0] = g_time_events[1] = nullptr;
         return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("event-stream kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;

@@ -158,21 +158,11 @@ struct LaneParams {
 };
 
 // Event-stream framing check (eventstream_kernel)
-// Event-stream block kernel constants (u32 words): nibble tables (8 positions x 16 values) of
-// X^e = x^(512 e) for e = 0..64, of x^(-8 p) for p = 0..63, I[l] = ~0 * x^(8 (64 - l)) for l < 64,
-// and the nibble table of x^256 (a half block)
-constexpr uint32_t kEsXeWord = 0;
-constexpr uint32_t kEsXiWord = 65 * 128;
-constexpr uint32_t kEsInitWord = kEsXiWord + 64 * 128;
-constexpr uint32_t kEsHalfWord = kEsInitWord + 64;
-constexpr uint32_t kEsConstWords = kEsHalfWord + 128;
-
 struct EventStreamParams {
     const uint8_t *base;
     const uint64_t *d_offsets;  // message starts, bytes from base
     uint64_t count, limit;      // limit: bytes readable from base
     uint32_t *d_prelude_crc, *d_message_crc, *d_status;
-    const uint32_t *d_consts;   // kEsConstWords (block kernel; null: one lane per message)
 };
 
 }  // namespace amdcrc
