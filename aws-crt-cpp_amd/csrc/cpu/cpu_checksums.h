@@ -97,5 +97,10 @@ void parallel(size_t n, const std::function<void(size_t)> &fn, int node = -1);
 // else -1.  AWS_CRT_AMD_NUMA=0: always -1; =force: one node counts too (tests).
 int home_node(const uint8_t *const *ptrs, const size_t *lens, size_t count, size_t threads);
 
+// The process's CPU share: the CPUs it may run on (its allowed-CPU list, /proc/self/status, else the
+// affinity mask), capped by OMP_NUM_THREADS; computed once.  The host path's thread counts and
+// home_node's placement use this one figure.
+size_t share();
+
 }  // namespace cpu
 }  // namespace amdcrc

@@ -270,7 +270,6 @@ namespace {
 // AWS_CRT_AMD_NUMA=0 turns placement off, =force places jobs on a one-node host too (tests).
 struct Numa {
     std::vector<cpu_set_t> node_cpus;  // allowed CPUs per node (may be empty)
-    cpu_set_t all;                     // the mask at first use: what a worker returns to
     bool on = false;
 };
 
@@ -292,12 +291,35 @@ bool parse_cpulist(const std::string &s, cpu_set_t *set) {
     return true;
 }
 
+// The CPUs the process may run on: the allowed-CPU list of /proc/self/status (the process's mask,
+// whichever thread asks; sched_getaffinity(0) would return the calling thread's own, possibly pinned,
+// mask), else that of the calling thread.
+bool process_cpus(cpu_set_t *set) {
+    CPU_ZERO(set);
+    std::ifstream f("/proc/self/status");
+    std::string line;
+    while (std::getline(f, line))
+        if (line.compare(0, 19, "Cpus_allowed_list:\t") == 0 && parse_cpulist(line.substr(19), set) && CPU_COUNT(set) > 0)
+            return true;
+    CPU_ZERO(set);
+    return sched_getaffinity(0, sizeof(cpu_set_t), set) == 0;
+}
+
+const cpu_set_t &allowed_cpus() {
+    static const cpu_set_t s = [] {
+        cpu_set_t c;
+        if (!process_cpus(&c)) CPU_ZERO(&c);
+        return c;
+    }();
+    return s;
+}
+
 const Numa &numa() {
     static const Numa n = [] {
         Numa m;
-        CPU_ZERO(&m.all);
         const char *env = std::getenv("AWS_CRT_AMD_NUMA");
-        if ((env && env[0] == '0') || sched_getaffinity(0, sizeof(cpu_set_t), &m.all) != 0) return m;
+        const cpu_set_t &all = allowed_cpus();
+        if ((env && env[0] == '0') || CPU_COUNT(&all) == 0) return m;
         int populated = 0;
         for (int node = 0; node < 64; ++node) {
             std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
@@ -307,7 +329,7 @@ const Numa &numa() {
             cpu_set_t set;
             CPU_ZERO(&set);
             if (!parse_cpulist(line, &set)) break;
-            CPU_AND(&set, &set, &m.all);
+            CPU_AND(&set, &set, &all);
             populated += CPU_COUNT(&set) > 0;
             m.node_cpus.push_back(set);
         }
@@ -364,7 +386,9 @@ class Pool {
   private:
     void loop(size_t idx) {
         uint64_t seen = 0;
-        int placed = -1;  // the node this thread's mask is on (-1: the process mask)
+        int placed = -1;  // the node this thread's mask is on (-1: its mask at creation)
+        cpu_set_t own;    // what the worker returns to after a placed batch
+        const bool have_own = pthread_getaffinity_np(pthread_self(), sizeof(cpu_set_t), &own) == 0;
         for (;;) {
             const std::function<void(size_t)> *fn;
             size_t shift;
@@ -379,9 +403,9 @@ class Pool {
                 shift = shift_;
                 node = node_;
             }
-            if (node != placed) {
+            if (node != placed && (node >= 0 || have_own)) {
                 const Numa &m = numa();
-                pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), node >= 0 ? &m.node_cpus[(size_t)node] : &m.all);
+                pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), node >= 0 ? &m.node_cpus[(size_t)node] : &own);
                 placed = node;
             }
             (*fn)(idx - shift);
@@ -434,6 +458,19 @@ int home_node(const uint8_t *const *ptrs, const size_t *lens, size_t count, size
     if (valid * 2 < k || votes[best] * 4 < valid * 3 || best >= m.node_cpus.size()) return -1;
     if ((size_t)CPU_COUNT(&m.node_cpus[best]) < threads) return -1;
     return (int)best;
+}
+
+size_t share() {
+    static const size_t s = [] {
+        size_t t = (size_t)CPU_COUNT(&allowed_cpus());
+        if (t == 0) t = std::max(1u, std::thread::hardware_concurrency());
+        if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+            const long v = std::strtol(e, nullptr, 10);
+            if (v > 0) t = std::min<size_t>(t, (size_t)v);
+        }
+        return std::max<size_t>(1, t);
+    }();
+    return s;
 }
 
 void parallel(size_t n, const std::function<void(size_t)> &fn, int node) {

@@ -23,6 +23,8 @@
 
 #include <type_traits>
 
+#include "variant_guard.h"
+
 #ifndef AMDCRC_R16_XCD  // compile-time only: crc64_rows16_kernel's sets in XCD-window order (1) or contiguous (0)
 #define AMDCRC_R16_XCD 1
 #endif
@@ -1607,15 +1609,6 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // loads in flight, and drained most of the ring at the top of every rotation (vmcnt 7..2 before the
     // first step's row loads); without the breaks every row waits exactly vmcnt(16).
     step(ra, rc, true);
-#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
-    while (q < nq) {
-        step(rb, ra, false);
-        if (q >= nq) break;
-        step(rc, rb, false);
-        if (q >= nq) break;
-        step(ra, rc, false);
-    }
-#else
     while (q + 3 <= nq) {
         step(rb, ra, false);
         step(rc, rb, false);
@@ -1625,7 +1618,6 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         step(rb, ra, false);
         if (q < nq) step(rc, rb, false);
     }
-#endif
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
     stream_publish(p, acc, eng, lane);
 }
@@ -1839,11 +1831,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         ga = g;
         u = 0;
         if (g == 0) {
-#ifdef AMDCRC_XP_LIST_NOHEAD  // experiment builds only (timing; results wrong): no head fold, no seed read
-            uint32_t s_h = ~0u;
-#else
             uint32_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
-#endif
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
@@ -1863,10 +1851,6 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     uint32_t nparts = 0;  // parts this wave has finished
     // the part [ga, g) ends: its share, moved to the buffer's end, finishes the buffer or joins it
     auto part_finish = [&]() {
-#ifdef AMDCRC_XP_LIST_NOFINISH  // experiment builds only (timing; results wrong): a part stores its lane-0 braid
-        if (lane == 0) asm volatile("global_store_dword %0, %1, off" : : "v"((uint32_t *)p.d_out + sc.b), "v"(u) : "memory");
-        return;
-#endif
         uint32_t r = wave_xor_s(eng.mulK(u, lane));
         const uint32_t mg = sc.vg - g;  // groups after the part
         if (mg && mg < (uint32_t)kBraidGmCount) {
@@ -2049,22 +2033,13 @@ struct Braid64 {
     __device__ __forceinline__ uint64_t step_x(uint64_t a, uint64_t wn) const {
         const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
         // COPIES = 4: slots 0..3 read dword ma, slots 4..7 dword mb (per lane half, see the layout)
-#ifdef AMDCRC_XP64_NOBFI  // experiment builds only: the byte sources without the per-lane dword select
-        const uint32_t ma = lo, mb = hi;
-#else
         const uint32_t ma = COPIES == 8 ? lo : (lo & lowmask) | (hi & ~lowmask);
         const uint32_t mb = COPIES == 8 ? hi : (hi & lowmask) | (lo & ~lowmask);
-#endif
         uint64_t v[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-#ifdef AMDCRC_XP64_NOLDS  // experiment builds only: the address perms without the table reads
-            v[k] = __builtin_amdgcn_perm(cst[k], ma, sel[k]);
-            v[4 + k] = (uint64_t)__builtin_amdgcn_perm(csth[k], mb, sel[k]) << 32;
-#else
             v[k] = lds64(L, __builtin_amdgcn_perm(cst[k], ma, sel[k]));
             v[4 + k] = lds64(L, __builtin_amdgcn_perm(csth[k], mb, sel[k]));
-#endif
         }
         uint32_t rl = xor3(xor3((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2]), (uint32_t)v[3], (uint32_t)v[4]);
         rl = xor3(xor3(rl, (uint32_t)v[5], (uint32_t)v[6]), (uint32_t)v[7], (uint32_t)wn);
@@ -2442,11 +2417,7 @@ __device__ __forceinline__ void stream64_issue(B64Group &g, uint32_t voff, uint6
 // per buffer; the buffer's last group finalises.
 template <class B>
 __device__ __forceinline__ void stream64_finish(const ScanParams &p, const Tile &d, uint64_t u, const B &eng, int lane) {
-#ifdef AMDCRC_XP64_NOFINISH  // experiment builds only: tiles end without the lane shares' product and reduction
-    const uint64_t r = __builtin_amdgcn_readfirstlane((uint32_t)u);
-#else
     const uint64_t r = wave_xor64_s(eng.mulK(u));
-#endif
     if (d.T == 1) {
         if (lane == 0) finalize<false>(p, d.b, r, eng);
         return;
@@ -2569,16 +2540,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
             if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
         }
     };
-#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
-    for (;;) {
-        step(ra, rc);
-        if (q >= nq) break;
-        step(rb, ra);
-        if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
-    }
-#else
     // whole rotations of three steps, then the rest (the breaks drained the ring at every loop
     // header: see crc32_stream_kernel)
     while (q + 3 <= nq) {
@@ -2590,7 +2551,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
         step(ra, rc);
         if (q < nq) step(rb, ra);
     }
-#endif
 }
 
 
@@ -2804,12 +2764,10 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     uint32_t hn = 0;
     auto part_finish = [&]() {
         const uint64_t r = part_raw();
-#ifndef AMDCRC_XP_XCD_NOPUB  // experiment builds only (timing; results wrong): mid-scan parts dropped
         if (hb != ~0ull) {
             const uint64_t v = shift_scalar(hr, CPB - 1 - hk);
             if (lane == 0) publish(hb, v, hn);
         }
-#endif
         hb = pb, hr = r, hk = pk, hn = pn;
     };
     // every wave's held and last parts go through LDS: wave 0 joins the parts of one buffer, so the
@@ -3244,16 +3202,6 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
             s += sstep;
         }
     };
-#ifdef AMDCRC_XP_RING_BREAKS  // experiment builds only: the round-2 loop, for A/B timing
-    for (;;) {
-        step(ra, rc);
-        if (q >= nq) break;
-        step(rb, ra);
-        if (q >= nq) break;
-        step(rc, rb);
-        if (q >= nq) break;
-    }
-#else
     // whole rotations of three steps, then the rest (the breaks drained the ring at every loop
     // header: see crc32_stream_kernel)
     while (q + 3 <= nq) {
@@ -3265,7 +3213,6 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
         step(ra, rc);
         if (q < nq) step(rb, ra);
     }
-#endif
     // the trailing placeholder rows: their registers stay live until the loads have landed
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]), "+v"(ra.w[5]),
                  "+v"(ra.w[6]), "+v"(ra.w[7])::"memory");

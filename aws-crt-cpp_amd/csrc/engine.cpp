@@ -10,6 +10,8 @@
 // No library call synchronises the whole device.  Growing a cached table or workspace never frees
 // memory that queued kernels may still read: the old allocation is retired (kept until process
 // exit; growth is geometric, so retired memory is bounded by the live size).
+#include "variant_guard.h"
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,6 +35,7 @@
 #include "cpu/cpu_checksums.h"
 #include "engine.h"
 #include "gf2.h"
+#include "ptr_class.h"
 #include "stream_states.h"
 
 #define AWS_CRT_AMD_BUILD 1
@@ -529,9 +532,6 @@ constexpr bool kXcd = AMDCRC_XCD != 0;
 #define AMDCRC_XCD_MIN_CHUNKS 256
 #endif
 constexpr uint64_t kXcdMinChunks = AMDCRC_XCD_MIN_CHUNKS;
-#ifndef AMDCRC_XP_STREAM64  // experiment: 0 sends aligned strided CRC64NVME batches to crc64_braid_kernel
-#define AMDCRC_XP_STREAM64 1
-#endif
 // W=32 streaming scans in XCD-window tile order (16 KiB tiles)
 #ifndef AMDCRC_STREAM_XCD  // compile-time only (A/B builds)
 #define AMDCRC_STREAM_XCD 0
@@ -921,7 +921,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     const bool small = ml * count < kSmallBatchBytes;
     const uint64_t wpc = w32 ? 8 * (small ? 1 : 2) : small ? 4 : (uint64_t)kWavesPerBlock;
     const uint32_t seg_stream = choose_seg(d, ml * count, ml, 1, wpc);
-    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0 && (w32 || AMDCRC_XP_STREAM64);
+    const bool stream = ml > 0 && ml % ((uint64_t)seg_stream * kWave) == 0;
     if (stream) p.seg = seg_stream;
     // W=32 braided scan: every wave scans one static tile, then claims tiles from its workgroup's
     // pool, where the pool does not shrink the tiles (smaller tiles cost a tile finish per 8 KiB and
@@ -1180,9 +1180,6 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         std::vector<uint64_t> sorted(mains);
         std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
         seg = choose_seg(d, total, sorted[count / 2]);
-#ifdef AMDCRC_XP_LIST_SEG_DIV  // experiment builds only: smaller list tiles (balance vs finishes)
-        seg = std::max<uint32_t>(kGroupBytes, seg / AMDCRC_XP_LIST_SEG_DIV);
-#endif
         tile = (uint64_t)seg * kWave;
     }
     // descriptor block: ptrs[count] lens[count] prefix[count+1] wavebuf[nwaves]
@@ -1262,18 +1259,25 @@ int ensure_stage(Device *d, size_t bytes) {
     return 0;
 }
 
-bool is_device_ptr(const void *p) {
-    if (!p || device_count_noinit() <= 0) return false;
+// the runtime's view of a pointer (ptr_class.h): 0 unregistered host, 1 runtime-known host, 2 device
+int probe_ptr(const void *p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return 0;
     }
-    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.type == hipMemoryTypeUnified;
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged || a.type == hipMemoryTypeUnified) return 2;
+    return a.type == hipMemoryTypeUnregistered ? 0 : 1;
+}
+using Classifier = PtrClass<probe_ptr>;
+
+bool is_device_ptr(const void *p) {
+    if (!p || device_count_noinit() <= 0) return false;
+    return Classifier::classify(p) == PtrKind::Device;
 }
 
 constexpr size_t kStageChunk = 16u << 20;
-constexpr size_t kHashStageMax = 256u << 20;  // cached device copy of a GPU-dispatched host hash
+constexpr size_t kHashStageMax = 64u << 20;  // cached device copy of a GPU-dispatched host hash (kept <= 64 MiB)
 
 // One buffer (host or device memory) on the GPU, synchronous.  Host data streams through two pinned
 // slots; chunk i+1 is seeded on the device with chunk i's result, so no host round trip sits
@@ -1377,6 +1381,11 @@ extern "C" int amdcrc_gpu_usable(void) {
     });
 }
 extern "C" int amdcrc_is_device_ptr(const void *p) { return is_device_ptr(p) ? 1 : 0; }
+#if AWS_CRT_AMD_DIAG
+// diagnostic library only: runtime pointer probes made by the calling thread (tests: the small-call
+// path stays out of the HIP runtime)
+extern "C" AWS_CRT_AMD_API unsigned long long aws_crt_amd_debug_pointer_probes(void) { return Classifier::tls().probes; }
+#endif
 extern "C" int amdcrc_gpu_single(int alg, const void *input, size_t len, uint64_t seed, uint64_t *out) {
     return guarded(err_sink, [&]() -> int {
         return single_impl(alg, input, len, seed, out);
@@ -1674,6 +1683,7 @@ struct aws_crt_amd_queue {
     };
     std::deque<Launch> launches;                               // recent launches, oldest first
     std::vector<Launch> failed;                                // pruned refused launches (bounded)
+    uint64_t expired_below = 0;                                // tickets below this may have lost their record
     std::vector<hipEvent_t> spare;                             // events of completed, pruned launches
     std::thread flusher;
     bool stop = false;
@@ -1687,8 +1697,17 @@ void queue_prune_locked(aws_crt_amd_queue *q) {
     while (q->launches.size() > kQueueKeepLaunches) {
         aws_crt_amd_queue::Launch &L = q->launches.front();
         if (L.rc) {
-            if (q->failed.size() >= kQueueKeepFailures) q->failed.erase(q->failed.begin());
-            q->failed.push_back(L);
+            // adjacent refused launches with one status share a record; past the bound the oldest
+            // record goes and its tickets (and every pruned one below them) report EXPIRED, never 0
+            if (!q->failed.empty() && q->failed.back().end == L.first && q->failed.back().rc == L.rc) {
+                q->failed.back().end = L.end;
+            } else {
+                if (q->failed.size() >= kQueueKeepFailures) {
+                    q->expired_below = q->failed.front().end;
+                    q->failed.erase(q->failed.begin());
+                }
+                q->failed.push_back(L);
+            }
         } else if (hipEventQuery(L.ev) != hipSuccess) {
             (void)hipGetLastError();
             return;  // still running: keep it (and every later one)
@@ -1759,7 +1778,8 @@ int queue_status_locked(aws_crt_amd_queue *q, uint64_t ticket, hipEvent_t *ev) {
     }
     for (const auto &L : q->failed)
         if (ticket >= L.first && ticket < L.end) return L.rc;
-    return 0;  // pruned: completed
+    if (ticket < q->expired_below) return AWS_CRT_AMD_ERR_TICKET_EXPIRED;  // outcome no longer recorded
+    return 0;  // pruned: completed (a launch is pruned only once complete or refused)
 }
 }  // namespace
 

@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "variant_guard.h"
+
 namespace amdcrc {
 
 // Work decomposition (DESIGN.md "Data layout"): every buffer is split into

@@ -45,6 +45,7 @@
 #include "abi_guard.h"
 #include "cpu/cpu_checksums.h"
 #include "gf2.h"
+#include "runner.h"
 
 #define AWS_CRT_AMD_BUILD 1
 #include <aws_crt_amd/checksums_batch.h>
@@ -247,50 +248,6 @@ void lane_free(Lane &L) {
     if (L.comp) (void)hipStreamDestroy(L.comp);
 }
 
-// Threads that run jobs' host-side coordinators, kept for reuse (a std::thread per job cost its
-// creation, ~0.1 ms, on every job); one more is started when none is idle, so concurrent jobs still
-// run concurrently.
-class Runner {
-  public:
-    void post(std::function<void()> f) {
-        std::lock_guard<std::mutex> g(mu_);
-        q_.push_back(std::move(f));
-        if (idle_ == 0)
-            ts_.emplace_back([this] { loop(); });
-        else
-            cv_.notify_one();
-    }
-    ~Runner() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : ts_) t.join();
-    }
-
-  private:
-    void loop() {
-        std::unique_lock<std::mutex> g(mu_);
-        for (;;) {
-            ++idle_;
-            cv_.wait(g, [this] { return stop_ || !q_.empty(); });
-            --idle_;
-            if (q_.empty()) return;  // stopping
-            std::function<void()> f = std::move(q_.front());
-            q_.pop_front();
-            g.unlock();
-            f();
-            g.lock();
-        }
-    }
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<std::function<void()>> q_;
-    std::vector<std::thread> ts_;
-    size_t idle_ = 0;
-    bool stop_ = false;
-};
 Runner &runner() {
     static Runner r;
     return r;
@@ -586,16 +543,9 @@ bool fan_reserve(FanStream *f, size_t bytes) {
     return true;
 }
 
-// host-path threads for a job that runs on the CPU: the process's CPU share, at most one per buffer
-size_t host_threads(size_t count) {
-    const unsigned hw = std::thread::hardware_concurrency();
-    size_t t = hw ? hw : 1;
-    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v > 0) t = std::min<size_t>(t, (size_t)v);
-    }
-    return std::max<size_t>(1, std::min(t, std::max<size_t>(count, 1)));
-}
+// host-path threads for a job that runs on the CPU: the process's CPU share (cpu::share: its allowed
+// CPUs capped by OMP_NUM_THREADS, the figure home_node places by), at most one per buffer
+size_t host_threads(size_t count) { return std::max<size_t>(1, std::min(cpu::share(), std::max<size_t>(count, 1))); }
 
 int visible_devices() {
     int n = 0;

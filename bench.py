@@ -56,9 +56,11 @@ ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_
 WIDE = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the job; default: WORLD_SIZE under a launcher, else 1.  N > 1 without a "
+                         "launcher spawns N rank processes (one per GPU) before any GPU call")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (RCCL; gloo only to rehearse the rank path)")
     ap.add_argument("--steps", type=int, default=200)
@@ -81,7 +83,77 @@ def parse():
     ap.add_argument("--only-coalesced", action="store_true",
                     help="profiling runs: every scan launch has the timed region's shape (no one-batch warm-up or timing "
                          "launches), so a kernel-trace average is the dominant kernel's duration")
-    return ap.parse_args()
+    ap.add_argument("--plumbing-check", type=int, default=None, metavar="DEVICES",
+                    help="tests: assume DEVICES visible GPUs; each rank prints its rank / world / device assignment as "
+                         "JSON and exits, with no GPU call")
+    return ap.parse_args(argv)
+
+
+class PlumbingError(SystemExit):
+    """A launch whose ranks or devices do not match --gpus (exit status 2)."""
+
+    def __init__(self, msg):
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+        super().__init__(2)
+
+
+def rank_layout(args, env, device_count):
+    """Where this process sits in the job, before any GPU call: (world, rank, local rank, device index,
+    shared).  `--gpus` must equal the launcher's WORLD_SIZE; with RCCL every rank needs its own device,
+    with --dist-backend gloo ranks beyond the visible devices share them round-robin (a rehearsal of
+    the rank path on fewer GPUs, reported as such).  device_count: torch.cuda.device_count(), which on
+    this image counts without initialising the GPU."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    rank = int(env.get("RANK", "0"))
+    local = int(env.get("LOCAL_RANK", str(rank)))
+    gpus = world if args.gpus is None else args.gpus
+    if gpus != world:
+        raise PlumbingError(f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if device_count < 1:
+        raise PlumbingError("no GPU visible")
+    if local >= device_count and args.dist_backend == "nccl":
+        raise PlumbingError(f"rank {rank} (local {local}) has no GPU of its own: {device_count} visible, RCCL needs one "
+                            f"per rank (--dist-backend gloo rehearses the rank path on shared devices)")
+    return world, rank, local, local % device_count, world > device_count
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv=None):
+    """--gpus N > 1 with no launcher: start N rank processes of this script (fresh interpreters, one
+    per GPU: RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1) and wait for them.  This
+    process makes no GPU call.  The first rank to fail ends the others; the exit status is the first
+    non-zero one.  Rank 0 prints the JSON line."""
+    import subprocess
+
+    argv = sys.argv[1:] if argv is None else argv
+    port = str(free_port())
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
 
 
 def cpu_topology():
@@ -523,138 +595,247 @@ class E2EPinned:
                            f"memory in one host job, results to host memory")
 
 
-def main_inproc(args):
-    """In-process multi-device mode: each GPU holds its own rotating C2 batches; the steps are sharded
-    round-robin over the devices (step i -> device i % N) and each device's share is submitted as
-    coalesced launches on that device's stream, all devices at once; the timed region ends when every
-    device is done.  value = all devices' bytes / that time."""
-    import torch
-    import aws_crt_amd as eng
+def box_state(props):
+    """The GPU's clocks and partition modes as the kernel driver reports them (sysfs of the device's
+    PCI function: pp_dpm_sclk / pp_dpm_mclk / pp_dpm_fclk with the current level marked '*', the
+    compute and memory partition modes), so that a box-to-box spread in the kernel fractions can be
+    traced to its clocks or memory mode.  Fields the box does not expose are null."""
+    import glob
 
-    ndev = min(max(1, args.gpus), torch.cuda.device_count())
-    alg, count, L = args.alg, args.buffers, args.buffer_bytes
-    G = max(1, min(32, args.coalesce))
-    step_bytes, nb = count * L, max(1, args.batches)
-    per = []
-    for dv in range(ndev):
-        torch.cuda.set_device(dv)
-        eng.init()
-        g = torch.Generator(device=f"cuda:{dv}")
-        g.manual_seed(0x5EED + dv)
-        data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=f"cuda:{dv}", generator=g)
-        outs = [torch.empty(count, dtype=torch.int64 if alg in WIDE else torch.int32, device=f"cuda:{dv}") for _ in range(nb)]
-        per.append((data, outs, torch.cuda.Stream(device=f"cuda:{dv}")))
+    bus = getattr(props, "pci_bus_id", None)
+    dom = getattr(props, "pci_domain_id", 0) or 0
+    devid = getattr(props, "pci_device_id", 0) or 0
+    cands = []
+    if bus is not None:
+        cands.append(f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{devid:02x}.0")
+    cands += sorted(glob.glob("/sys/class/drm/card*/device"))
+    path = next((c for c in cands if os.path.exists(os.path.join(c, "pp_dpm_sclk"))), None)
 
-    def prepare(k):
-        subs = []
-        for dv in range(ndev):
-            data, outs, st = per[dv]
-            mine = list(range(dv, k, ndev))  # round-robin steps
-            cuts = split(len(mine), G)
-            for j in range(len(cuts) - 1):
-                bs = [(data.data_ptr() + (mine[i] // ndev % nb) * step_bytes, None, outs[mine[i] // ndev % nb])
-                      for i in range(cuts[j], cuts[j + 1])]
-                subs.append((dv, eng.BatchSet(ALG[alg], bs, L, L, count), st))
-        return subs
+    def rd(name, cur_only=False):
+        if path is None:
+            return None
+        try:
+            txt = open(os.path.join(path, name)).read().strip()
+        except OSError:
+            return None
+        if cur_only:
+            cur = [ln.split(":", 1)[-1].replace("*", "").strip() for ln in txt.splitlines() if ln.rstrip().endswith("*")]
+            return {"current": cur[0] if cur else None, "levels": [ln.strip() for ln in txt.splitlines()]}
+        return txt
 
-    def run(subs):
-        for dv, bs, st in subs:
-            torch.cuda.set_device(dv)
-            bs.run(st)
-        for dv in range(ndev):
-            torch.cuda.synchronize(dv)
-
-    run(prepare(max(args.warmup, ndev)))
-    subs = prepare(args.steps)
-    for dv in range(ndev):
-        torch.cuda.synchronize(dv)
-    t0 = time.perf_counter()
-    run(subs)
-    el = time.perf_counter() - t0
-    value = args.steps * step_bytes / el / 2**30
-    print(json.dumps({
-        "metric": "GiB/s CRC32C over device-resident buffers; % of HBM read peak", "value": round(value, 2),
-        "unit": "GiB/s", "n_gpus": ndev, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic (torch.randint bytes on device)",
-        "config": {"workload": f"{config_label(alg, count, L)}: {count} x {L // 1024} KiB per step, {alg.upper()}, steps round-robin over "
-                               f"{ndev} GPU(s) of one process", "launch": f"in-process fan-out, up to {G} batches per launch, "
-                               "one HIP stream per GPU", "parallelism": f"in-process, {ndev} device(s), no collective"},
-        "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / ndev / HBM_PEAK_GBS, 2)}), flush=True)
+    return {"sysfs": path, "sclk": rd("pp_dpm_sclk", True), "mclk": rd("pp_dpm_mclk", True),
+            "fclk": rd("pp_dpm_fclk", True), "compute_partition": rd("current_compute_partition"),
+            "memory_partition": rd("current_memory_partition"),
+            "power_profile": (rd("pp_power_profile_mode") or "").splitlines()[:1] or None}
 
 
-def main():
-    args = parse()
-    if args.inproc:
-        return main_inproc(args)
-    import torch
-    import torch.distributed as dist
-    import aws_crt_amd as eng
+class Rig:
+    """One GPU's share of the job (one rank, or one device of the in-process fan-out): its resident
+    batches -- at least --batches and never fewer than one launch holds, so every launch streams from
+    HBM and no launch reads a batch twice (aliased batches would hit in L2 / the Infinity Cache) --
+    their result buffers and streams, and the launch plans over them."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one rank per GPU; ranks beyond the visible devices share them round-robin (only for rehearsing
-    # the multi-rank path on fewer GPUs, with --dist-backend gloo)
-    local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    eng.init()
+    def __init__(self, eng, dev, args, seed):
+        import torch
 
-    alg, count, L = args.alg, args.buffers, args.buffer_bytes
-    # hash batches run one launch per batch (aws_crt_amd_checksum_batches coalesces CRC scans only),
-    # so their launch shape is one batch
-    G = 1 if alg in ("xxh64", "xxh3_64", "xxh3_128") else max(1, min(32, args.coalesce))
-    step_bytes = count * L
-    # resident batches: at least --batches, and never fewer than a launch holds, so no launch reads a
-    # batch twice (aliased batches in one launch would hit in L2 / the Infinity Cache)
-    nb = max(1, args.batches, widest(max(args.steps, 1), G), widest(max(args.warmup, 1), G))
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + rank)
-    data = torch.randint(0, 256, (nb * step_bytes,), dtype=torch.uint8, device=dev, generator=g)
-    wide = alg in WIDE
-    per = 2 if alg == "xxh3_128" else 1
-    outs = [torch.empty(count * per, dtype=torch.int64 if wide else torch.int32, device=dev) for _ in range(nb)]
-    streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.branches))]
+        self.eng, self.dev, self.args = eng, dev, args
+        self.alg, self.count, self.L = args.alg, args.buffers, args.buffer_bytes
+        # hash batches run one launch per batch (aws_crt_amd_checksum_batches coalesces CRC scans only)
+        self.G = 1 if self.alg in ("xxh64", "xxh3_64", "xxh3_128") else max(1, min(32, args.coalesce))
+        self.step_bytes = self.count * self.L
+        self.nb = max(1, args.batches, widest(max(args.steps, 1), self.G), widest(max(args.warmup, 1), self.G))
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        self.data = torch.randint(0, 256, (self.nb * self.step_bytes,), dtype=torch.uint8, device=dev, generator=g)
+        self.per = 2 if self.alg == "xxh3_128" else 1
+        odt = torch.int64 if self.alg in WIDE else torch.int32
+        self.outs = [torch.empty(self.count * self.per, dtype=odt, device=dev) for _ in range(self.nb)]
+        self.streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, args.branches))]
 
-    def batch(i):
-        b = i % nb
-        return (data.data_ptr() + b * step_bytes, None, outs[b])
+    def batch(self, i):
+        b = i % self.nb
+        return (self.data.data_ptr() + b * self.step_bytes, None, self.outs[b])
 
-    def launch_group(i0, i1, st):
-        eng.checksum_batches(ALG[alg], [batch(i) for i in range(i0, i1)], L, L, count, stream=st)
+    def launch_group(self, i0, i1, st):
+        self.eng.checksum_batches(ALG[self.alg], [self.batch(i) for i in range(i0, i1)], self.L, self.L, self.count,
+                                  stream=st)
 
-    def prepare(k, g_):
+    def prepare(self, k, g_):
         """the submissions of k steps in launches of <= g_ batches (descriptors built up front, as a
         producer fills a submission queue), alternating over the streams"""
         cuts = split(k, g_)
-        return [(eng.BatchSet(ALG[alg], [batch(i) for i in range(cuts[j], cuts[j + 1])], L, L, count),
-                 streams[j % len(streams)]) for j in range(len(cuts) - 1)]
+        return [(self.eng.BatchSet(ALG[self.alg], [self.batch(i) for i in range(cuts[j], cuts[j + 1])], self.L, self.L,
+                                   self.count), self.streams[j % len(self.streams)]) for j in range(len(cuts) - 1)]
 
-    def run_steps(k, g_):
-        for bs, st in prepare(k, g_):
-            bs.run(st)
+    def warm(self):
+        """every batch and every stream once (per-stream workspaces are allocated on first use), then
+        the requested warm-up steps the same way as the timed ones"""
+        if not self.args.only_coalesced:
+            for j in range(self.nb * len(self.streams)):
+                self.launch_group(j, j + 1, self.streams[j % len(self.streams)])
+        if self.args.warmup > 0:
+            for bs, st in self.prepare(self.args.warmup, self.G):
+                bs.run(st)
 
+    def parity_sample(self):
+        """the first 64 buffers of the first resident batch (written by the warm-up and the timed
+        region) against the engine's host path"""
+        nchk = min(self.count, 64)
+        hs = self.data[: nchk * self.L].cpu().numpy()
+        got = self.eng.as_unsigned(self.outs[0])[: nchk * self.per]
+        want = self.eng.cpu_batch(ALG[self.alg], [hs.ctypes.data + i * self.L for i in range(nchk)], [self.L] * nchk,
+                                  threads=8)
+        if self.alg == "xxh3_128":
+            got = [(got[2 * i] << 64) | got[2 * i + 1] for i in range(nchk)]
+        return nchk, got == want
+
+    def roofline(self):
+        """dominant kernel: launches of the timed region's shape, then (unless --only-coalesced) one-batch
+        launches, each stamped by its own dispatch"""
+        args = self.args
+        nt = max(1, args.timing_launches)
+        gsz = widest(max(args.steps, 1), self.G)  # batches per launch in the timed region
+        kms, kmed = time_launches(self.eng, lambda i, st: self.launch_group(i * gsz, i * gsz + gsz, st), self.streams[0], nt)
+        roof = roofline(gsz * self.step_bytes, kms, kernel_name(self.alg, self.count, self.L))
+        roof["kernel_ms_median"] = round(kmed, 5)
+        roof["timing_launches"] = nt
+        if not args.only_coalesced:
+            kms1, _ = time_launches(self.eng, lambda i, st: self.launch_group(i, i + 1, st), self.streams[0], nt)
+            roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(self.step_bytes, kms1, "")["frac"],
+                                    "bytes_per_launch": self.step_bytes}
+        roof["traffic"] = None
+        trf = pmc_traffic(self.alg, self.count, self.L, gsz)
+        if trf:
+            roof["traffic"], roof["traffic_source"] = trf
+        return roof, gsz
+
+    def device_record(self):
+        import torch
+
+        props = torch.cuda.get_device_properties(self.dev)
+        return {"device": torch.cuda.get_device_name(self.dev), "device_index": self.dev.index,
+                "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")) or None}
+
+
+def distinct_devices(recs):
+    """devices actually used by the ranks / fan-out entries (by UUID, else PCI bus, else index)"""
+    return len({r.get("uuid") or r.get("pci_bus_id") or r.get("device_index") for r in recs})
+
+
+def metric_name(alg):
+    return ("GiB/s CRC32C over device-resident buffers; % of HBM read peak" if alg == "crc32c"
+            else f"GiB/s {alg.upper()} over device-resident buffers; % of HBM read peak")
+
+
+def main_inproc(args):
+    """In-process multi-device mode (the engine's in-process fan-out: one HIP stream per GPU, no
+    collective).  Weak scaling, as the rank path: every device holds its own rotating batches and runs
+    the full --steps of them (each device's steps submitted as prepared launches on its own stream,
+    the devices' launches interleaved); the timed region ends when every device is done.  value = all
+    devices' bytes / that time.  Every device's kernel fraction and parity sample are reported."""
+    import torch
+    import aws_crt_amd as eng
+
+    n = args.gpus or 1
+    vis = torch.cuda.device_count()
+    if n > vis:
+        raise PlumbingError(f"--inproc --gpus {n} but {vis} GPU(s) visible")
+    rigs = []
+    for dv in range(n):
+        torch.cuda.set_device(dv)
+        eng.init()
+        rigs.append(Rig(eng, torch.device("cuda", dv), args, 0x5EED + dv))
+    for dv, rig in enumerate(rigs):
+        torch.cuda.set_device(dv)
+        rig.warm()
+    per_dev = [rig.prepare(args.steps, rig.G) if args.steps > 0 else [] for rig in rigs]
+    order = [(dv, per_dev[dv][j]) for j in range(max(len(p) for p in per_dev)) for dv in range(n) if j < len(per_dev[dv])]
+    for dv in range(n):
+        torch.cuda.synchronize(dv)
+    t0 = time.perf_counter()
+    for dv, (bs, st) in order:
+        torch.cuda.set_device(dv)
+        bs.run(st)
+    for dv in range(n):
+        torch.cuda.synchronize(dv)
+    el = time.perf_counter() - t0
+    step_bytes = rigs[0].step_bytes
+    value = n * args.steps * step_bytes / max(el, 1e-9) / 2**30
+    devs = []
+    for dv, rig in enumerate(rigs):
+        with torch.cuda.device(dv):
+            nchk, ok = rig.parity_sample()
+            roof, _ = rig.roofline()
+        devs.append(dict(rig.device_record(), kernel_ms=roof["kernel_ms"], frac=roof["frac"],
+                         roofline={k: roof[k] for k in ("achieved", "frac", "kernel_ms", "bytes_per_launch")},
+                         parity_sample_buffers=nchk, parity=ok))
+    used = distinct_devices(devs)
+    gsz = widest(max(args.steps, 1), rigs[0].G)
+    rec = {
+        "metric": metric_name(args.alg), "value": round(value, 2), "unit": "GiB/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (torch.randint bytes on device)",
+        "config": {"workload": f"{config_label(args.alg, args.buffers, args.buffer_bytes)}: {args.buffers} x "
+                               f"{args.buffer_bytes // 1024} KiB independent buffers per step, {args.alg.upper()}, "
+                               f"device-resident, {args.steps} steps per GPU",
+                   "launch": f"in-process fan-out: each device's steps in launches of up to {rigs[0].G} batches "
+                             f"({gsz} per launch) on its own HIP stream",
+                   "parallelism": f"one process, {n} device(s), no collective"},
+        "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / n / HBM_PEAK_GBS, 2),
+        "per_gpu_gibs": round(value / n, 2), "devices_used": used,
+        "parity": all(d["parity"] for d in devs), "devices": devs,
+        "roofline": dict(devs[0]["roofline"], bound="hbm", peak=HBM_PEAK_GBS, unit="GB/s",
+                         kernel=kernel_name(args.alg, args.buffers, args.buffer_bytes)),
+    }
+    print(json.dumps(rec), flush=True)
+    if used != n:
+        raise PlumbingError(f"--inproc --gpus {n} ran on {used} distinct device(s)")
+    if not rec["parity"]:
+        raise SystemExit(1)
+
+
+def main_rank(args):
+    import torch
+
+    ndev = torch.cuda.device_count() if args.plumbing_check is None else args.plumbing_check
+    world, rank, local, devidx, shared = rank_layout(args, os.environ, ndev)
+    if args.plumbing_check is not None:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local, "device_index": devidx, "shared": shared,
+                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
+              flush=True)
+        return
+    import torch.distributed as dist
+    import aws_crt_amd as eng
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(devidx)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", devidx))
+        else:
+            dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", devidx)
+    torch.cuda.set_device(dev)
+    eng.init()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    rig = Rig(eng, dev, args, 0x5EED + rank)
+    alg, count, L, G, nb, step_bytes = args.alg, rig.count, rig.L, rig.G, rig.nb, rig.step_bytes
+    data, outs, streams = rig.data, rig.outs, rig.streams
     torch.cuda.synchronize()
-    # every batch and every stream once (per-stream workspaces are allocated on first use), then the
-    # requested warm-up steps the same way as the timed ones
-    if not args.only_coalesced:
-        for j in range(nb * len(streams)):
-            launch_group(j, j + 1, streams[j % len(streams)])
-    if args.warmup > 0:
-        run_steps(args.warmup, G)
+    rig.warm()
     torch.cuda.synchronize()
 
     if world > 1:
         dist.barrier()
-    subs = prepare(args.steps, G) if args.steps > 0 else []
+    subs = rig.prepare(args.steps, G) if args.steps > 0 else []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for bs, st in subs:
@@ -662,21 +843,18 @@ def main():
     torch.cuda.synchronize()
     # each rank's clock stops when its own GPU is done; the closing barrier follows, and the slowest
     # rank's time (max over ranks) is the job's, so the barrier's own latency is not counted as work
-    elapsed = time.perf_counter() - t0
+    own = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
         torch.cuda.synchronize()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(own)
     value = world * args.steps * step_bytes / max(elapsed, 1e-9) / 2**30
 
     # the same K steps submitted one launch per batch (--coalesce 1), timed the same way: the rate a
     # caller that never queues batches together sees (reported beside `value`, never as it)
     one_per_launch = None
     if G > 1 and args.steps > 0:
-        subs1 = prepare(args.steps, 1)
+        subs1 = rig.prepare(args.steps, 1)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -684,11 +862,7 @@ def main():
         for bs, st in subs1:
             bs.run(st)
         torch.cuda.synchronize()
-        el1 = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el1], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el1 = float(t.item())
+        el1 = max_over_ranks(time.perf_counter() - t0)
         one_per_launch = {"value": round(world * args.steps * step_bytes / max(el1, 1e-9) / 2**30, 2), "unit": "GiB/s",
                           "ms_per_step": round(el1 / args.steps * 1e3, 4),
                           "launch": f"one launch per batch, {args.steps} launches over {len(streams)} streams"}
@@ -703,50 +877,25 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            b = batch(i)
+            b = rig.batch(i)
             q.push(b[0], b[2])
         q.flush()
         torch.cuda.synchronize()
-        elq = time.perf_counter() - t0
+        elq = max_over_ranks(time.perf_counter() - t0)
         q.close()
-        if world > 1:
-            t = torch.tensor([elq], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elq = float(t.item())
         queued = {"value": round(world * args.steps * step_bytes / max(elq, 1e-9) / 2**30, 2), "unit": "GiB/s",
                   "ms_per_step": round(elq / args.steps * 1e3, 4),
                   "launch": f"{args.steps} pushes of one batch into aws_crt_amd_queue (launch at 32 queued and at flush)"}
 
-    # every rank checks a sample of its own results against the engine's host path (the first 64
-    # buffers of the first resident batch, which the timed region and the warm-up both wrote)
+    # every rank checks a sample of its own results against the engine's host path
     torch.cuda.synchronize()
-    nchk = min(count, 64)
-    hs = data[: nchk * L].cpu().numpy()
-    got = eng.as_unsigned(outs[0])[: nchk * per]
-    want = eng.cpu_batch(ALG[alg], [hs.ctypes.data + i * L for i in range(nchk)], [L] * nchk, threads=8)
-    if alg == "xxh3_128":
-        got = [(got[2 * i] << 64) | got[2 * i + 1] for i in range(nchk)]
-    rank_parity = got == want
-
-    # dominant kernel: launches of G batches (the timed region's launch shape), then one-batch launches
-    nt = max(1, args.timing_launches)
-    gsz = widest(max(args.steps, 1), G)  # batches per launch in the timed region
-    kms, kmed = time_launches(eng, lambda i, st: launch_group(i * gsz, i * gsz + gsz, st), streams[0], nt)
-    roof = roofline(gsz * step_bytes, kms, kernel_name(alg, count, L))
-    roof["kernel_ms_median"] = round(kmed, 5)
-    roof["timing_launches"] = nt
-    if not args.only_coalesced:
-        kms1, _ = time_launches(eng, lambda i, st: launch_group(i, i + 1, st), streams[0], nt)
-        roof["single_batch"] = {"kernel_ms": round(kms1, 5), "frac": roofline(step_bytes, kms1, "")["frac"],
-                                "bytes_per_launch": step_bytes}
-    roof["traffic"] = None
-    trf = pmc_traffic(alg, count, L, gsz)
-    if trf:
-        roof["traffic"], roof["traffic_source"] = trf
+    nchk, rank_parity = rig.parity_sample()
+    roof, gsz = rig.roofline()
 
     # secondary denominator: the streaming-read ceiling of a one-batch launch and
     # of a launch of the timed region's size (the same bytes, read by an XOR-reduce kernel)
     if not args.no_read_ceiling and not args.only_coalesced:
+        nt = max(1, args.timing_launches)
         rc_ms, _ = time_launches(eng, lambda i, st, e0, e1: eng.read_ceiling(data, step_bytes, stream=st,
                                                                              base_offset=(i % nb) * step_bytes,
                                                                              start_event=e0, stop_event=e1),
@@ -758,20 +907,22 @@ def main():
                                   streams[0], max(2, nt // 4), stamps=True)
         roof["read_ceiling"] = {"kernel_ms": round(rcg_ms, 5), "frac": roofline(gsz * step_bytes, rcg_ms, "")["frac"],
                                 "timing_launches": max(2, nt // 4),
-                                "scan_frac_of_ceiling": round(rcg_ms / kms, 4),
+                                "scan_frac_of_ceiling": round(rcg_ms / roof["kernel_ms"], 4),
                                 "kernel": "read_ceiling_kernel: the scan's launch shape, 256-B non-temporal rows XOR-reduced"}
 
-    # per-rank record (device, kernel time, fraction, parity), gathered on rank 0
-    props = torch.cuda.get_device_properties(dev)
-    mine = {"rank": rank, "local_rank": local, "device": torch.cuda.get_device_name(dev), "device_index": dev.index,
-            "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")) or None,
-            "kernel_ms": roof["kernel_ms"], "frac": roof["frac"], "parity_sample_buffers": nchk, "parity": rank_parity}
+    # per-rank record (device, own rate, kernel time and fraction, parity), gathered on rank 0
+    mine = dict({"rank": rank, "local_rank": local}, **rig.device_record())
+    mine.update({"value": round(args.steps * step_bytes / max(own, 1e-9) / 2**30, 2), "unit": "GiB/s",
+                 "kernel_ms": roof["kernel_ms"], "frac": roof["frac"],
+                 "roofline": {k: roof[k] for k in ("achieved", "frac", "kernel_ms", "bytes_per_launch")},
+                 "parity_sample_buffers": nchk, "parity": rank_parity})
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
     else:
         ranks = [mine]
     parity_all = all(r["parity"] for r in ranks)
+    used = distinct_devices(ranks)
 
     cpu = e2e = None
     configs = {}
@@ -790,7 +941,7 @@ def main():
             e2e = e2e_legs.record()
             del e2e_legs
         if not args.no_configs:
-            del data
+            del data, rig
             torch.cuda.empty_cache()
             do_cpu = not args.no_cpu_baseline
             legs = {"do_cpu": do_cpu, "do_e2e": args.e2e_batches > 0}
@@ -808,8 +959,7 @@ def main():
 
     if rank == 0:
         rec = {
-            "metric": "GiB/s CRC32C over device-resident buffers; % of HBM read peak" if alg == "crc32c"
-            else f"GiB/s {alg.upper()} over device-resident buffers; % of HBM read peak",
+            "metric": metric_name(alg),
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -828,10 +978,15 @@ def main():
                        "launch": f"aws_crt_amd_checksum_batches, up to {G} queued batches per launch "
                                  f"({len(split(max(args.steps, 1), G)) - 1} launches for {args.steps} steps)",
                        "streams": len(streams),
-                       "parallelism": f"buffers sharded over {world} GPU(s), no collective"},
+                       "parallelism": f"buffers sharded over {world} rank(s) on {used} GPU(s), no collective"
+                                      + (" (gloo rehearsal: ranks share devices)" if shared else "")},
             "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
+            "per_gpu_gibs": round(value / world, 2),
+            "devices_used": used,
+            "shared_devices": shared,
             "parity": parity_all,
             "ranks": ranks,
+            "box": box_state(torch.cuda.get_device_properties(dev)),
             "one_batch_per_launch": one_per_launch,
             "queued_one_at_a_time": queued,
             "roofline": roof,
@@ -842,6 +997,23 @@ def main():
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    # RCCL ranks each need their own GPU (rank_layout refused a rank without one); a job whose ranks
+    # ran on fewer distinct devices than --gpus without asking for the gloo rehearsal is not an N-GPU
+    # measurement
+    if used != world and not shared:
+        raise PlumbingError(f"{world} ranks ran on {used} distinct GPU(s)")
+    if not parity_all:
+        raise SystemExit(1)
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.inproc:
+        return main_inproc(args)
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # no launcher: one fresh rank process per GPU, started before this process touches the GPU
+        raise SystemExit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
+    return main_rank(args)
 
 
 if __name__ == "__main__":

@@ -55,6 +55,7 @@ enum aws_crt_amd_status {
     AWS_CRT_AMD_ERR_INVALID_ARG = -2,
     AWS_CRT_AMD_ERR_HIP = -3,
     AWS_CRT_AMD_ERR_OOM = -4,
+    AWS_CRT_AMD_ERR_TICKET_EXPIRED = -5, /* queue_status: the ticket's record is gone (see below) */
 };
 
 /*
@@ -203,6 +204,10 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
  *   0                            complete: the batch's results are written
  *   < 0                          the launch that held it was refused (that status): its results are
  *                                never written -- every batch of a refused launch reports it
+ *   AWS_CRT_AMD_ERR_TICKET_EXPIRED  the queue no longer knows the ticket's outcome: it lies below the
+ *                                oldest of more than 1024 separate refused ranges, whose records were
+ *                                dropped (adjacent refused launches share one record).  Never
+ *                                reported for a ticket whose outcome is still recorded.
  * queue_wait(ticket) launches the ticket's batch if it is still queued and waits for it; it returns 0
  * or the error.  queue_first_pending: the ticket of the oldest queued batch (every lower ticket has
  * been launched or refused).  Status and wait may be called from any thread.

@@ -5,4 +5,4 @@ set -e
 cd "$(dirname "$0")/../aws-crt-cpp_amd"
 n=$1; shift
 rm -rf build_$n  # make does not track flags: a variant dir left from other flags would be reused
-make -s -j8 BUILD=build_$n LIB=../ab/lib$n.so HIPFLAGS_EXTRA="$*" ../ab/lib$n.so
+make -s -j8 BUILD=build_$n LIB=../ab/lib$n.so HIPFLAGS_EXTRA="-DAMDCRC_VARIANT_BUILD=1 $*" ../ab/lib$n.so

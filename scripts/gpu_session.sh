@@ -56,6 +56,10 @@ for s in "$@"; do
     ingest) step 300 $O/ingest.log env AWS_CRT_AMD_INGEST_TRACE=${INGEST_TRACE:-0} python -u aws-crt-cpp_amd/tools/ingest_probe.py; rc=$?; grep '^{' $O/ingest.log | tail -1 | cut -c1-300 ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;
+    # the value-only ABI's small-call latency (C++), pointer cache on and off
+    lat)   step 120 $O/lat.log bash -c "experiments/build/abi_latency 200000 && AWS_CRT_AMD_PTR_CACHE=0 experiments/build/abi_latency 200000"; rc=$?; cat $O/lat.log ;;
+    # the multi-GPU rank path rehearsed on the box's one GPU (two gloo ranks) and the in-process fan-out
+    ranks) step 300 $O/ranks.log bash -c "python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-configs --e2e-batches 0 --no-cpu-baseline && python -u bench.py --inproc --gpus 1 --steps 20 --warmup 5"; rc=$?; grep '^{' $O/ranks.log | cut -c1-600 ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }

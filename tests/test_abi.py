@@ -6,6 +6,8 @@ import re
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
 C_HEADERS = ["include/aws_crt_amd/checksums_batch.h", "include/aws/checksums/crc.h", "include/aws/checksums/xxhash.h",
@@ -136,3 +138,65 @@ def test_value_abi_never_aborts_without_device():
                            env=dict(os.environ, AWS_CRT_AMD_DISPATCH=mode, HIP_VISIBLE_DEVICES="-1"))
         assert r.returncode == 0, r.stderr
         assert int(r.stdout.split()[-1]) == oracle.crc("crc32c", b"123456789") == 0xE3069283
+
+
+def test_pointer_classifier_model():
+    """csrc/ptr_class.h with a stand-in probe (tests/cpp/ptr_class_test.cpp, ASan): the common small host
+    call never reaches the HIP runtime; device and runtime-known host memory always do; per thread;
+    AWS_CRT_AMD_PTR_CACHE=0 probes every call"""
+    cpp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp")
+    subprocess.run(["make", "-s", "-C", cpp, "build/ptr_class"], check=True, capture_output=True, text=True)
+    exe = os.path.join(cpp, "build", "ptr_class")
+    for env, args in (({}, []), ({"AWS_CRT_AMD_PTR_CACHE": "0"}, ["off"])):
+        r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120, env=dict(os.environ, **env))
+        assert r.returncode == 0 and "[PASS] PtrClass" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_value_abi_small_host_calls_skip_the_runtime_probe(engine):
+    """AUTO-mode aws_checksums_crc32c_ex on small host buffers classifies the
+    pointer without hipPointerGetAttributes after the first call in a 64 KiB window; a device
+    pointer is still detected and served by the kernels (the diagnostic build counts the probes)"""
+    import ctypes
+
+    import torch
+
+    from oracle import oracle
+
+    D = engine.diag_lib()
+    D.aws_crt_amd_debug_pointer_probes.restype = ctypes.c_ulonglong
+    f = D.aws_checksums_crc32c_ex
+    f.restype, f.argtypes = ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32]
+    assert D.aws_crt_amd_init() == 0 and D.aws_crt_amd_set_dispatch(0) == 0
+    buf = ctypes.create_string_buffer(bytes(range(256)) * 16, 4096)
+    base = ctypes.addressof(buf)
+    p0 = D.aws_crt_amd_debug_pointer_probes()
+    vals = {}
+    for i in range(1000):
+        n = (8, 12, 32, 4096)[i % 4]
+        vals[n] = f(base + (i % 64), n, 0) if i % 64 == 0 else f(base, n, 0)
+    vals = {n: f(base, n, 0) for n in (8, 12, 32, 4096)}
+    probes = D.aws_crt_amd_debug_pointer_probes() - p0
+    assert probes <= 2, probes
+    raw = (bytes(range(256)) * 16)
+    assert vals == {n: oracle.crc("crc32c", raw[:n]) for n in (8, 12, 32, 4096)}
+    d = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    p1 = D.aws_crt_amd_debug_pointer_probes()
+    assert f(d.data_ptr(), 4096, 0) == oracle.crc("crc32c", raw)
+    assert D.aws_crt_amd_debug_pointer_probes() - p1 == 1  # device memory is always asked about
+
+
+def test_release_build_rejects_ab_knobs():
+    """an AMDCRC_* A/B knob outside a variant build is a compile error
+    (csrc/variant_guard.h); the results-breaking timing switches are not in the source at all"""
+    pkg = os.path.join(REPO, "aws-crt-cpp_amd")
+    base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__",
+            "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(pkg, "csrc"), os.path.join(pkg, "csrc", "engine.cpp")]
+    r = subprocess.run(base + ["-DAMDCRC_XCD=0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "not a variant build" in r.stderr
+    r = subprocess.run(base + ["-DAMDCRC_XCD=0", "-DAMDCRC_VARIANT_BUILD=1"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    src = open(os.path.join(pkg, "csrc", "crc_kernels.hip")).read() + open(os.path.join(pkg, "csrc", "engine.cpp")).read()
+    for gone in ("AMDCRC_XP_LIST_NOHEAD", "AMDCRC_XP_LIST_NOFINISH", "AMDCRC_XP_XCD_NOPUB", "AMDCRC_XP"):
+        assert gone not in src, gone

@@ -39,3 +39,51 @@ def test_bench_json_line():
     # every rank checked a sample of its results against the host path (BASELINE multi-GPU runs)
     assert d["parity"] is True and len(d["ranks"]) == 1 and d["ranks"][0]["parity"] is True
     assert d["one_batch_per_launch"]["value"] > 0
+    assert d["devices_used"] == 1 and d["per_gpu_gibs"] == d["value"]
+    r0 = d["ranks"][0]
+    assert r0["value"] > 0 and r0["roofline"]["frac"] == roof["frac"] and "uuid" in r0 and "pci_bus_id" in r0
+    assert "box" in d and "sclk" in d["box"]
+
+
+def _bench(args, timeout=300):
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2", "--no-configs",
+           "--e2e-batches", "0", "--timing-launches", "4", "--no-cpu-baseline", "--no-read-ceiling"] + args
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_rehearsal():
+    """--gpus 2 without a launcher: two rank processes (here sharing the box's one GPU over gloo, the
+    rehearsal of the 8-GPU rank path); rank 0 prints one line with both ranks' records"""
+    r, lines = _bench(["--gpus", "2", "--dist-backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["shared_devices"] is True
+    assert [x["rank"] for x in d["ranks"]] == [0, 1]
+    assert all(x["parity"] is True and x["value"] > 0 and 0 < x["frac"] <= 1 for x in d["ranks"])
+    assert d["parity"] is True and d["cpu_baseline"] is None
+    assert abs(d["per_gpu_gibs"] * 2 - d["value"]) < 0.05
+
+
+@pytest.mark.gpu
+def test_bench_rccl_refuses_more_ranks_than_gpus():
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    r, lines = _bench(["--gpus", str(n)], timeout=180)
+    assert r.returncode == 2 and "no GPU of its own" in r.stderr and not lines
+
+
+@pytest.mark.gpu
+def test_bench_inproc_per_device_records():
+    """--inproc: every device runs the full --steps (weak scaling) with its own roofline and parity"""
+    r, lines = _bench(["--inproc", "--gpus", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["devices_used"] == 1
+    assert len(d["devices"]) == 1 and d["devices"][0]["parity"] is True and 0 < d["devices"][0]["frac"] <= 1
+    assert d["roofline"]["bound"] == "hbm" and d["value"] > 0

@@ -193,3 +193,15 @@ def test_numa_placed_host_path(tmp_path):
     traces = [json.loads(l) for l in r.stderr.splitlines() if l.startswith('{"ingest_trace"')]
     crc = [t for t in traces if t["host_threads"] > 0]
     assert len(crc) == 3 and all(t["numa_node"] == 0 for t in crc), traces
+
+
+def test_runner_runs_concurrent_jobs_concurrently():
+    """the coordinator threads (csrc/runner.h) give every queued job a thread of its own,
+    so two jobs submitted together overlap (tests/cpp/runner_test.cpp under TSan)"""
+    import os
+    import subprocess
+
+    cpp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp")
+    subprocess.run(["make", "-s", "-C", cpp, "build/runner_tsan"], check=True, capture_output=True, text=True)
+    r = subprocess.run([os.path.join(cpp, "build", "runner_tsan")], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "[PASS] RunnerConcurrent" in r.stdout, r.stdout + r.stderr

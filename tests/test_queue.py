@@ -207,3 +207,30 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
     assert qr.wait(tr[1]) == -2
     qr.close()
     del big
+
+
+def test_queue_refused_tickets_never_report_complete():
+    """beyond 1024 pruned refused launches the oldest records used to be dropped and their
+    tickets then read 0 (complete, results written).  Adjacent refused launches now share a record, so
+    3,000 refused one-batch launches all still report the refusal; a ticket whose record is gone would
+    report AWS_CRT_AMD_ERR_TICKET_EXPIRED (-5), never 0."""
+    code = (
+        "import ctypes\n"
+        f"L=ctypes.CDLL({LIB!r})\n"
+        "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
+        "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
+        "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
+        "L.aws_crt_amd_queue_status.argtypes=[vp,u64]\n"
+        "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
+        "q=vp(); t=u64()\n"
+        "assert L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(1,0)),ctypes.byref(q))==0\n"
+        "rc=[L.aws_crt_amd_queue_push_ex(q,4096,None,8192,ctypes.byref(t)) for i in range(3000)]\n"
+        "st=[L.aws_crt_amd_queue_status(q,k) for k in range(1,3001)]\n"
+        "print('pushes', set(rc), 'status', sorted(set(st)), 'last', t.value)\n"
+        "print('destroy', L.aws_crt_amd_queue_destroy(q))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+    assert r.returncode == 0, r.stderr
+    assert "pushes {-1} status [-1] last 3000" in r.stdout, r.stdout
+    assert "destroy 0" in r.stdout
