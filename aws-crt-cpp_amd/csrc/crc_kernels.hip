@@ -45,6 +45,28 @@ typedef __attribute__((address_space(1))) const v4u gv4u;
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 typedef __attribute__((address_space(1))) const uint64_t gu64;
 
+// floor(n / d) for wave-uniform n and d >= 1.  The compiler's 64-bit integer division is ~150 scalar
+// instructions (issued at most one per 4 cycles per SIMD); the W=32 streaming scan's prologue had nine
+// of them and took 3.2-6.5 us from entry to its first barrier (per-wave stamps, profiles/r05/stamps).
+// Here: the correctly rounded double quotient, which for n < 2^52 is floor(n / d) or one more (an
+// exact quotient k is representable and stays k; a larger one cannot round below its floor), and one
+// correction.  About a dozen vector instructions on uniform values.
+__device__ __forceinline__ uint64_t udiv_u(uint64_t n, uint64_t d) {
+    if (d == 1) return n;
+    if ((n | d) >> 52) {  // never on a real launch (2^52 tiles); compact shift-subtract, not 150 inlined ops
+        uint64_t q = 0, r = 0;
+#pragma unroll 1
+        for (int i = 63; i >= 0; --i) {
+            r = (r << 1) | ((n >> i) & 1u);
+            if (r >= d) r -= d, q |= 1ull << i;
+        }
+        return q;
+    }
+    uint64_t q = (uint64_t)((double)n / (double)d);
+    if (q * d > n) --q;
+    return q;
+}
+
 __device__ __forceinline__ uint32_t lds32(const char *L, uint32_t a) { return *(const uint32_t *)(L + a); }
 __device__ __forceinline__ uint64_t lds64(const char *L, uint32_t a) { return *(const uint64_t *)(L + a); }
 
@@ -130,7 +152,7 @@ struct BatchPos {
 };
 __device__ __forceinline__ BatchPos batch_pos(const ScanParams &p, uint64_t b) {
     if (p.nbatch <= 1) return {0, b};
-    const uint64_t j = b / p.bcount;
+    const uint64_t j = udiv_u(b, p.bcount);
     return {j, b - j * p.bcount};
 }
 // the kernel-argument arrays, indexed with a wave-uniform j (ordinary reads of the kernarg segment:
@@ -168,7 +190,7 @@ __device__ __forceinline__ Tile make_tile(const ScanParams &p, uint64_t t, Walke
     Tile d;
     if (!LIST) {
         d.T = p.tiles_per_buf;
-        d.b = t / d.T;
+        d.b = udiv_u(t, d.T);
         d.k = t - d.b * d.T;
         d.tbase = t - d.k;
     } else {
@@ -861,15 +883,15 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     const bool dyn = !LIST && p.nstatic != 0;
     uint64_t t0, t1, pool_base = 0, pool_size = 0;
     if (dyn) {
-        const uint64_t wb0 = (uint64_t)blockIdx.x * p.ntiles / gridDim.x, wb1 = ((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x;
+        const uint64_t wb0 = udiv_u((uint64_t)blockIdx.x * p.ntiles, gridDim.x), wb1 = udiv_u(((uint64_t)blockIdx.x + 1) * p.ntiles, gridDim.x);
         const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
         t0 = wb0 + wv < wb1 ? wb0 + wv : wb1;
         t1 = wb0 + wv < wb1 ? t0 + 1 : wb1;
         pool_base = wb0 + kBraidWaves;
         pool_size = pool_base < wb1 ? wb1 - pool_base : 0;
     } else {
-        t0 = gw * p.ntiles / nw;
-        t1 = (gw + 1) * p.ntiles / nw;
+        t0 = udiv_u(gw * p.ntiles, nw);
+        t1 = udiv_u((gw + 1) * p.ntiles, nw);
     }
     t0 = rfl64(t0), t1 = rfl64(t1);
     // tiles entered by the prefetch cursor from the pool, in order, for the scan cursor
@@ -1383,6 +1405,21 @@ __device__ __forceinline__ void stream_finish_xcd(const ScanParams &p, const Til
     }
 }
 
+#if AWS_CRT_AMD_DIAG
+// Diagnostic library only: per-wave timeline of crc32_stream_kernel (aws_crt_amd_debug_scan_stamps),
+// kStampWords words per wave at (blockIdx * waves + wave): entry, tables built (after the barrier),
+// first group scanned, loop end, exit (s_memrealtime, 100 MHz), hardware id (HW_ID | XCC_ID << 32),
+// groups scanned, tile finishes.  Null: no stamps.  Stamps are taken outside the scan loop only.
+__device__ uint64_t *g_scan_stamps;
+constexpr int kStampWords = 8;
+__device__ __forceinline__ uint64_t stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t stamp_hwid() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    return (uint64_t)hw | ((uint64_t)(xcc & 0xF) << 32);
+}
+#endif
+
 // Tiles: an even static split over the waves (a workgroup-local pool was tried: see DESIGN.md).
 // WB = bytes per lane word: 8 (512-thread workgroups, 64 KiB of tables, two per CU) or 16 (one
 // 1024-thread workgroup per CU, 128 KiB of tables); 4 remains as the AMDCRC_STREAM_W8=0 build.
@@ -1404,13 +1441,18 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     constexpr int WAVES = SS::kWaves;
     __shared__ __attribute__((aligned(16))) char lds[SS::kLds];
     char *const cb = lds + SS::kTab;  // constants region (K image, P columns, byte table, flag, local slots)
+#if AWS_CRT_AMD_DIAG
+    uint64_t *const stamps = g_scan_stamps;
+    const uint64_t t_entry = stamp_now();
+    uint64_t t_tab = 0, t_first = 0, t_loop = 0;
+#endif
 
     const int lane = threadIdx.x & 63;
     const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * WAVES;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + wv);
-    const uint64_t wt0 = rfl64((uint64_t)blockIdx.x * p.ntiles / gridDim.x);
-    const uint64_t wt1 = rfl64(((uint64_t)blockIdx.x + 1) * p.ntiles / gridDim.x);
+    const uint64_t wt0 = rfl64(udiv_u((uint64_t)blockIdx.x * p.ntiles, gridDim.x));
+    const uint64_t wt1 = rfl64(udiv_u(((uint64_t)blockIdx.x + 1) * p.ntiles, gridDim.x));
     // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
     const uint32_t G = p.seg / kGroupBytes;
     const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
@@ -1428,10 +1470,10 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * p.ntiles / 8, xhi = (xcd + 1) * p.ntiles / 8;
         t0 = rfl64(xlo + (uint64_t)(blockIdx.x >> 3) * WAVES + wv);
         tstep = nwx;
-        ntw = rfl64(t0 < xhi ? (xhi - t0 + nwx - 1) / nwx : 0);
+        ntw = rfl64(t0 < xhi ? udiv_u(xhi - t0 + nwx - 1, nwx) : 0);
     } else {
-        t0 = rfl64(gw * p.ntiles / nw);
-        ntw = rfl64((gw + 1) * p.ntiles / nw) - t0;
+        t0 = rfl64(udiv_u(gw * p.ntiles, nw));
+        ntw = rfl64(udiv_u((gw + 1) * p.ntiles, nw)) - t0;
     }
     const uint32_t gsh = __builtin_ctz(G);
     const uint32_t nq = (uint32_t)(ntw << gsh);  // groups of this wave
@@ -1439,7 +1481,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // prefetch cursor: the next group to issue, as (buffer, tile, group); fbuf is the main-region
     // address of buffer fb, which walks batch by batch (fj, fi)
     uint32_t fq = 0;  // groups issued
-    uint64_t fb = t0 / T, fk = t0 - fb * T;
+    uint64_t fb = udiv_u(t0, T), fk = t0 - fb * T;
     uint32_t fg = 0;
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
@@ -1459,7 +1501,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
             if constexpr (xo) {  // the wave's next tile is tstep tiles on
                 ft += tstep;
                 if (fq < nq) {
-                    fb = ft / T, fk = ft - fb * T;
+                    fb = udiv_u(ft, T), fk = ft - fb * T;
                     fpos = batch_pos(p, fb);
                     fbuf = karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff;
                 }
@@ -1486,7 +1528,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
     LocalBufs lb{0, 0};
     if (T > 1 && T <= 32) {
-        const uint64_t b0 = (wt0 + T - 1) / T, b1 = wt1 / T;
+        const uint64_t b0 = udiv_u(wt0 + T - 1, T), b1 = udiv_u(wt1, T);
         if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
     }
     Grp ra, rb, rc;
@@ -1538,6 +1580,9 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
     if (threadIdx.x < kLocalSlots) ((unsigned long long *)(cb + (kLocalOff - kBKOff)))[threadIdx.x] = 0ull;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if AWS_CRT_AMD_DIAG
+    t_tab = stamp_now();
+#endif
     B eng;
     eng.init(lds, lane);
     if (work) {
@@ -1561,15 +1606,27 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
             __builtin_amdgcn_s_sleep(1);
         consts_ready = true;
     };
+#if AWS_CRT_AMD_DIAG
+    auto put_stamps = [&](uint64_t groups) {
+        if (stamps && lane == 0) {
+            uint64_t *w = stamps + kStampWords * ((uint64_t)blockIdx.x * WAVES + wv);
+            w[0] = t_entry, w[1] = t_tab, w[2] = t_first, w[3] = t_loop, w[4] = stamp_now(), w[5] = stamp_hwid();
+            w[6] = groups, w[7] = groups >> gsh;
+        }
+    };
+#endif
     if (!work) {
         publish_consts();
+#if AWS_CRT_AMD_DIAG
+        put_stamps(0);
+#endif
         return;
     }
 
     // scan cursor: tile d (buffer, index in buffer), group g, global group q
     Tile d;
     d.T = T;
-    d.b = t0 / T;
+    d.b = udiv_u(t0, T);
     d.k = t0 - d.b * T;
     d.tbase = d.b * T;
     d.vbase = 0;
@@ -1594,7 +1651,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
                 stream_finish_xcd(p, d, u, eng, lane, (uint32_t)(st_n * (WAVES / T) + wv / T));
                 ++st_n;
                 st_t += tstep;
-                d.b = st_t / T, d.k = st_t - d.b * T, d.tbase = d.b * T;
+                d.b = udiv_u(st_t, T), d.k = st_t - d.b * T, d.tbase = d.b * T;
             } else {
                 stream_finish(p, d, u, eng, lane, acc, lb);
                 if (++d.k == T) d.k = 0, ++d.b, d.tbase += T;
@@ -1609,6 +1666,9 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // loads in flight, and drained most of the ring at the top of every rotation (vmcnt 7..2 before the
     // first step's row loads); without the breaks every row waits exactly vmcnt(16).
     step(ra, rc, true);
+#if AWS_CRT_AMD_DIAG
+    t_first = stamp_now();
+#endif
     while (q + 3 <= nq) {
         step(rb, ra, false);
         step(rc, rb, false);
@@ -1618,8 +1678,14 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         step(rb, ra, false);
         if (q < nq) step(rc, rb, false);
     }
+#if AWS_CRT_AMD_DIAG
+    t_loop = stamp_now();
+#endif
     ring_drain(ra, rb, rc);  // the trailing placeholder rows
     stream_publish(p, acc, eng, lane);
+#if AWS_CRT_AMD_DIAG
+    put_stamps(nq);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2280,7 +2346,7 @@ __global__ __launch_bounds__(kBlock, 1) void crc64_braid_kernel(const ScanParams
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint64_t t0 = gw * p.ntiles / nw, t1 = (gw + 1) * p.ntiles / nw;
+    const uint64_t t0 = udiv_u(gw * p.ntiles, nw), t1 = udiv_u((gw + 1) * p.ntiles, nw);
 
     Walker w0{0, 0, 0};
     if (LIST && t0 < t1) {
@@ -2468,7 +2534,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6));
-    const uint64_t t0 = rfl64(gw * p.ntiles / nw), t1 = rfl64((gw + 1) * p.ntiles / nw);
+    const uint64_t t0 = rfl64(udiv_u(gw * p.ntiles, nw)), t1 = rfl64(udiv_u((gw + 1) * p.ntiles, nw));
     // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
     const uint32_t G = p.seg / kGroupBytes;
     const uint32_t gsh = __builtin_ctz(G);
@@ -2479,7 +2545,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     const uint32_t nq = (uint32_t)((t1 - t0) << gsh);  // groups of this wave
     const bool work = t0 < t1;
     uint32_t fq = 0;  // groups issued
-    uint64_t fb = t0 / T, fk = t0 - fb * T;
+    uint64_t fb = udiv_u(t0, T), fk = t0 - fb * T;
     uint32_t fg = 0;
     BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
     uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
@@ -2519,7 +2585,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
 
     Tile d;
     d.T = T;
-    d.b = t0 / T;
+    d.b = udiv_u(t0, T);
     d.k = t0 - d.b * T;
     d.tbase = d.b * T;
     d.vbase = 0;
@@ -2645,16 +2711,16 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint64_t NC = p.ntiles, CPB = p.tiles_per_buf;
     const uint64_t xlo = xcd * NC / 8, xhi = (xcd + 1) * NC / 8;
     const uint64_t c0 = xlo + j;
-    const uint32_t nchunks = c0 < xhi ? (uint32_t)((xhi - c0 + nwx - 1) / nwx) : 0u;
+    const uint32_t nchunks = c0 < xhi ? (uint32_t)udiv_u(xhi - c0 + nwx - 1, nwx) : 0u;
     const uint32_t nq = nchunks * kXcdChunkGroups;  // groups of this wave
     const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
     const uint32_t voff = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);  // 16 KiB constant block (placeholder rows)
-    const uint64_t dq = nwx / CPB, dr = nwx - dq * CPB;   // chunk step as (buffers, chunks)
+    const uint64_t dq = udiv_u(nwx, CPB), dr = nwx - dq * CPB;   // chunk step as (buffers, chunks)
     // every buffer's main region is front-padded with virtual zeros to CPB whole chunks (pad < chunk)
     const uint32_t pad = p.xcd_pad;
     auto cur_at = [&](uint64_t c) -> XcdCursor {
-        const uint64_t b = c / CPB;
+        const uint64_t b = udiv_u(c, CPB);
         const BatchPos bp = batch_pos(p, b);
         return XcdCursor{b, c - b * CPB, karg64(p.bbase, bp.j) + bp.i * p.stride + hoff - pad};
     };
@@ -3114,11 +3180,11 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
     if ((gridDim.x & 7u) == 0) {
         const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * nsets / 8, xhi = (xcd + 1) * nsets / 8;
         const uint64_t j = rfl64((uint64_t)(blockIdx.x >> 3) * kWaves + (threadIdx.x >> 6));
-        s0 = xlo + j, sstep = nwx, nsw = s0 < xhi ? (xhi - s0 + nwx - 1) / nwx : 0;
+        s0 = xlo + j, sstep = nwx, nsw = s0 < xhi ? udiv_u(xhi - s0 + nwx - 1, nwx) : 0;
     } else
 #endif
     {
-        s0 = rfl64(gw * nsets / nw), sstep = 1, nsw = rfl64((gw + 1) * nsets / nw) - s0;
+        s0 = rfl64(udiv_u(gw * nsets, nw)), sstep = 1, nsw = rfl64(udiv_u((gw + 1) * nsets, nw)) - s0;
     }
     const Edges e0 = buffer_edges<false>(p, 0);
     const uint64_t hoff = e0.headend - p.base, ml = e0.tail - e0.headend;
@@ -3680,7 +3746,7 @@ __global__ __launch_bounds__(256) void crc_lanes_kernel(const LaneParams p) {
         // the batch index differs between lanes: read the descriptors through the kernarg segment
         // (an indexed read of the by-value parameter would copy the whole block to scratch)
         const LaneParams *kp = (const LaneParams *)__builtin_amdgcn_kernarg_segment_ptr();
-        const uint64_t j = b / p.bcount;
+        const uint64_t j = udiv_u(b, p.bcount);
         ix = b - j * p.bcount;
         ptr = (const uint8_t *)(kp->bbase[j] + ix * p.stride);
         n = p.len;
@@ -3749,7 +3815,7 @@ __global__ __launch_bounds__(kBraidBlock) void read_ceiling_kernel(const uint8_t
     constexpr int D = kBraidRowsPerGroup;
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * kBraidWaves, gw = (uint64_t)blockIdx.x * kBraidWaves + (threadIdx.x >> 6);
-    const uint64_t rows = bytes / kBraidRow, r0 = gw * rows / nw, r1 = (gw + 1) * rows / nw;
+    const uint64_t rows = bytes / kBraidRow, r0 = udiv_u(gw * rows, nw), r1 = udiv_u((gw + 1) * rows, nw);
     const uint64_t a0 = (uint64_t)base + r0 * kBraidRow + 4u * lane;
     const uint64_t ng = (r1 - r0) / D;
     uint32_t s0[D], s1[D], acc = 0;
@@ -3790,6 +3856,12 @@ extern "C" int amdcrc_launch_read_ceiling(const void *base, uint64_t bytes, uint
 }
 
 #if AWS_CRT_AMD_DIAG
+// Diagnostic library only: crc32_stream_kernel writes its per-wave timeline to d_buf (kStampWords words
+// per wave; null turns the stamps off).  Returns 0 on success.
+extern "C" __attribute__((visibility("default"))) int aws_crt_amd_debug_scan_stamps(void *d_buf) {
+    uint64_t *p = (uint64_t *)d_buf;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_scan_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
 // Debug builds (-DAMDCRC_GUARD): read and clear the streaming scan's guard record
 extern "C" __attribute__((visibility("default"))) int amdcrc_debug_guard(unsigned long long *out4) {
 #ifdef AMDCRC_GUARD
