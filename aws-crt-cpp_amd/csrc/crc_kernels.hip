@@ -152,7 +152,7 @@ struct BatchPos {
 };
 __device__ __forceinline__ BatchPos batch_pos(const ScanParams &p, uint64_t b) {
     if (p.nbatch <= 1) return {0, b};
-    const uint64_t j = udiv_u(b, p.bcount);
+    const uint64_t j = p.bshift1 ? b >> (p.bshift1 - 1) : udiv_u(b, p.bcount);
     return {j, b - j * p.bcount};
 }
 // the kernel-argument arrays, indexed with a wave-uniform j (ordinary reads of the kernarg segment:
@@ -500,6 +500,46 @@ __device__ __forceinline__ uint32_t basis_w8(uint32_t e) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) v ^= ((e >> i) & 1u) ? B.b[K][i] : 0u;
     return v;
+}
+// bt[i] = T'_t[1 << i] for a per-lane t < 8: one AND-OR per candidate through opaque masks (a select
+// chain over constants would become a per-lane load from a constant table, waited for behind the
+// payload loads already in flight)
+template <uint32_t POLY>
+__device__ __forceinline__ void basis_w8_lane(uint32_t t, uint32_t (&bt)[8]) {
+    constexpr BraidW8Basis<POLY> B{};
+    uint32_t m[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        m[k] = t == (uint32_t)k ? ~0u : 0u;
+        asm("" : "+v"(m[k]));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v |= B.b[k][i] & m[k];
+        bt[i] = v;
+    }
+}
+// The eight slice-by-8 tables in 8 copies (64 KiB: one 256-byte row per entry e, table t at 32 t,
+// copies 0-3 then 4-7) from a 512-thread workgroup, as 4096 chunks of 16 bytes: chunk k = tid + 512 m
+// holds copies 4 (k & 1) .. + 3 of T'_t[e], t = (k & 15) >> 1, e = k >> 4 = (tid >> 4) + 32 m.
+// Consecutive lanes store consecutive chunks, so every ds_write_b128 is conflict-free.  Round 4 built
+// table t in wave t: the 64 lanes of each store met one 32-byte bank group, and the per-wave stamps
+// put ~4 us between a wave's entry and its barrier (tools/stamp_probe.py).
+template <uint32_t POLY>
+__device__ __forceinline__ void build_w8_tables(char *lds, uint32_t tid) {
+    uint32_t bt[8];
+    basis_w8_lane<POLY>((tid & 15u) >> 1, bt);
+    const uint32_t e0 = tid >> 4;  // bits 0-4 of e; bits 5-7 are m
+    uint32_t t0v = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) t0v ^= ((e0 >> i) & 1u) ? bt[i] : 0u;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const uint32_t te = t0v ^ (m & 1 ? bt[5] : 0u) ^ (m & 2 ? bt[6] : 0u) ^ (m & 4 ? bt[7] : 0u);
+        *(uint4 *)(lds + 16u * (tid + 512u * m)) = make_uint4(te, te, te, te);
+    }
 }
 template <uint32_t POLY>
 __device__ __forceinline__ uint32_t basis_w8_rt(uint32_t t, uint32_t e) {  // t wave-uniform
@@ -970,15 +1010,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_braid_kernel(const ScanP
     if (any && !dyn) pf_advance();  // pool mode: after the barrier, where the pool counter is set up
     if constexpr (W8) {
         // the eight slice-by-8 tables, 8 copies (as crc32_stream_kernel<POLY, true>)
-        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint32_t e = (uint32_t)lane + 64u * n;
-            const uint32_t te = basis_w8_rt<POLY>(t, e);
-            char *row = lds + (e << 8) + (t << 5);
-            *(uint4 *)row = make_uint4(te, te, te, te);
-            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
-        }
+        static_assert(kBraidBlock == 512, "build_w8_tables: 512 threads");
+        build_w8_tables<POLY>(lds, threadIdx.x);
         if (threadIdx.x < 256) *(uint32_t *)(lds + kT0Off + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
         if (threadIdx.x == 0) *(uint32_t *)(lds + kConstFlagOff) = 0u;
         if (threadIdx.x == 0) *(uint32_t *)(lds + kPoolOff) = 0u;
@@ -1411,7 +1444,7 @@ __device__ __forceinline__ void stream_finish_xcd(const ScanParams &p, const Til
 // first group scanned, loop end, exit (s_memrealtime, 100 MHz), hardware id (HW_ID | XCC_ID << 32),
 // groups scanned, tile finishes.  Null: no stamps.  Stamps are taken outside the scan loop only.
 __device__ uint64_t *g_scan_stamps;
-constexpr int kStampWords = 8;
+constexpr int kStampWords = 16;  // [8..11]: kernel arguments in, first group issued, second group issued, tables stored
 __device__ __forceinline__ uint64_t stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ uint64_t stamp_hwid() {
     const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
@@ -1444,21 +1477,37 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
 #if AWS_CRT_AMD_DIAG
     uint64_t *const stamps = g_scan_stamps;
     const uint64_t t_entry = stamp_now();
-    uint64_t t_tab = 0, t_first = 0, t_loop = 0;
+    uint64_t t_tab = 0, t_first = 0, t_loop = 0, t_karg = 0, t_ra = 0, t_rb = 0, t_built = 0;
 #endif
 
     const int lane = threadIdx.x & 63;
+    // Prologue (round 5): the kernel arguments that the first group's address needs come in as one
+    // batch of scalar loads with one wait.  The compiler had spread them over five dependent round
+    // trips between branches, and the per-wave stamps put ~4 us between a wave's entry and its
+    // barrier in a 16 us one-batch launch (tools/stamp_probe.py).  The wave's first two groups are
+    // then issued before the tables are built, so HBM streams through the table build.
+    const uint64_t a_ntiles = p.ntiles, a_T = p.tiles_per_buf, a_base = p.base, a_stride = p.stride, a_len = p.len,
+                   a_bcount = p.bcount, a_kv = (uint64_t)p.d_kvals, a_pc = (uint64_t)p.d_pcols, a_bb0 = p.bbase[0];
+    const uint32_t a_seg = p.seg, a_nbatch = p.nbatch, a_grid = gridDim.x, a_r = p.split_r;
+    const uint64_t a_q = p.split_q;
+    const uint32_t a_sh = (uint32_t)p.tshift1 | ((uint32_t)p.bshift1 << 8);
+    asm volatile("" ::"s"(a_ntiles), "s"(a_T), "s"(a_base), "s"(a_stride), "s"(a_len), "s"(a_bcount), "s"(a_kv), "s"(a_pc),
+                 "s"(a_bb0), "s"(a_seg), "s"(a_nbatch), "s"(a_grid), "s"(a_r), "s"(a_q), "s"(a_sh));
+    const uint32_t a_tsh1 = a_sh & 0xFFu, a_bsh1 = a_sh >> 8;
+#if AWS_CRT_AMD_DIAG
+    t_karg = stamp_now();
+#endif
     const uint64_t wv = (uint64_t)(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * WAVES;
+    const uint64_t nw = (uint64_t)a_grid * WAVES;
     const uint64_t gw = rfl64((uint64_t)blockIdx.x * WAVES + wv);
-    const uint64_t wt0 = rfl64(udiv_u((uint64_t)blockIdx.x * p.ntiles, gridDim.x));
-    const uint64_t wt1 = rfl64(udiv_u(((uint64_t)blockIdx.x + 1) * p.ntiles, gridDim.x));
+    // the static split (ScanParams::split_q): wave w's first tile, no division
+    auto split_at = [&](uint64_t w) -> uint64_t { return w * a_q + (w < a_r ? w : (uint64_t)a_r); };
     // geometry: G groups of 4 KiB per tile, T tiles per buffer, main region at hoff of every buffer
-    const uint32_t G = p.seg / kGroupBytes;
-    const uint64_t T = p.tiles_per_buf, tile_bytes = (uint64_t)p.seg * kWave;
-    const uint64_t hoff = buffer_edges<false>(p, 0).headend - p.base;
+    const uint32_t G = a_seg / kGroupBytes;
+    const uint64_t T = a_T, tile_bytes = (uint64_t)a_seg * kWave;
+    const uint64_t hoff = edges_of(a_bb0, a_len).headend - a_base;  // buffer 0 of batch 0
     const uint32_t voff = (uint32_t)WB * (uint32_t)lane;
-    const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
+    const uint64_t dummy = rfl64(a_kv);
     // the wave's tiles: t0, t0 + tstep, ... (ntw of them).  XCD windows (p.xcd_order): the waves of XCD
     // x = blockIdx mod 8 take tiles j, j + nwx, ... of the x-th eighth, so at every step an XCD's waves
     // read one compact window (DESIGN.md "Read order"); a buffer's T tiles go to T consecutive waves of
@@ -1467,13 +1516,13 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     constexpr bool xo = WB == 8 && XO;  // a separate instantiation: the contiguous split's loop is unchanged
     uint64_t t0, tstep = 1, ntw;
     if constexpr (xo) {
-        const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * p.ntiles / 8, xhi = (xcd + 1) * p.ntiles / 8;
+        const uint64_t nwx = nw / 8, xcd = blockIdx.x & 7u, xlo = xcd * a_ntiles / 8, xhi = (xcd + 1) * a_ntiles / 8;
         t0 = rfl64(xlo + (uint64_t)(blockIdx.x >> 3) * WAVES + wv);
         tstep = nwx;
         ntw = rfl64(t0 < xhi ? udiv_u(xhi - t0 + nwx - 1, nwx) : 0);
     } else {
-        t0 = rfl64(udiv_u(gw * p.ntiles, nw));
-        ntw = rfl64(udiv_u((gw + 1) * p.ntiles, nw)) - t0;
+        t0 = rfl64(split_at(gw));
+        ntw = rfl64(a_q + (gw < a_r ? 1u : 0u));
     }
     const uint32_t gsh = __builtin_ctz(G);
     const uint32_t nq = (uint32_t)(ntw << gsh);  // groups of this wave
@@ -1481,10 +1530,16 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // prefetch cursor: the next group to issue, as (buffer, tile, group); fbuf is the main-region
     // address of buffer fb, which walks batch by batch (fj, fi)
     uint32_t fq = 0;  // groups issued
-    uint64_t fb = udiv_u(t0, T), fk = t0 - fb * T;
+    uint64_t fb = a_tsh1 ? t0 >> (a_tsh1 - 1) : udiv_u(t0, T), fk = t0 - fb * T;
+    const uint64_t b_first = fb, k_first = fk;  // the scan cursor starts here too
     uint32_t fg = 0;
-    BatchPos fpos = work ? batch_pos(p, fb) : BatchPos{0, 0};
-    uint64_t fbuf = work ? karg64(p.bbase, fpos.j) + fpos.i * p.stride + hoff : 0;
+    BatchPos fpos{0, fb};
+    if (a_nbatch > 1) {
+        fpos.j = a_bsh1 ? fb >> (a_bsh1 - 1) : udiv_u(fb, a_bcount);
+        fpos.i = fb - fpos.j * a_bcount;
+    }
+    // (a wave starting in batch 0 needs no second round trip for its base)
+    uint64_t fbuf = work ? (fpos.j == 0 ? a_bb0 : karg64(p.bbase, fpos.j)) + fpos.i * a_stride + hoff : 0;
     uint64_t ft = t0;  // XCD windows: the tile being issued
     auto f_addr = [&]() -> uint64_t {
         uint64_t a = fq < nq ? fbuf + fk * tile_bytes + (uint64_t)fg * (kBraidRow * kBraidRowsPerGroup) : dummy;
@@ -1516,25 +1571,36 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
             }
         }
     };
-    // K-image words and P columns of this thread, published to LDS after the first scan step (ordinary
-    // loads: issued before the first group, so the compiler's wait for them in the peeled first step
-    // is the exact count of the row loads issued after them).  The K image is 8 KiB (512 x 16 B) and
-    // the P columns 4 KiB (1024 words) whatever the workgroup size.
-    const uint64_t *pcs = p.d_pcols ? p.d_pcols : p.d_kvals;
-    const uint32_t kti = (uint32_t)threadIdx.x & 511u;
-    const v4u kq = *(gv4u *)((const uint32_t *)p.d_kvals + SS::kKWord + 4 * kti);
-    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x);
-    const uint32_t pce1 = SS::kBlock < 1024 ? *(gu32 *)(pcs + threadIdx.x + SS::kBlock) : 0u;
-    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
-    LocalBufs lb{0, 0};
-    if (T > 1 && T <= 32) {
-        const uint64_t b0 = udiv_u(wt0 + T - 1, T), b1 = udiv_u(wt1, T);
-        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
-    }
     Grp ra, rb, rc;
     if (work) {
         stream_issue<0>(ra, voff, f_addr());
         f_next();
+    }
+#if AWS_CRT_AMD_DIAG
+    t_ra = stamp_now();
+#endif
+    // K-image words and P columns of this thread, published to LDS after the first scan step (ordinary
+    // loads between the first and the second group, so the compiler's wait for them in the peeled first
+    // step is the exact count of the row loads issued after them).  The K image is 8 KiB (512 x 16 B)
+    // and the P columns 4 KiB (1024 words) whatever the workgroup size.
+    const uint64_t *pcs = (const uint64_t *)(a_pc ? a_pc : a_kv);
+    const uint32_t kti = (uint32_t)threadIdx.x & 511u;
+    const v4u kq = *(gv4u *)((const uint32_t *)a_kv + SS::kKWord + 4 * kti);
+    const uint32_t pce0 = *(gu32 *)(pcs + threadIdx.x);
+    const uint32_t pce1 = SS::kBlock < 1024 ? *(gu32 *)(pcs + threadIdx.x + SS::kBlock) : 0u;
+    if (work) {
+        stream_issue<0>(rb, voff, f_addr());
+        f_next();
+    }
+#if AWS_CRT_AMD_DIAG
+    t_rb = stamp_now();
+#endif
+    // buffers wholly inside this workgroup's tile range (T <= 32, slots permitting): LDS combine
+    LocalBufs lb{0, 0};
+    if (!xo && T > 1 && T <= 32) {
+        const uint64_t wt0 = split_at((uint64_t)blockIdx.x * WAVES), wt1 = split_at(((uint64_t)blockIdx.x + 1) * WAVES);
+        const uint64_t b0 = udiv_u(wt0 + T - 1, T), b1 = udiv_u(wt1, T);
+        if (b1 > b0 && b1 - b0 <= kLocalSlots) lb = LocalBufs{b0, b1};
     }
     if constexpr (WB == 16) {
         // wave t builds table T'_t (t wave-uniform): entries lane + 64 n, 8 copies (two 16-byte stores)
@@ -1550,17 +1616,10 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
         }
         if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w16<POLY, 16>(threadIdx.x);
     } else if constexpr (WB == 8) {
-        // wave t builds table T'_t (t wave-uniform): entries lane + 64 n, 8 copies (two 16-byte stores)
-        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint32_t e = (uint32_t)lane + 64u * n;
-            const uint32_t te = basis_w8_rt<POLY>(t, e);
-            char *row = lds + (e << 8) + (t << 5);
-            *(uint4 *)row = make_uint4(te, te, te, te);
-            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
-        }
-        if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
+        static_assert(SS::kBlock == 512, "build_w8_tables: 512 threads");
+        const uint32_t tid = threadIdx.x;
+        build_w8_tables<POLY>(lds, tid);
+        if (tid < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * tid) = basis_w8<POLY, 8>(tid);
     } else {
         const uint32_t i = threadIdx.x;
         const uint32_t q = (i >> 1) & 3u, h = i & 1u;
@@ -1579,16 +1638,15 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     }
     if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
     if (threadIdx.x < kLocalSlots) ((unsigned long long *)(cb + (kLocalOff - kBKOff)))[threadIdx.x] = 0ull;
+#if AWS_CRT_AMD_DIAG
+    t_built = stamp_now();
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #if AWS_CRT_AMD_DIAG
     t_tab = stamp_now();
 #endif
     B eng;
     eng.init(lds, lane);
-    if (work) {
-        stream_issue<0>(rb, voff, f_addr());
-        f_next();
-    }
     bool consts_ready = false;
     // every wave publishes its share of the K image and P columns once and counts itself in LDS; a
     // wave spins on the count only before its first tile finish
@@ -1612,6 +1670,7 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
             uint64_t *w = stamps + kStampWords * ((uint64_t)blockIdx.x * WAVES + wv);
             w[0] = t_entry, w[1] = t_tab, w[2] = t_first, w[3] = t_loop, w[4] = stamp_now(), w[5] = stamp_hwid();
             w[6] = groups, w[7] = groups >> gsh;
+            w[8] = t_karg, w[9] = t_ra, w[10] = t_rb, w[11] = t_built;
         }
     };
 #endif
@@ -1626,8 +1685,8 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     // scan cursor: tile d (buffer, index in buffer), group g, global group q
     Tile d;
     d.T = T;
-    d.b = udiv_u(t0, T);
-    d.k = t0 - d.b * T;
+    d.b = b_first;
+    d.k = k_first;
     d.tbase = d.b * T;
     d.vbase = 0;
     d.pad = 0;
@@ -1840,15 +1899,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     list_issue<0>(ra, f_rsrc(), f_off(), f_lim());
     f_next();
     {
-        const uint32_t t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint32_t e = (uint32_t)lane + 64u * n;
-            const uint32_t te = basis_w8_rt<POLY>(t, e);
-            char *row = lds + (e << 8) + (t << 5);
-            *(uint4 *)row = make_uint4(te, te, te, te);
-            *(uint4 *)(row + 16) = make_uint4(te, te, te, te);
-        }
+        static_assert(kBraidBlock == 512, "build_w8_tables: 512 threads");
+        build_w8_tables<POLY>(lds, threadIdx.x);
         if (threadIdx.x < 256) *(uint32_t *)(cb + (kT0Off - kBKOff) + 4 * threadIdx.x) = basis_w8<POLY, 8>(threadIdx.x);
     }
     if (threadIdx.x == 0) *(uint32_t *)(cb + (kConstFlagOff - kBKOff)) = 0u;
@@ -2292,22 +2344,39 @@ __device__ __forceinline__ void b64_build_tables(char *lds) {
     if (i < 256) *(uint64_t *)(lds + kB64T0Off + 8 * i) = basis64<POLY, 8>(i);
 }
 
-// the 4-copy layout (Braid64<POLY, 4>) from 512 threads: thread i fills the table of byte
-// t = i >> 6 of a (T'_(7-t), wave-uniform) for entries (i & 63) + 64 n, n < 4, two 16-byte stores
-// (4 copies) each; then T0
+// the 4-copy layout (Braid64<POLY, 4>: row e of 256 bytes, slot t at 32 t holding T'_(7-t)[e] in 4
+// copies) from 512 threads, as 4096 chunks of 16 bytes: chunk k = i + 512 m holds copies 2 (k & 1),
+// +1 of slot t = (k & 15) >> 1 of entry e = k >> 4 = (i >> 4) + 32 m; consecutive lanes store
+// consecutive chunks (conflict-free, as build_w8_tables; round 4 built slot t in wave t, one 32-byte
+// bank group per store); then T0
 template <uint64_t POLY, uint32_t ROW = kB64Row>
 __device__ __forceinline__ void b64x4_build_tables(char *lds) {
+    constexpr Braid64Basis<POLY, ROW> B{};
     const uint32_t i = threadIdx.x;
-    if (i >= 512) return;  // eight waves build the eight tables
-    const uint32_t t = __builtin_amdgcn_readfirstlane(i >> 6);
+    if (i >= 512) return;
+    const uint32_t t = (i & 15u) >> 1;
+    uint32_t mk[8];  // opaque per-lane masks: table 7 - t (a select chain over constants would load them)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const uint32_t e = (i & 63u) + 64u * n;
-        const uint64_t v = basis64_rt<POLY, ROW>(7u - t, e);
-        const v4u vv = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
-        char *row = lds + (e << 8) + (t << 5);
-        *(v4u *)(row + (((i >> 2) & 1u) << 4)) = vv;
-        *(v4u *)(row + ((((i >> 2) & 1u) ^ 1u) << 4)) = vv;
+    for (int k = 0; k < 8; ++k) {
+        mk[k] = t == 7u - (uint32_t)k ? ~0u : 0u;
+        asm("" : "+v"(mk[k]));
+    }
+    uint64_t bt[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lo |= (uint32_t)B.b[k][b] & mk[k], hi |= (uint32_t)(B.b[k][b] >> 32) & mk[k];
+        bt[b] = ((uint64_t)hi << 32) | lo;
+    }
+    const uint32_t e0 = i >> 4;
+    uint64_t v0 = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) v0 ^= ((e0 >> b) & 1u) ? bt[b] : 0ull;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const uint64_t v = v0 ^ (m & 1 ? bt[5] : 0ull) ^ (m & 2 ? bt[6] : 0ull) ^ (m & 4 ? bt[7] : 0ull);
+        *(v4u *)(lds + 16u * (i + 512u * m)) = v4u{(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)v, (uint32_t)(v >> 32)};
     }
     if (i < 256) *(uint64_t *)(lds + kB64x4T0Off + 8 * i) = basis64<POLY, 8>(i);
 }

@@ -66,6 +66,40 @@ def main():
                                         "parity": eng.as_unsigned(res) == want}
     del d
     torch.cuda.empty_cache()
+    # C5's XXH64 shape (8 x 64 MiB) on one stream and on three streams at once
+    # (each its own bytes), beside the D2H-only rate of the same bytes (the route's PCIe ceiling)
+    n8, L8 = 8, 64 << 20
+    ds = [torch.randint(0, 256, (n8 * L8,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(3)]
+    sts = [torch.cuda.Stream() for _ in range(3)]
+    outs = [torch.empty(n8, dtype=torch.int64, device="cuda") for _ in range(3)]
+
+    def run(k_streams, reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for k in range(k_streams):
+                eng.checksum_strided(eng.XXH64, ds[k], L8, L8, n8, out=outs[k], stream=sts[k])
+        torch.cuda.synchronize()
+        return k_streams * reps * n8 * L8 / (time.perf_counter() - t0) / 2**30
+
+    run(3, 1)
+    one, three = run(1, args.reps), run(3, args.reps)
+    pin = torch.empty(n8 * L8, dtype=torch.uint8, pin_memory=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        pin.copy_(ds[0], non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = args.reps * n8 * L8 / (time.perf_counter() - t0) / 2**30
+    par = []
+    for k in range(3):
+        h = ds[k].cpu().numpy()
+        par.append(eng.as_unsigned(outs[k]) == eng.cpu_batch(eng.XXH64, [h.ctypes.data + i * L8 for i in range(n8)], [L8] * n8,
+                                                             threads=8))
+    out["xxh64_c5_streams"] = {"one_stream_gibs": round(one, 2), "three_streams_gibs": round(three, 2),
+                               "ratio": round(three / one, 3), "d2h_only_gibs": round(d2h, 2), "parity": all(par)}
+    del ds, pin
+    torch.cuda.empty_cache()
     # streaming XXH3 over one device chunk
     n = args.stream_mib << 20
     d = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 import aws_crt_amd as eng  # noqa: E402
 
 TICK_US = 0.01
-W = 8  # words per wave
+W = 16  # words per wave (crc_kernels.hip kStampWords)
 
 
 def pct(v, ps=(0, 10, 50, 90, 99, 100)):
@@ -37,6 +37,9 @@ def analyse(st, nw):
     span = max(ex)
     work = [r for r in rows if r[6] > 0]
     tab = [(r[1] - r[0]) * TICK_US for r in rows]
+    pro = {name: pct([(r[k] - r[0]) * TICK_US for r in work]) for name, k in
+           (("kernel_args_in_us", 8), ("first_group_issued_us", 9), ("second_group_issued_us", 10),
+            ("tables_stored_us", 11), ("barrier_passed_us", 1))}
     first = [(r[2] - r[1]) * TICK_US for r in work]
     life = [(r[4] - r[0]) * TICK_US for r in work]
     fin = [(r[4] - r[3]) * TICK_US for r in work]
@@ -49,7 +52,7 @@ def analyse(st, nw):
                   "max_exit_us": round(max(e for e, _ in v), 2), "median_exit_us": round(statistics.median(e for e, _ in v), 2)}
               for x, v in sorted(xcc.items())}
     return {"waves": len(rows), "working_waves": len(work), "groups_per_wave": pct([r[6] for r in work], (0, 50, 100)),
-            "span_us": round(span, 2), "entry_us": pct(entry), "tables_us": pct(tab), "first_group_us": pct(first),
+            "span_us": round(span, 2), "entry_us": pct(entry), "tables_us": pct(tab), "prologue_from_entry": pro, "first_group_us": pct(first),
             "per_group_us": pct(per_group), "life_us": pct(life), "mean_life_frac": round(statistics.mean(life) / span, 4),
             "final_finish_us": pct(fin), "exit_us": pct(ex), "by_xcc": by_xcc}
 

@@ -837,6 +837,7 @@ def main_rank(args):
         dist.barrier()
     subs = rig.prepare(args.steps, G) if args.steps > 0 else []
     torch.cuda.synchronize()
+    w0 = time.time()
     t0 = time.perf_counter()
     for bs, st in subs:
         bs.run(st)
@@ -844,10 +845,15 @@ def main_rank(args):
     # each rank's clock stops when its own GPU is done; the closing barrier follows, and the slowest
     # rank's time (max over ranks) is the job's, so the barrier's own latency is not counted as work
     own = time.perf_counter() - t0
+    w1 = time.time()
     if world > 1:
         dist.barrier()
         torch.cuda.synchronize()
     elapsed = max_over_ranks(own)
+    # the job's wall-clock span on this node (first rank's start to last rank's end): equal to
+    # `elapsed` when the ranks start together; on a gloo rehearsal with shared devices the ranks'
+    # regions need not overlap, so there `value` is no N-GPU rate and the span is reported beside it
+    span = max_over_ranks(w1) + max_over_ranks(-w0)
     value = world * args.steps * step_bytes / max(elapsed, 1e-9) / 2**30
 
     # the same K steps submitted one launch per batch (--coalesce 1), timed the same way: the rate a
@@ -984,8 +990,10 @@ def main_rank(args):
             "per_gpu_gibs": round(value / world, 2),
             "devices_used": used,
             "shared_devices": shared,
+            "span_ms": round(span * 1e3, 4),
             "parity": parity_all,
             "ranks": ranks,
+            **({"note": "gloo rehearsal on shared devices: value is not an N-GPU rate"} if shared else {}),
             "box": box_state(torch.cuda.get_device_properties(dev)),
             "one_batch_per_launch": one_per_launch,
             "queued_one_at_a_time": queued,

@@ -60,6 +60,8 @@ for s in "$@"; do
     lat)   step 120 $O/lat.log bash -c "experiments/build/abi_latency 200000 && AWS_CRT_AMD_PTR_CACHE=0 experiments/build/abi_latency 200000"; rc=$?; cat $O/lat.log ;;
     # the multi-GPU rank path rehearsed on the box's one GPU (two gloo ranks) and the in-process fan-out
     ranks) step 300 $O/ranks.log bash -c "python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-configs --e2e-batches 0 --no-cpu-baseline && python -u bench.py --inproc --gpus 1 --steps 20 --warmup 5"; rc=$?; grep '^{' $O/ranks.log | cut -c1-600 ;;
+    # every config leg's kernel fraction (no CPU baseline, no host legs)
+    legs)  step 400 $O/legs.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-batches 0; rc=$?; grep '^{' $O/legs.log | cut -c1-300 ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }

