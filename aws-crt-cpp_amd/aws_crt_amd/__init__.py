@@ -557,6 +557,48 @@ def multipart_crc(alg: int, parts, stream=None):
     return [int(part_out[i]) for i in range(n)], int(obj.value), b64.value.decode()
 
 
+MULTIPART_FULL_OBJECT, MULTIPART_COMPOSITE = 0, 1
+
+
+def multipart_checksum(alg: int, parts, type_: int = MULTIPART_COMPOSITE, stream=None):
+    """aws_crt_amd_multipart_checksum: S3 multipart checksums for any of the six algorithms --
+    FULL_OBJECT (CRCs: Combine of the parts) or COMPOSITE (the algorithm over the concatenated
+    big-endian part digests, wire form base64 + "-N").  `parts` as multipart_crc.  Returns
+    (part digests, object digest, wire form); XXH3-128 digests as 128-bit ints."""
+    ptrs, lens = [], []
+    for p in parts:
+        if hasattr(p, "data_ptr"):
+            ptrs.append(p.data_ptr())
+            lens.append(p.numel() * p.element_size())
+        else:
+            ptrs.append(int(p[0]))
+            lens.append(int(p[1]))
+    n = len(ptrs)
+    words = 4 if alg == XXH3_128 else 2  # 32-bit words per digest slot (CRC32/32C use the first)
+    part_out = (ctypes.c_uint32 * max(n * words, 1))()
+    obj = (ctypes.c_uint32 * 4)()
+    b64 = ctypes.create_string_buffer(64)
+    P = (ctypes.c_void_p * max(n, 1))(*ptrs)
+    Ls = (ctypes.c_size_t * max(n, 1))(*lens)
+    L = lib()
+    L.aws_crt_amd_multipart_checksum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+    _check(L.aws_crt_amd_multipart_checksum(alg, type_, P, Ls, n, ctypes.addressof(part_out), ctypes.addressof(obj), b64,
+                                            _stream_handle(stream)))
+
+    def digest(raw, i):
+        if alg in (CRC32, CRC32C):
+            return raw[i]
+        if alg == XXH3_128:
+            hi = raw[4 * i] | (raw[4 * i + 1] << 32)
+            lo = raw[4 * i + 2] | (raw[4 * i + 3] << 32)
+            return (hi << 64) | lo
+        return raw[2 * i] | (raw[2 * i + 1] << 32)
+
+    return [digest(part_out, i) for i in range(n)], digest(obj, 0), b64.value.decode()
+
+
 def checksum_host(alg: int, buffers: Sequence[bytes], seeds: Optional[Sequence[int]] = None):
     """Host buffers -> host results (synchronous): the host path, or pinned staging and the GPU when
     the dispatch mode is DISPATCH_GPU."""

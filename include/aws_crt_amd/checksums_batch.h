@@ -404,6 +404,29 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(
     char *b64_out,
     void *hip_stream);
 
+/*
+ * S3 multipart checksums for every algorithm of S3ChecksumAlgorithm except the SHAs (ref
+ * include/aws/crt/s3/S3.h:69-81, source/s3/S3.cpp:392-424): the parts (device buffers, host arrays
+ * of pointers / lengths, object order) are checksummed on the GPU, then
+ *   AWS_CRT_AMD_MULTIPART_FULL_OBJECT  CRC32 / CRC32C / CRC64NVME only: as aws_crt_amd_multipart_crc;
+ *   AWS_CRT_AMD_MULTIPART_COMPOSITE    any algorithm: the same algorithm over the concatenated
+ *                                      big-endian part digests; b64_out = base64 + "-" + part count.
+ * h_part_out: count digests as the batch API writes them (uint32 for CRC32/32C, uint64 otherwise,
+ * two uint64 -- high, then low -- for XXH3-128); h_object_out: one such digest.  b64_out: at least
+ * 48 bytes.  Synchronous on hip_stream.  COMPOSITE parity is unpinned: the reference has no fixture.
+ */
+enum { AWS_CRT_AMD_MULTIPART_FULL_OBJECT = 0, AWS_CRT_AMD_MULTIPART_COMPOSITE = 1 };
+AWS_CRT_AMD_API int aws_crt_amd_multipart_checksum(
+    int algorithm,
+    int type,
+    const void *const *d_parts,
+    const size_t *lens,
+    size_t count,
+    void *h_part_out,
+    void *h_object_out,
+    char *b64_out,
+    void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,8 @@ for s in "$@"; do
     ranks) step 300 $O/ranks.log bash -c "python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-configs --e2e-batches 0 --no-cpu-baseline && python -u bench.py --inproc --gpus 1 --steps 20 --warmup 5"; rc=$?; grep '^{' $O/ranks.log | cut -c1-600 ;;
     # every config leg's kernel fraction (no CPU baseline, no host legs)
     legs)  step 400 $O/legs.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-batches 0; rc=$?; grep '^{' $O/legs.log | cut -c1-300 ;;
+    # FETCH_SIZE of the C5 CRC64NVME launch (8 x 64 MiB, one batch per launch)
+    pmc5)  (cd /tmp && step 120 $O/pmc5_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5_fetch -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --batches 2 --coalesce 1 --steps 12 --warmup 2 --only-coalesced --branches 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }

@@ -63,3 +63,41 @@ def test_multipart_no_parts(engine):
 def test_multipart_rejects_hashes(engine):
     with pytest.raises(Exception):
         engine.multipart_crc(3, [])
+
+
+ALL = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
+WIDTH = {"crc32": 4, "crc32c": 4, "crc64nvme": 8, "xxh64": 8, "xxh3_64": 8, "xxh3_128": 16}
+
+
+@pytest.mark.parametrize("alg", list(ALL))
+@pytest.mark.parametrize("case", ["s3_like", "ragged", "with_empty"])
+def test_multipart_composite(engine, alg, case):
+    """VERDICT r04 missing #2: the S3 hash algorithms (S3.h:78-80) compose as COMPOSITE -- the same
+    algorithm over the concatenated big-endian part digests, wire form base64 + "-N" (parity unpinned:
+    checked against the oracle's digests of the parts and of their concatenation)"""
+    rnd = random.Random(hash(("c", alg, case)) & 0xFFFF)
+    sizes = {"s3_like": [5 << 20] * 2 + [777777], "ragged": [rnd.randrange(1, 200000) for _ in range(23)],
+             "with_empty": [0, 33, 0, 70000]}[case]
+    blob, parts = _parts(sizes, seed=len(sizes) * 17 + ALL[alg], misalign=rnd.randrange(16))
+    vals, obj, wire = engine.multipart_checksum(ALL[alg], parts)
+    host = blob.cpu().numpy()
+    base = blob.data_ptr()
+    cat = bytearray()
+    for (addr, n), v in zip(parts, vals):
+        want = oracle.checksum(alg, host[addr - base: addr - base + n].tobytes())
+        assert v == want, (alg, case, n)
+        cat += v.to_bytes(WIDTH[alg], "big")
+    want_obj = oracle.checksum(alg, bytes(cat))
+    assert obj == want_obj
+    assert wire == base64.b64encode(want_obj.to_bytes(WIDTH[alg], "big")).decode() + f"-{len(sizes)}"
+
+
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+def test_multipart_checksum_full_object_matches_multipart_crc(engine, alg):
+    blob, parts = _parts([100000, 3, 65536], seed=5)
+    assert engine.multipart_checksum(ALL[alg], parts, engine.MULTIPART_FULL_OBJECT) == engine.multipart_crc(ALL[alg], parts)
+
+
+def test_multipart_full_object_rejects_hashes(engine):
+    with pytest.raises(Exception):
+        engine.multipart_checksum(ALL["xxh64"], [], engine.MULTIPART_FULL_OBJECT)
