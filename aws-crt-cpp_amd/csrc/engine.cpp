@@ -611,7 +611,7 @@ int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
     return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("hash kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;
 }
 
-// log2(v) + 1 when v is a power of two, else 0 (ScanParams::tshift1 / bshift1)
+// log2(v) + 1 when v is a power of two, else 0 (ScanParams::shifts1)
 uint8_t pow2_shift1(uint64_t v) { return v && (v & (v - 1)) == 0 ? (uint8_t)(__builtin_ctzll(v) + 1) : (uint8_t)0; }
 
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, uint64_t total_main, hipStream_t s) {
@@ -652,7 +652,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
         const uint64_t nw = blocks * 8;
         p.split_q = p.ntiles / nw;
         p.split_r = (uint32_t)(p.ntiles % nw);
-        p.tshift1 = pow2_shift1(p.tiles_per_buf);
+        p.shifts1 = (p.shifts1 & ~0xFFu) | pow2_shift1(p.tiles_per_buf);
     }
     if (t_plan) {
         PlannedLaunch pl;
@@ -950,7 +950,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     ScanParams p{};
     p.nbatch = (uint32_t)nb;
     p.bcount = count;
-    p.bshift1 = pow2_shift1(count);
+    p.shifts1 = (uint32_t)pow2_shift1(count) << 8;
     for (size_t j = 0; j < nb; ++j) {
         p.bbase[j] = bs[j].base;
         p.bout[j] = (uint64_t)(uintptr_t)bs[j].out;

@@ -104,10 +104,10 @@ struct ScanParams {
     // ---- round 5: the division-free prologue of crc32_stream_kernel.  Wave w of the launch's nw
     // waves takes tiles [w q + min(w, r), + q + (w < r)) (split_q = ntiles / nw, split_r = ntiles % nw,
     // set by the host once the grid is known).  tshift1 / bshift1: log2 + 1 of tiles_per_buf / bcount
-    // when it is a power of two, else 0 (the kernels then divide).
+    // when it is a power of two, else 0 (the kernels then divide), packed as tshift1 | bshift1 << 8.
     uint64_t split_q;
     uint32_t split_r;
-    uint8_t tshift1, bshift1, pad0[2];
+    uint32_t shifts1;
 };
 
 // W=32 braided scan constants (engine.cpp get_braid_consts), u32 words:

@@ -10,7 +10,7 @@ for r in $(seq 1 ${REPS:-3}); do
   for v in ${VARIANTS:-A B}; do
     cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so || exit 1
     bash scripts/gpu_step.sh 200 $O/${v}_$r.log "$@" || exit 1
-    echo "$v $r $(grep '^{' $O/${v}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.readline()); print(d["value"], d["roofline"]["frac"], d["roofline"]["kernel_ms"])')"
+    echo "$v $r $(grep '^{' $O/${v}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.readline()); r=d["roofline"]; sb=r.get("single_batch") or {}; print(d["value"], r["frac"], r["kernel_ms"], "one", (d.get("one_batch_per_launch") or {}).get("value"), "sb", sb.get("frac"), sb.get("kernel_ms"))')"
   done
 done
 cp /tmp/ab_release.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so

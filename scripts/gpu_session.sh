@@ -64,6 +64,8 @@ for s in "$@"; do
     legs)  step 400 $O/legs.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-batches 0; rc=$?; grep '^{' $O/legs.log | cut -c1-300 ;;
     # FETCH_SIZE of the C5 CRC64NVME launch (8 x 64 MiB, one batch per launch)
     pmc5)  (cd /tmp && step 120 $O/pmc5_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5_fetch -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --batches 2 --coalesce 1 --steps 12 --warmup 2 --only-coalesced --branches 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
+    # A/B of library builds on the C4 shard CRC64NVME launch (131072 x 8 KiB, crc64_rows16_kernel)
+    abr16) step 900 $O/abr16.log env TAG=${TAG}/abr16 VARIANTS="${R16VARIANTS:-R OLD}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --alg crc64nvme --buffers 131072 --buffer-bytes 8192 --batches 2 --coalesce 1 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/abr16.log ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }
