@@ -2776,6 +2776,15 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     constexpr int kWaves = BLOCK / 64;
     static_assert(kWaves <= 16, "two held-part slots per wave, 32 entries");
     const int lane = threadIdx.x & 63;
+    // the kernel arguments the first group's address needs, in one batch of scalar loads with one wait
+    // (crc32_stream_kernel's round-5 prologue: the compiler had spread them over dependent round trips)
+    {
+        const uint64_t a0 = p.ntiles, a1 = p.tiles_per_buf, a2 = p.base, a3 = p.stride, a4 = p.len, a5 = p.bcount,
+                       a6 = (uint64_t)p.d_kvals, a7 = (uint64_t)p.d_pcols, a8 = p.bbase[0];
+        const uint32_t a9 = p.nbatch, a10 = p.xcd_pad, a11 = gridDim.x;
+        asm volatile("" ::"s"(a0), "s"(a1), "s"(a2), "s"(a3), "s"(a4), "s"(a5), "s"(a6), "s"(a7), "s"(a8), "s"(a9), "s"(a10),
+                     "s"(a11));
+    }
     const uint64_t nwx = (uint64_t)gridDim.x * kWaves / 8;  // waves per XCD (gridDim % 8 == 0)
     const uint64_t xcd = blockIdx.x & 7u;
     const uint64_t j = rfl64((uint64_t)(blockIdx.x >> 3) * kWaves + (threadIdx.x >> 6));
@@ -2835,11 +2844,21 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
             if (fq < nq) cur_next(fc);
         }
     };
+    // the tile-finish constants (needed before the barrier), then the wave's first two groups, issued
+    // unconditionally (placeholder rows past a wave's last group), so that the wait for the constants
+    // is one exact count on every path and both groups stream while the tables are built (round 5; the
+    // conditional issue had left the compiler a vmcnt(0) before the barrier)
+    // (PADDED keeps the round-4 order -- the first group only, the second after the barrier: its
+    // buffer resources then push the kernel to 128 VGPRs and spill)
     const uint64_t kl = *(gu64 *)(p.d_kvals + lane);
     const uint64_t jt = threadIdx.x < 256 ? *(gu64 *)(p.d_pcols + threadIdx.x) : 0ull;
     B64Group ra, rb, rc;
-    if (nq) {
+    if (!PADDED || nq) {
         issue(ra);
+        f_next();
+    }
+    if constexpr (!PADDED) {
+        issue(rb);
         f_next();
     }
     b64x4_build_tables<POLY>(lds);
@@ -2941,11 +2960,17 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
         }
     };
     if (!nq) {
+        if constexpr (!PADDED)  // the placeholder groups land before the wave ends
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ra.w[0]), "+v"(ra.w[1]), "+v"(ra.w[2]), "+v"(ra.w[3]), "+v"(ra.w[4]),
+                         "+v"(ra.w[5]), "+v"(ra.w[6]), "+v"(ra.w[7]), "+v"(rb.w[0]), "+v"(rb.w[1]), "+v"(rb.w[2]), "+v"(rb.w[3]),
+                         "+v"(rb.w[4]), "+v"(rb.w[5]), "+v"(rb.w[6]), "+v"(rb.w[7])::"memory");
         final_parts(false);
         return;
     }
-    issue(rb);
-    f_next();
+    if constexpr (PADDED) {
+        issue(rb);
+        f_next();
+    }
 
     // the head state enters lane (pad mod 512) / 8 at the start of chunk 0 divided by X^jr (X = x^(8*512),
     // jr = the pad's row): that lane's words before the pad are zero, so jr row steps bring it to the head
