@@ -113,14 +113,6 @@ __device__ __forceinline__ uint32_t wave_xor_s(uint32_t v) {
     return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) ^ __builtin_amdgcn_readlane((int)v, 16) ^
                       __builtin_amdgcn_readlane((int)v, 32) ^ __builtin_amdgcn_readlane((int)v, 48));
 }
-__device__ __forceinline__ uint32_t wave_add_s(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
-    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) + __builtin_amdgcn_readlane((int)v, 16) +
-                      __builtin_amdgcn_readlane((int)v, 32) + __builtin_amdgcn_readlane((int)v, 48));
-}
 __device__ __forceinline__ uint64_t wave_xor64_s(uint64_t v) {
     const uint32_t lo = wave_xor_s((uint32_t)v), hi = wave_xor_s((uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
@@ -2706,14 +2698,16 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
 //    LDS (16 broadcast-friendly reads; ScanParams::d_pcols holds them and the shift columns).
 //  * A part (the wave's chunks of one buffer) ends with the stream kernel's tile finish (lane shares
 //    K_l, wave XOR), moved to the buffer end by x^(8 * chunk * m), m = chunks after its last one (one
-//    column product per set bit of m), then XORed into the buffer's accumulator; the part adds its
-//    chunk count, and the part completing the buffer's count finalises it.
+//    column product per set bit of m), then XORed into the workgroup's part table in LDS (one entry per
+//    buffer: value, chunk count).  After the scan wave 0 publishes the table, one entry per lane, into
+//    the buffers' accumulators and counts; the entry completing a buffer's count finalises it.
 // Taken by strided CRC64NVME launches whose main regions are whole chunks of at least kXcdMinChunks.
 constexpr int kXcdChunkGroups = AMDCRC_XCD_CHUNK_GROUPS;
 constexpr uint32_t kXcdChunk = kXcdChunkGroups * kB64Row * kB64RowsPerGroup;
 constexpr uint32_t kXcdJumpOff = kB64x4Lds;               // 16 nibbles x 16 x u64: v << 4n times J
-constexpr uint32_t kXcdSlotOff = kXcdJumpOff + 16 * 16 * 8;  // two held parts per wave (b, value, chunks)
-constexpr uint32_t kXcdLds = kXcdSlotOff + 32 * 32;           // up to 16 waves
+constexpr uint32_t kXcdSlotOff = kXcdJumpOff + 16 * 16 * 8;  // part table: buffer, value, chunks
+constexpr uint32_t kXcdSlots = 64;
+constexpr uint32_t kXcdLds = kXcdSlotOff + kXcdSlots * (8 + 8 + 4);
 static_assert(2 * kXcdLds <= 160 * 1024, "two crc64_xcd_kernel workgroups per CU");
 
 __device__ __forceinline__ uint64_t xcd_jump(const char *lds, uint64_t u) {
@@ -2774,7 +2768,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
     constexpr int kWaves = BLOCK / 64;
-    static_assert(kWaves <= 16, "two held-part slots per wave, 32 entries");
     const int lane = threadIdx.x & 63;
     // the kernel arguments the first group's address needs, in one batch of scalar loads with one wait
     // (crc32_stream_kernel's round-5 prologue: the compiler had spread them over dependent round trips)
@@ -2864,6 +2857,10 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     b64x4_build_tables<POLY>(lds);
     b64x4_build_nib<POLY>(lds, kl);
     if (threadIdx.x < 256) *(uint64_t *)(lds + kXcdJumpOff + 8u * threadIdx.x) = jt;
+    uint64_t *const ptag = (uint64_t *)(lds + kXcdSlotOff);  // the part table (empty tag ~0)
+    uint64_t *const pval = ptag + kXcdSlots;
+    uint32_t *const pcnt = (uint32_t *)(pval + kXcdSlots);
+    if (threadIdx.x < kXcdSlots) ptag[threadIdx.x] = ~0ull, pval[threadIdx.x] = 0ull, pcnt[threadIdx.x] = 0u;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     B eng;
     eng.init(lds, lane);
@@ -2912,51 +2909,55 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
             finalize<false>(p, b, fin, eng);
         }
     };
-    // A part that ends inside the scan is held (one per wave) and published with the wave's last part:
-    // the waves of an XCD cross a buffer boundary at about the same step, and 512 returning atomics on
-    // one address at once would stall every one of them (with its payload ring drained).  An older held
-    // part is published at once.
-    uint64_t hb = ~0ull, hr = 0, hk = 0;  // the held part: buffer, raw register, last chunk, chunks
-    uint32_t hn = 0;
-    auto part_finish = [&]() {
-        const uint64_t r = part_raw();
-        if (hb != ~0ull) {
-            const uint64_t v = shift_scalar(hr, CPB - 1 - hk);
-            if (lane == 0) publish(hb, v, hn);
+    // a part into the workgroup's table (lane 0; LDS atomics, open addressing from b): no global atomic
+    // and so no drained payload ring inside the scan (round 4's held parts published one part per buffer
+    // crossing with three returning atomics, each a vmcnt(0): 20-batch C5 launches at 0.66 against 0.77
+    // for one batch).  A full table -- more than kXcdSlots buffers in one workgroup -- publishes directly.
+    auto part_put = [&](uint64_t b, uint64_t v, uint32_t n) {
+        for (uint32_t i = 0; i < kXcdSlots; ++i) {
+            const uint32_t e = ((uint32_t)b + i) & (kXcdSlots - 1);
+            uint64_t t = ~0ull;
+            __hip_atomic_compare_exchange_strong(&ptag[e], &t, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t == ~0ull || t == b) {
+                __hip_atomic_fetch_xor(&pval[e], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&pcnt[e], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return;
+            }
         }
-        hb = pb, hr = r, hk = pk, hn = pn;
+        publish(b, v, n);
     };
-    // every wave's held and last parts go through LDS: wave 0 joins the parts of one buffer, so the
-    // workgroup's eight waves (neighbouring chunks at every step) meet its accumulator once
+    auto part_finish = [&]() {
+        const uint64_t v = shift_scalar(part_raw(), CPB - 1 - pk);
+        if (lane == 0) part_put(pb, v, pn);
+    };
+    // the wave's last part, then wave 0 publishes the table: entry e in lane e, all accumulators in one
+    // round trip and all counts in a second; the buffers completed finalise one at a time
     auto final_parts = [&](bool have) {
-        const uint64_t r = have ? shift_lanes(part_raw(), CPB - 1 - pk) : 0ull;
-        const uint64_t h = hb != ~0ull ? shift_lanes(hr, CPB - 1 - hk) : 0ull;
-        if (lane == 0) {
-            uint64_t *slot = (uint64_t *)(lds + kXcdSlotOff) + 8 * (threadIdx.x >> 6);
-            slot[0] = have ? pb : ~0ull;
-            slot[1] = r;
-            slot[2] = have ? pn : 0u;
-            slot[4] = hb;
-            slot[5] = h;
-            slot[6] = hn;
+        if (have) {
+            const uint64_t v = shift_lanes(part_raw(), CPB - 1 - pk);
+            if (lane == 0) part_put(pb, v, pn);
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (threadIdx.x >= 64) return;
-        // wave 0: entry e in lane e (< 2 per wave); one publication per distinct buffer
-        constexpr int kEntries = 2 * kWaves;
-        const uint64_t *slot = (const uint64_t *)(lds + kXcdSlotOff) + 4 * (lane < kEntries ? lane : 0);
-        uint64_t eb = lane < kEntries ? slot[0] : ~0ull;
-        const uint64_t er = slot[1];
-        const uint32_t en = (uint32_t)slot[2];
-        for (int e = 0; e < kEntries; ++e) {
+        static_assert(kXcdSlots == 64, "one table entry per lane of wave 0");
+        const uint64_t eb = ptag[lane];
+        bool done = false;
+        if (eb != ~0ull) {
+            const uint32_t en = pcnt[lane];
+            (void)sx_xor64_ret(&p.d_acc[eb], (unsigned long long)pval[lane]);  // every value lands first
+            done = sx_add32_ret(&p.d_cnt[eb], en) + en == (unsigned int)CPB;
+        }
+        uint64_t fm = __builtin_amdgcn_ballot_w64(done);
+        while (fm) {
+            const int e = __builtin_ctzll(fm);
+            fm &= fm - 1;
             const uint64_t b = rfl64((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)eb, e) |
                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(eb >> 32), e) << 32));
-            if (b == ~0ull) continue;
-            const bool mine = eb == b;
-            const uint64_t r = wave_xor64_s(mine ? er : 0ull);
-            const uint32_t n = wave_add_s(mine ? en : 0u);
-            if (mine) eb = ~0ull;
-            if (lane == 0) publish(b, r, n);
+            if (lane == 0) {
+                const uint64_t fin = sx_swap64_ret(&p.d_acc[b], 0ull);
+                sx_store32(&p.d_cnt[b], 0u);
+                finalize<false>(p, b, fin, eng);
+            }
         }
     };
     if (!nq) {

@@ -682,11 +682,13 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
 // gfx950 SIMD a round is issue-bound at about 41 cycles (experiments/chainbench.hip: 31.5 for the six chain
 // instructions, 9 more for the two DPP moves that bring the next stripe's product in), 1.7 GiB/s
 // per buffer, against about 1.3 ns per round on one host core.  A batch of at most kX64HostMaxBuffers
-// long buffers therefore goes to the host: slices of every buffer (one hipMemcpy2DAsync per slice)
-// are copied D2H on the device's copy stream into two pinned halves, alternately, while the caller's
-// stream runs host functions that hash the previous slice with one thread per buffer; the results go
-// back H2D on the caller's stream.  The call keeps the batch ABI's asynchronous, stream-ordered
-// contract (the copies wait for the caller's stream; later work on it waits for the results).
+// long buffers therefore goes to the host: slices of every buffer (one hipMemcpy2DAsync per slice) are
+// copied D2H on the caller's stream into two pinned halves, alternately, each copy gated by a stream
+// wait on a signal-memory counter that the host worker advances once it has hashed the slice two back;
+// the worker (a runner thread, not HIP's callback thread: round 5) hashes a slice with one pool thread
+// per buffer as soon as its copy lands, and the results go back H2D on the caller's stream behind a
+// final wait.  The call keeps the batch ABI's asynchronous, stream-ordered contract.
+// AWS_CRT_AMD_XXH64_ROUTE=0 (read per call) keeps every batch on the GPU kernels.
 #ifndef AMDCRC_X64_HOST_MAX  // compile-time only (A/B builds: 0 keeps every XXH64 batch on the GPU kernels)
 #define AMDCRC_X64_HOST_MAX 16
 #endif
@@ -742,14 +744,26 @@ inline void sig_store(uint64_t *p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC
 // The job's host worker (a runner thread, never the runtime's callback thread): slice k once the copy
 // stream reports it copied, one host thread per buffer; then the stage goes back once the caller's
 // stream has taken the results.
+// AWS_CRT_AMD_X64_TRACE=1 prints one line per job: time waiting for copies, time hashing.
 void x64_work(X64Job *j) noexcept {
     X64Stage *st = j->st;
+    static const bool trace = [] {
+        const char *e = getenv("AWS_CRT_AMD_X64_TRACE");
+        return e && e[0] == '1';
+    }();
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    double wait_us = 0, hash_us = 0, first_us = 0;
     for (size_t k = 0; k < j->nslices; ++k) {
         const uint64_t want = j->base + k + 1;
+        const auto w0 = clk::now();
         for (unsigned spin = 0; sig_load(st->copied) < want; ++spin) {
             if (spin < 64) std::this_thread::yield();
             else std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
+        const auto w1 = clk::now();
+        if (k == 0) first_us = std::chrono::duration<double, std::micro>(w1 - w0).count();
+        else wait_us += std::chrono::duration<double, std::micro>(w1 - w0).count();
         const uint8_t *rows = st->pin + (k & 1) * kX64Half;
         const size_t off = k * j->slice, rb = std::min(j->slice, j->len - off);
         const bool first = k == 0, last = k + 1 == j->nslices;
@@ -760,7 +774,12 @@ void x64_work(X64Job *j) noexcept {
         });
         if (k + 1 == j->nslices && j->out_host) std::memcpy(j->out_host, j->h_res, 8 * j->count);
         sig_store(st->hashed, want);
+        hash_us += std::chrono::duration<double, std::micro>(clk::now() - w1).count();
     }
+    if (trace)
+        fprintf(stderr, "[x64] buffers %zu slices %zu of %zu B: first copy %.0f us, copy waits %.0f us, hashing %.0f us, total %.0f us, threads %zu\n",
+                j->count, j->nslices, j->slice, first_us, wait_us, hash_us,
+                std::chrono::duration<double, std::micro>(clk::now() - t0).count(), cpu::share());
     while (!j->submitted.load(std::memory_order_acquire)) std::this_thread::yield();
     (void)hipEventSynchronize(st->done);  // the results' H2D has read h_res
     {
@@ -792,6 +811,12 @@ int x64_take_stage(int dev, X64Stage **out) {
     HIP_TRY(hipEventCreateWithFlags(&st->done, hipEventDisableTiming));
     *out = st.release();
     return 0;
+}
+
+// AWS_CRT_AMD_XXH64_ROUTE=0: every XXH64 batch on the kernels (a caller with no spare host CPUs)
+bool x64_route_wanted() {
+    const char *e = getenv("AWS_CRT_AMD_XXH64_ROUTE");
+    return !(e && e[0] == '0' && e[1] == 0);
 }
 
 // the device can order its streams on memory values (hipStreamWaitValue64); otherwise the route is off
@@ -890,7 +915,7 @@ int strided_impl(Device *d, int alg, uint64_t base, size_t stride, size_t len, s
     // buffers (stride < len, e.g. stride 0 = one buffer under several seeds) and pitches past the
     // device's 2D-copy limit stay on the kernels
     if (alg == AWS_CRT_AMD_XXH64 && count <= kX64HostMaxBuffers && len >= kX64HostMinBytes && (count == 1 || stride >= len) &&
-        x64_route_usable(d->id) &&
+        x64_route_usable(d->id) && x64_route_wanted() &&
         (count == 1 || stride <= d->max_pitch) && !capturing(s))
         return xxh64_host_route(d->id, base, count == 1 ? len : stride, len, count, d_seeds, seed_all, d_out, s);
     {

@@ -28,8 +28,42 @@ def pct(v, ps=(0, 10, 50, 90, 99, 100)):
     return [round(s[min(len(s) - 1, int(p / 100 * (len(s) - 1) + 0.5))], 2) for p in ps]
 
 
+def hw_fields(hwid):
+    """gfx9 HW_ID: wave [3:0], SIMD [5:4], CU [11:8], SH [12], SE [15:13]; XCC_ID in the high word"""
+    return {"simd": (hwid >> 4) & 3, "cu": ((hwid >> 32) & 0xF, (hwid >> 13) & 7, (hwid >> 12) & 1, (hwid >> 8) & 0xF)}
+
+
+def by_cu_order(rows, idx):
+    """the two workgroups sharing a CU: the one entering first against the second (oldest-first issue
+    would favour the first), and the spread over SIMDs"""
+    cus = {}
+    for r, i in zip(rows, idx):
+        if r[6] == 0:
+            continue
+        f = hw_fields(r[5])
+        cus.setdefault(f["cu"], {}).setdefault(i // 8, []).append(r)
+    first, second = [], []
+    for wgs in cus.values():
+        if len(wgs) != 2:
+            continue
+        a, b = sorted(wgs.values(), key=lambda ws: min(w[0] for w in ws))
+        first += [(w[4] - w[0]) * TICK_US for w in a]
+        second += [(w[4] - w[0]) * TICK_US for w in b]
+    simd = {}
+    for r in rows:
+        if r[6]:
+            simd.setdefault(hw_fields(r[5])["simd"], []).append((r[4] - r[0]) * TICK_US)
+    out = {"cus_with_two_workgroups": sum(1 for w in cus.values() if len(w) == 2),
+           "simd_mean_life_us": {k: round(statistics.mean(v), 2) for k, v in sorted(simd.items())}}
+    if first:
+        out["first_workgroup_life_us"] = pct(first)
+        out["second_workgroup_life_us"] = pct(second)
+    return out
+
+
 def analyse(st, nw):
-    rows = [st[i * W:(i + 1) * W] for i in range(nw) if st[i * W + 4] != 0]
+    idx = [i for i in range(nw) if st[i * W + 4] != 0]
+    rows = [st[i * W:(i + 1) * W] for i in idx]
     t0 = min(r[0] for r in rows)
     us = lambda t: (t - t0) * TICK_US  # noqa: E731
     entry = [us(r[0]) for r in rows]
@@ -54,7 +88,7 @@ def analyse(st, nw):
     return {"waves": len(rows), "working_waves": len(work), "groups_per_wave": pct([r[6] for r in work], (0, 50, 100)),
             "span_us": round(span, 2), "entry_us": pct(entry), "tables_us": pct(tab), "prologue_from_entry": pro, "first_group_us": pct(first),
             "per_group_us": pct(per_group), "life_us": pct(life), "mean_life_frac": round(statistics.mean(life) / span, 4),
-            "final_finish_us": pct(fin), "exit_us": pct(ex), "by_xcc": by_xcc}
+            "final_finish_us": pct(fin), "exit_us": pct(ex), "by_xcc": by_xcc, "by_cu": by_cu_order(rows, idx)}
 
 
 def main():

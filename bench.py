@@ -526,6 +526,9 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
            "value": round(gibs, 2), "unit": "GiB/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 4),
            "pct_hbm_peak": round(100.0 * gibs * 2**30 / 1e9 / HBM_PEAK_GBS, 2),
            "roofline": dict(roofline(per * step_bytes, kms, kernel_name(alg, nbuf, L)), timing_launches=timing)}
+    if alg == "xxh64":  # the host route is PCIe-bound: the link's state right after the timed launches
+        bx = box_state(torch.cuda.get_device_properties(dev))
+        rec["pcie_after"] = {"dpm": (bx.get("pcie") or {}).get("current"), "link": bx.get("link")}
     trf = pmc_traffic(alg, nbuf, L, per)
     if trf:
         rec["roofline"]["traffic"], rec["roofline"]["traffic_source"] = trf
@@ -597,9 +600,10 @@ class E2EPinned:
 
 def box_state(props):
     """The GPU's clocks and partition modes as the kernel driver reports them (sysfs of the device's
-    PCI function: pp_dpm_sclk / pp_dpm_mclk / pp_dpm_fclk with the current level marked '*', the
-    compute and memory partition modes), so that a box-to-box spread in the kernel fractions can be
-    traced to its clocks or memory mode.  Fields the box does not expose are null."""
+    PCI function: pp_dpm_sclk / pp_dpm_mclk / pp_dpm_fclk / pp_dpm_pcie with the current level marked
+    '*', the PCIe link's current speed and width, the compute and memory partition modes), so that a
+    box-to-box spread in the kernel fractions (or in the PCIe-bound XXH64 route) can be traced to its
+    clocks, link or memory mode.  Fields the box does not expose are null."""
     import glob
 
     bus = getattr(props, "pci_bus_id", None)
@@ -624,7 +628,9 @@ def box_state(props):
         return txt
 
     return {"sysfs": path, "sclk": rd("pp_dpm_sclk", True), "mclk": rd("pp_dpm_mclk", True),
-            "fclk": rd("pp_dpm_fclk", True), "compute_partition": rd("current_compute_partition"),
+            "fclk": rd("pp_dpm_fclk", True), "pcie": rd("pp_dpm_pcie", True),
+            "link": {"speed": rd("current_link_speed"), "width": rd("current_link_width")},
+            "compute_partition": rd("current_compute_partition"),
             "memory_partition": rd("current_memory_partition"),
             "power_profile": (rd("pp_power_profile_mode") or "").splitlines()[:1] or None}
 

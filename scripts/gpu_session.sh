@@ -15,6 +15,7 @@ rc=0
 for s in "$@"; do
   case $s in
     test)  step 900 $O/pytest.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest.log ;;
+    tsel)  step 600 $O/pytest_sel.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "${TESTK:-xcd}"; rc=$?; tail -3 $O/pytest_sel.log ;;
     smoke) step 180 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; tail -2 $O/smoke.log ;;
     bench) step 400 $O/bench.log python -u bench.py ${BENCH_ARGS:-}; rc=$?; tail -1 $O/bench.log ;;
     driver*) step 400 $O/$s.log python -u bench.py --gpus 1 --steps 20 --warmup 5; rc=$?; grep '^{' $O/$s.log | cut -c1-400 ;;
@@ -63,6 +64,8 @@ for s in "$@"; do
     # every config leg's kernel fraction (no CPU baseline, no host legs)
     legs)  step 400 $O/legs.log python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-batches 0; rc=$?; grep '^{' $O/legs.log | cut -c1-300 ;;
     # FETCH_SIZE of the C5 CRC64NVME launch (8 x 64 MiB, one batch per launch)
+    legsx) step 400 $O/legsx.log env AWS_CRT_AMD_X64_TRACE=1 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-batches 0; rc=$?; grep '^\[x64\]' $O/legsx.log | tail -4 ;;
+    stamps) step 180 $O/stamps.log python -u aws-crt-cpp_amd/tools/stamp_probe.py ${STAMP_REPS:-5}; rc=$?; grep -c '^{' $O/stamps.log ;;
     pmc5)  (cd /tmp && step 120 $O/pmc5_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5_fetch -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --batches 2 --coalesce 1 --steps 12 --warmup 2 --only-coalesced --branches 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
     # A/B of library builds on the C4 shard CRC64NVME launch (131072 x 8 KiB, crc64_rows16_kernel)
     abr16) step 900 $O/abr16.log env TAG=${TAG}/abr16 VARIANTS="${R16VARIANTS:-R OLD}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --alg crc64nvme --buffers 131072 --buffer-bytes 8192 --batches 2 --coalesce 1 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/abr16.log ;;

@@ -204,6 +204,28 @@ def test_xxh64_host_route_concurrent_streams(engine):
     assert results(engine, "xxh64", out) == want[0]
 
 
+def test_xxh64_config5_on_the_kernels(engine, monkeypatch):
+    """BASELINE C5's XXH64 half (8 x 64 MiB) on the GPU kernels (AWS_CRT_AMD_XXH64_ROUTE=0; by default
+    the batch takes the host route): results equal the oracle and the default route's, seeds on half
+    the buffers."""
+    import torch
+
+    n, L = 8, 64 << 20
+    d = dev_random(n * L, 0xC5)
+    rng = random.Random(0xC5)
+    seeds = [rng.getrandbits(64) if i % 2 else 0 for i in range(n)]
+    monkeypatch.setenv("AWS_CRT_AMD_XXH64_ROUTE", "0")
+    kern = engine.checksum_strided(ALG["xxh64"], d, L, L, n, seeds=seeds_tensor("xxh64", seeds))
+    torch.cuda.synchronize()
+    monkeypatch.delenv("AWS_CRT_AMD_XXH64_ROUTE")
+    route = engine.checksum_strided(ALG["xxh64"], d, L, L, n, seeds=seeds_tensor("xxh64", seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.checksum("xxh64", h[i * L:(i + 1) * L], s) for i, s in enumerate(seeds)]
+    assert results(engine, "xxh64", kern) == want
+    assert results(engine, "xxh64", route) == want
+
+
 def test_xxh64_few_long_buffers_host_route(engine):
     """Strided XXH64 batches of at most 32 buffers of >= 1 MiB take the stream-ordered host route
     (engine.cpp xxh64_host_route: D2H slices, host threads, results H2D on the caller's stream; a
@@ -357,6 +379,37 @@ def test_crc64_xcd_multi_batch(engine):
         got = engine.as_unsigned(outs[j])
         for i in range(count):
             o = (j * count + i) * L
+            assert got[i] == oracle.crc("crc64nvme", h[o:o + L], seeds[j][i] if seeds[j] else 0), (j, i)
+
+
+@pytest.mark.parametrize("count,nb", [(2048, 1), (768, 3)])
+def test_crc64_xcd_part_table_overflow(engine, count, nb):
+    """crc64_xcd_kernel joins a workgroup's parts in an LDS table of 64 buffers (round 5); a workgroup
+    meeting more buffers publishes the rest straight to the accumulators.  Overlapping 4 MiB windows
+    at a 64 KiB + 16 stride put ~256 buffers on every XCD (and ~128 in every workgroup's walk): all
+    results against the ragged-list kernel (crc64_list_stream_kernel) over the same windows, a sample
+    against the oracle; seeds on the last batch."""
+    import torch
+
+    L, stride = 256 * 16384, 65536 + 16
+    span = stride * (count - 1) + L
+    d = dev_random(nb * span + 64, 0x7AB + count)
+    rng = random.Random(count)
+    seeds = [[rng.getrandbits(64) for _ in range(count)] if j == nb - 1 else None for j in range(nb)]
+    outs = [torch.empty(count, dtype=torch.int64, device="cuda") for _ in range(nb)]
+    engine.checksum_batches(ALG["crc64nvme"], [(d.data_ptr() + j * span, seeds_tensor("crc64nvme", seeds[j]) if seeds[j] else None,
+                                                outs[j]) for j in range(nb)], stride, L, count)
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    for j in range(nb):
+        got = engine.as_unsigned(outs[j])
+        ptrs = [d.data_ptr() + j * span + i * stride for i in range(count)]
+        lst = engine.checksum_list(ALG["crc64nvme"], ptrs, [L] * count,
+                                   seeds=seeds_tensor("crc64nvme", seeds[j]) if seeds[j] else None)
+        torch.cuda.synchronize()
+        assert got == engine.as_unsigned(lst), j
+        for i in (0, 1, count // 2, count - 1):
+            o = j * span + i * stride
             assert got[i] == oracle.crc("crc64nvme", h[o:o + L], seeds[j][i] if seeds[j] else 0), (j, i)
 
 
