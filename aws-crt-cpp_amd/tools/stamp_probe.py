@@ -43,10 +43,13 @@ def by_cu_order(rows, idx):
         f = hw_fields(r[5])
         cus.setdefault(f["cu"], {}).setdefault(i // 8, []).append(r)
     first, second = [], []
+    nblocks = max(idx) // 8 + 1 if idx else 0
+    low_first = 0
     for wgs in cus.values():
         if len(wgs) != 2:
             continue
-        a, b = sorted(wgs.values(), key=lambda ws: min(w[0] for w in ws))
+        (ba, a), (bb, b) = sorted(wgs.items(), key=lambda kv: min(w[0] for w in kv[1]))
+        low_first += ba < nblocks // 2 <= bb
         first += [(w[4] - w[0]) * TICK_US for w in a]
         second += [(w[4] - w[0]) * TICK_US for w in b]
     simd = {}
@@ -54,6 +57,7 @@ def by_cu_order(rows, idx):
         if r[6]:
             simd.setdefault(hw_fields(r[5])["simd"], []).append((r[4] - r[0]) * TICK_US)
     out = {"cus_with_two_workgroups": sum(1 for w in cus.values() if len(w) == 2),
+           "first_workgroup_in_lower_half_of_grid": low_first,
            "simd_mean_life_us": {k: round(statistics.mean(v), 2) for k, v in sorted(simd.items())}}
     if first:
         out["first_workgroup_life_us"] = pct(first)
