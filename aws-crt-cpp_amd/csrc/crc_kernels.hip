@@ -325,6 +325,49 @@ __device__ __forceinline__ T mul_pcols(T r, const uint64_t *cols) {
     return acc;
 }
 
+// r * M for a wave-uniform r from M's nibble image (engine.cpp nib_image: entry 16 i + v = the product
+// of nibble i's value v): one scalar load per nibble at a data-dependent offset, all issued before one
+// wait -- one round trip for W = 32, two for W = 64 (sixteen 64-bit results at once would hold ~50
+// SGPRs), against mul_pcols' W / 8 dependent rounds (round 5: the list scans' head entries and part
+// shifts, the CRC64 part shifts)
+__device__ __forceinline__ uint32_t mul_nib32(uint32_t r, const uint32_t *img) {
+    const uint64_t a = rfl64((uint64_t)img);
+    r = __builtin_amdgcn_readfirstlane(r);
+    uint32_t o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = 64u * i + 4u * ((r >> (28 - 4 * i)) & 15u);
+    uint32_t k0, k1, k2, k3, k4, k5, k6, k7;
+    asm volatile(
+        "s_load_dword %0, %8, %9\n\ts_load_dword %1, %8, %10\n\ts_load_dword %2, %8, %11\n\ts_load_dword %3, %8, %12\n\t"
+        "s_load_dword %4, %8, %13\n\ts_load_dword %5, %8, %14\n\ts_load_dword %6, %8, %15\n\ts_load_dword %7, %8, %16\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
+        : "s"(a), "s"(o[0]), "s"(o[1]), "s"(o[2]), "s"(o[3]), "s"(o[4]), "s"(o[5]), "s"(o[6]), "s"(o[7])
+        : "memory");
+    return k0 ^ k1 ^ k2 ^ k3 ^ k4 ^ k5 ^ k6 ^ k7;
+}
+__device__ __forceinline__ uint64_t mul_nib64(uint64_t r, const uint64_t *img) {
+    const uint64_t a = rfl64((uint64_t)img);
+    r = rfl64(r);
+    uint64_t acc = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 128u * (8 * h + i) + 8u * (uint32_t)((r >> (60 - 4 * (8 * h + i))) & 15u);
+        uint64_t k0, k1, k2, k3, k4, k5, k6, k7;
+        asm volatile(
+            "s_load_dwordx2 %0, %8, %9\n\ts_load_dwordx2 %1, %8, %10\n\ts_load_dwordx2 %2, %8, %11\n\ts_load_dwordx2 %3, %8, %12\n\t"
+            "s_load_dwordx2 %4, %8, %13\n\ts_load_dwordx2 %5, %8, %14\n\ts_load_dwordx2 %6, %8, %15\n\ts_load_dwordx2 %7, %8, %16\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(k0), "=&s"(k1), "=&s"(k2), "=&s"(k3), "=&s"(k4), "=&s"(k5), "=&s"(k6), "=&s"(k7)
+            : "s"(a), "s"(o[0]), "s"(o[1]), "s"(o[2]), "s"(o[3]), "s"(o[4]), "s"(o[5]), "s"(o[6]), "s"(o[7])
+            : "memory");
+        acc ^= k0 ^ k1 ^ k2 ^ k3 ^ k4 ^ k5 ^ k6 ^ k7;
+    }
+    return acc;
+}
+
 __device__ __forceinline__ unsigned long long atomic_xor_ret(unsigned long long *a, unsigned long long v) {
     return __hip_atomic_fetch_xor(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1858,9 +1901,9 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     const uint32_t nq = (uint32_t)(sload64(wq + gw + 1) - sload64(wq + gw));  // groups of this wave
     const uint32_t lo8 = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const uint64_t *xinv = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidXinvWord);
-    const uint64_t *gsh = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGshiftWord);
-    const uint64_t *gmc = (const uint64_t *)((const uint32_t *)p.d_kvals + kBraidGmWord);
+    const uint32_t *xinv = (const uint32_t *)p.d_kvals + kBraidNibXinvWord;  // nibble images (mul_nib32)
+    const uint32_t *gsh = (const uint32_t *)p.d_kvals + kBraidNibGshiftWord;
+    const uint32_t *gmc = (const uint32_t *)p.d_kvals + kBraidNibGmWord;
     const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
     uint64_t *const jslots = (uint64_t *)(cb + (kLocalOff - kBKOff));  // 9 x {value, parts << 32 | groups}
     if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
@@ -1945,7 +1988,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (g == 0) {
             uint32_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
             const uint32_t j = (sc.pad >> 9) & 7u;
-            if (j) s_h = mul_pcols<uint32_t, 32>(s_h, xinv + 32 * j);
+            if (j) s_h = mul_nib32(s_h, xinv + 128 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
@@ -1966,10 +2009,10 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         uint32_t r = wave_xor_s(eng.mulK(u, lane));
         const uint32_t mg = sc.vg - g;  // groups after the part
         if (mg && mg < (uint32_t)kBraidGmCount) {
-            r = mul_pcols<uint32_t, 32>(r, gmc + 32 * mg);
+            r = mul_nib32(r, gmc + 128 * mg);
         } else {
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
-                if (m & 1u) r = mul_pcols<uint32_t, 32>(r, gsh + 32 * i);
+                if (m & 1u) r = mul_nib32(r, gsh + 128 * i);
         }
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;
@@ -2892,7 +2935,9 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     // the same product on the scalar unit (columns by SMEM): a part ending inside the scan (one per
     // buffer a wave leaves: multi-batch launches cross many).  One product per nonzero byte of m --
     // m < nwx, so one or two -- not one per set bit (round 4: up to twelve products of eight L2 round
-    // trips each made a 20-batch C5 launch 0.63 of the HBM peak)
+    // trips each made a 20-batch C5 launch 0.63 of the HBM peak).  (Round 5: the nibble-image product,
+    // two round trips, measured 0.5 % slower here -- 1,024 images of 2 KiB against 512-byte column
+    // sets, each product touching sixteen lines -- and is kept for the list scans.)
     auto shift_scalar = [&](uint64_t r, uint64_t m) -> uint64_t {
         for (int L = 0; m; ++L, m >>= 8)
             if (m & 255u) r = mul_pcols<uint64_t, 64>(r, bytecols + (256u * L + (m & 255u)) * 64);
@@ -2976,7 +3021,6 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     // the head state enters lane (pad mod 512) / 8 at the start of chunk 0 divided by X^jr (X = x^(8*512),
     // jr = the pad's row): that lane's words before the pad are zero, so jr row steps bring it to the head
     // state exactly where the first real word joins (crc32_list_stream_kernel's head entry)
-    const uint64_t *xinv = p.d_pcols + 256 + 40 * 64 + 4 * 256 * 64;  // [jr < 32][j]: X^(-jr) * x^j
     const uint32_t jr = pad / kB64Row, l0 = (pad % kB64Row) / 8u;
     XcdCursor sc = cur_at(c0);
     uint32_t g = 0, q = 0;
@@ -2990,7 +3034,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
                 u = 0ull;
                 if (sc.k == 0) {
                     uint64_t s_h = head_state<false>(p, sc.b, eng);
-                    if (jr) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * jr);
+                    if (jr) s_h = mul_nib64(s_h, p.d_pcols + kXcdNibXinvU64 + 256 * jr);
                     if ((uint32_t)lane == l0) u = s_h;
                 }
             }
@@ -3040,10 +3084,8 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
 // buffer end by x^(8*4096*m) for the m groups after it, and finishes the buffer or joins it through the
 // per-buffer accumulator and group count.  The tables, the nibble-table finish and the row step are
 // crc64_stream4_kernel's (4 copies, two 512-thread workgroups per CU).  Constants: ScanParams::d_pcols
-// = engine.cpp get_xcd_consts (the X^(-j) and x^(8*4096*2^i) columns).
-constexpr uint32_t kXcdXinvU64 = 256 + 40 * 64 + 4 * 256 * 64;  // get_xcd_consts: X^(-j) columns, j < 32
-constexpr uint32_t kXcdGshiftU64 = kXcdXinvU64 + 32 * 64;        // x^(8*4096*2^i) columns, i < 40
-constexpr uint32_t kXcdGmU64 = kXcdGshiftU64 + 40 * 64;            // x^(8*4096*m) columns, m < kBraidGmCount
+// = engine.cpp get_xcd_consts (the nibble images of X^(-j), x^(8*4096*2^i) and x^(8*4096*m): engine.h
+// kXcdNib*).
 
 template <uint64_t POLY>
 __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanParams p) {
@@ -3059,9 +3101,9 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     const uint32_t nq = (uint32_t)(sload64(wq + gw + 1) - sload64(wq + gw));  // groups of this wave
     const uint32_t lo8 = 8u * (uint32_t)lane;
     const uint64_t dummy = rfl64((uint64_t)p.d_kvals);
-    const uint64_t *xinv = p.d_pcols + kXcdXinvU64;
-    const uint64_t *gsh = p.d_pcols + kXcdGshiftU64;
-    const uint64_t *gmc = p.d_pcols + kXcdGmU64;
+    const uint64_t *xinv = p.d_pcols + kXcdNibXinvU64;  // nibble images (mul_nib64)
+    const uint64_t *gsh = p.d_pcols + kXcdNibGshiftU64;
+    const uint64_t *gmc = p.d_pcols + kXcdNibGmU64;
     const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
     __shared__ uint64_t jslots[2 * kListJoinSlots];   // {value, parts << 32 | groups}
     if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
@@ -3134,7 +3176,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         if (g == 0) {
             uint64_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
             const uint32_t j = (sc.pad >> 9) & 7u;
-            if (j) s_h = mul_pcols<uint64_t, 64>(s_h, xinv + 64 * j);
+            if (j) s_h = mul_nib64(s_h, xinv + 256 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
@@ -3152,10 +3194,10 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         uint64_t r = wave_xor64_s(eng.mulK(u));
         const uint32_t mg = sc.vg - g;  // groups after the part
         if (mg && mg < (uint32_t)kBraidGmCount) {
-            r = mul_pcols<uint64_t, 64>(r, gmc + 64 * mg);
+            r = mul_nib64(r, gmc + 256 * mg);
         } else {
             for (uint32_t m = mg, i = 0; m; m >>= 1, ++i)
-                if (m & 1u) r = mul_pcols<uint64_t, 64>(r, gsh + 64 * i);
+                if (m & 1u) r = mul_nib64(r, gsh + 256 * i);
         }
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;

@@ -248,6 +248,20 @@ int upload_new(DevBuf &b, const void *host, size_t bytes) {
 inline uint32_t inv_mulx32(uint32_t t, uint32_t poly) { return (t & 0x80000000u) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 inline uint64_t inv_mulx64(uint64_t t, uint64_t poly) { return (t >> 63) ? (((t ^ poly) << 1) | 1u) : (t << 1); }
 
+// Nibble image of a GF(2) matrix given by its W columns (col(j) is the product of operand bit W-1-j):
+// entry 16 i + v is the product of nibble i's value v, i.e. of bits W-1-4i .. W-4-4i (the kernels'
+// mul_nib: one scalar load per nibble, all issued together)
+template <class T, int W, class Col>
+void nib_image(T *out, Col col) {
+    for (int i = 0; i < W / 4; ++i)
+        for (int v = 0; v < 16; ++v) {
+            T e = 0;
+            for (int k = 0; k < 4; ++k)
+                if ((v >> (3 - k)) & 1) e ^= (T)col(4 * i + k);
+            out[16 * i + v] = e;
+        }
+}
+
 // W=32 braided-scan constants (layout: engine.h kBraidConstWords): the K image of x^(-32 l) (32 matrix
 // columns per lane), T' (the row step's slice-by-4 tables) and T0 (byte table)
 int get_braid_consts(Device *d, int alg, const uint64_t **out) {
@@ -312,6 +326,13 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
             }
             gm = gf2_mulmod(gm, g1, poly, 32);
         }
+        // the three sets again as nibble images (one-round-trip products, round 5)
+        for (int j = 0; j < 8; ++j)
+            nib_image<uint32_t, 32>(&c[kBraidNibXinvWord + 128 * j], [&](int k) { return c[kBraidXinvWord + 2 * (32 * j + k)]; });
+        for (int i = 0; i < 32; ++i)
+            nib_image<uint32_t, 32>(&c[kBraidNibGshiftWord + 128 * i], [&](int k) { return c[kBraidGshiftWord + 2 * (32 * i + k)]; });
+        for (int m = 0; m < kBraidGmCount; ++m)
+            nib_image<uint32_t, 32>(&c[kBraidNibGmWord + 128 * m], [&](int k) { return c[kBraidGmWord + 2 * (32 * m + k)]; });
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
@@ -346,13 +367,14 @@ int get_braid64_consts(Device *d, int alg, const uint64_t **out) {
 // jump J = x^(8 * chunk * (nwx - 1)), entry 16 n + v = (v << 4n) * J; then 40 x 64 columns of
 // x^(8 * chunk * 2^i) * x^j; then [level < 4][v < 256] x 64 columns of x^(8 * chunk * v * 256^level) * x^j
 // (a part's shift to its buffer end: a byte of the distance per product); then the list scan's X^(-j)
-// columns, x^(8*4096*2^i) columns and x^(8*4096*m) columns (m < kBraidGmCount)
+// columns, x^(8*4096*2^i) columns and x^(8*4096*m) columns (m < kBraidGmCount); then the nibble
+// images of the last three sets (engine.h kXcdNib*)
 int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
     const auto key = std::make_pair(alg, nwx);
     auto it = d->xcd.find(key);
     if (it == d->xcd.end()) {
         const uint64_t poly = alg_poly(alg);
-        std::vector<uint64_t> c(256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64, 0);
+        std::vector<uint64_t> c(kXcdConstU64, 0);
         const uint64_t J = gf2_xpow8n((uint64_t)kXcdChunkBytes * (nwx - 1), poly, 64);
         for (int n = 0; n < 16; ++n)
             for (uint64_t v = 0; v < 16; ++v) c[16 * n + v] = gf2_mulmod(v << (4 * n), J, poly, 64);
@@ -409,6 +431,16 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
             }
             gm = gf2_mulmod(gm, g1, poly, 64);
         }
+        // nibble images (256 u64 per matrix) of X^(-jr), x^(8*4096*2^i) and x^(8*4096*m): the list
+        // scan's mul_nib64 (two scalar round trips instead of eight, round 5)
+        constexpr uint64_t kXinv = 256 + 40 * 64 + 4 * 256 * 64, kGsh = kXinv + 32 * 64, kGm = kGsh + 40 * 64;
+        static_assert(kGm + kBraidGmCount * 64 == kXcdNibXinvU64, "xcd constant layout");
+        for (uint64_t m = 0; m < 32; ++m)
+            nib_image<uint64_t, 64>(&c[kXcdNibXinvU64 + 256 * m], [&](int k) { return c[kXinv + 64 * m + k]; });
+        for (uint64_t m = 0; m < 40; ++m)
+            nib_image<uint64_t, 64>(&c[kXcdNibGshiftU64 + 256 * m], [&](int k) { return c[kGsh + 64 * m + k]; });
+        for (uint64_t m = 0; m < (uint64_t)kBraidGmCount; ++m)
+            nib_image<uint64_t, 64>(&c[kXcdNibGmU64 + 256 * m], [&](int k) { return c[kGm + 64 * m + k]; });
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 8);
         if (rc) return rc;

@@ -69,6 +69,7 @@ for s in "$@"; do
     # effective shader clock per dispatch (GRBM_GUI_ACTIVE / duration): CRC64 C5 20-batch vs single, C2
     clk64) (cd /tmp && step 120 $O/clk64.log timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES --kernel-trace -d $O/clk64 -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --steps 20 --warmup 2 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
     clk32) (cd /tmp && step 120 $O/clk32.log timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES --kernel-trace -d $O/clk32 -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
+    lists) step 240 $O/lists.log bash -c "python -u aws-crt-cpp_amd/tools/list_probe.py crc32c && python -u aws-crt-cpp_amd/tools/list_probe.py crc64nvme"; rc=$?; grep '^{' $O/lists.log | cut -c1-300 ;;
     pmc5)  (cd /tmp && step 120 $O/pmc5_fetch.log timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE -d $O/pmc5_fetch -o run --output-format csv -- python3 $R/bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --batches 2 --coalesce 1 --steps 12 --warmup 2 --only-coalesced --branches 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 4); rc=$? ;;
     # A/B of library builds on the C4 shard CRC64NVME launch (131072 x 8 KiB, crc64_rows16_kernel)
     abr16) step 900 $O/abr16.log env TAG=${TAG}/abr16 VARIANTS="${R16VARIANTS:-R OLD}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --alg crc64nvme --buffers 131072 --buffer-bytes 8192 --batches 2 --coalesce 1 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/abr16.log ;;
