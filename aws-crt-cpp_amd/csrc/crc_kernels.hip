@@ -157,6 +157,13 @@ __device__ __forceinline__ Edges edges_of(uint64_t ptr, uint64_t n) {
     const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
     return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
 }
+// the list streaming scans' edges (round 5): main region [ptr rounded up to 8, end rounded down to 8) --
+// their lane words are 8 bytes, so the head and tail folds (serial byte steps) take at most 7 bytes
+// each instead of 15 (host: engine.cpp main_len8)
+__device__ __forceinline__ Edges edges8_of(uint64_t ptr, uint64_t n) {
+    const uint64_t end = ptr + n, H = (ptr + 7) & ~7ull, Ea = end & ~7ull;
+    return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
+}
 // a list buffer's address and length: both scalar loads in flight together, one wait
 __device__ __forceinline__ void list_desc(const ScanParams &p, uint64_t b, uint64_t &ptr, uint64_t &n) {
     const uint64_t pa = rfl64((uint64_t)(p.d_ptrs + b)), la = rfl64((uint64_t)(p.d_lens + b));
@@ -1832,12 +1839,12 @@ struct LBuf {        // the cursor's buffer (wave-uniform)
     uint32_t vg;     // groups (0: no main region)
     uint32_t pad;    // virtual zero bytes in front of main (< 4096)
     uint64_t ptr, n; // the buffer (its head and tail folds need no second descriptor load)
-    __device__ __forceinline__ Edges edges() const { return edges_of(ptr, n); }
+    __device__ __forceinline__ Edges edges() const { return edges8_of(ptr, n); }
 };
 __device__ __forceinline__ LBuf lbuf_at(const ScanParams &p, uint64_t b) {
     uint64_t ptr, n;
     list_desc(p, b, ptr, n);
-    const Edges e = edges_of(ptr, n);
+    const Edges e = edges8_of(ptr, n);
     const uint64_t m = e.tail - e.headend;
     const uint64_t vg = (m + kWaveGroupBytes - 1) / kWaveGroupBytes;
     const uint32_t pad = (uint32_t)(vg * kWaveGroupBytes - m);

@@ -520,6 +520,11 @@ inline uint64_t main_len(uint64_t ptr, uint64_t n) {
     const uint64_t H = (ptr + 15) & ~15ull, E = (ptr + n) & ~15ull;
     return E > H ? E - H : 0;
 }
+// the list streaming scans' main regions are 8-byte aligned (crc_kernels.hip edges8_of)
+inline uint64_t main_len8(uint64_t ptr, uint64_t n) {
+    const uint64_t H = (ptr + 7) & ~7ull, E = (ptr + n) & ~7ull;
+    return E > H ? E - H : 0;
+}
 
 // Bytes per lane per tile.  A tile is 64*seg bytes; pick the largest seg (fewest partials to
 // combine) that still gives every wavefront slot on the chip a tile and does not exceed the
@@ -1172,7 +1177,7 @@ int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
 }
 
 // Ragged CRC32 / CRC32C lists on crc32_list_stream_kernel.  Every buffer's main
-// region is front-padded to whole 4 KiB groups; the list is one sequence of groups, split evenly over
+// region (8-byte aligned: main_len8) is front-padded to whole 4 KiB groups; the list is one sequence of groups, split evenly over
 // the waves (cut anywhere, also inside a buffer).  Wave w walks buffers [wbuf[w], wbuf[w + 1]) from
 // group woff[w] of the first, scans groups [wq[w], wq[w + 1]) of the sequence and folds the buffers
 // without a main region whose place in the sequence falls in its range.  Descriptor block:
@@ -1299,8 +1304,11 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
     bool padded64 = false;
     if (width_of(alg) == 64)
         for (size_t i = 0; i < count && !padded64; ++i) padded64 = mains[i] % (kGroupBytes * kWave) != 0;
-    if (kListStream && !xxh && (width_of(alg) == 32 || (kListStream64 && padded64)))
-        return list_stream(d, alg, ptrs, lens, count, mains, total, d_seeds, d_out, s);
+    if (kListStream && !xxh && (width_of(alg) == 32 || (kListStream64 && padded64))) {
+        uint64_t total8 = 0;
+        for (size_t i = 0; i < count; ++i) total8 += (mains[i] = main_len8((uint64_t)(uintptr_t)ptrs[i], lens[i]));
+        return list_stream(d, alg, ptrs, lens, count, mains, total8, d_seeds, d_out, s);
+    }
     if (!xxh) {
         std::vector<uint64_t> sorted(mains);
         std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());

@@ -3,7 +3,7 @@ the oracle on ragged CRC64NVME lists.  The work split is test_list_partition_mod
 list's sequence of groups evenly over the waves, cut anywhere, also inside buffers); the row step, the
 lane shares and the byte tables are test_braid64_model's.  New at W = 64:
 
-  * a buffer's 16-byte-aligned main region is front-padded to whole groups with virtual zeros (the
+  * a buffer's 8-byte-aligned main region (round 5: 16 before) is front-padded to whole groups with virtual zeros (the
     kernel's buffer-resource loads return zeros there); the head state enters lane (pad mod 512) / 8
     of group 0 divided by X^j, X = x^(8 * 512), j = pad // 512 (the host's X^(-j) columns);
   * a part (a wave's groups ga..gz of one buffer) ends with the lane shares sum_l u_l K_l moved to the
@@ -43,7 +43,7 @@ def shift_bits(r, m):
 def list64_model(br, data, ptrs, lens, seeds, nw):
     edges = []
     for p, L in zip(ptrs, lens):
-        H, E = (p + 15) & ~15, (p + L) & ~15
+        H, E = (p + 7) & ~7, (p + L) & ~7
         main = E - H if E > H else 0
         vg = -(-main // GROUP)
         edges.append((H if main else p + L, main, vg, vg * GROUP - main))
