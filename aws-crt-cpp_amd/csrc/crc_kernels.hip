@@ -157,13 +157,6 @@ __device__ __forceinline__ Edges edges_of(uint64_t ptr, uint64_t n) {
     const uint64_t end = ptr + n, H = (ptr + 15) & ~15ull, Ea = end & ~15ull;
     return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
 }
-// the list streaming scans' edges (round 5): main region [ptr rounded up to 8, end rounded down to 8) --
-// their lane words are 8 bytes, so the head and tail folds (serial byte steps) take at most 7 bytes
-// each instead of 15 (host: engine.cpp main_len8)
-__device__ __forceinline__ Edges edges8_of(uint64_t ptr, uint64_t n) {
-    const uint64_t end = ptr + n, H = (ptr + 7) & ~7ull, Ea = end & ~7ull;
-    return Ea > H ? Edges{ptr, H, Ea, end} : Edges{ptr, end, end, end};
-}
 // a list buffer's address and length: both scalar loads in flight together, one wait
 __device__ __forceinline__ void list_desc(const ScanParams &p, uint64_t b, uint64_t &ptr, uint64_t &n) {
     const uint64_t pa = rfl64((uint64_t)(p.d_ptrs + b)), la = rfl64((uint64_t)(p.d_lens + b));
@@ -1833,22 +1826,45 @@ __device__ __forceinline__ void list_join(uint64_t *slot, uint32_t d, T r, uint3
     done(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), (uint32_t)now);
 }
 
+// The list streaming scans' buffers (round 5): a buffer of at least kListMainMin bytes is scanned as the
+// 8-byte words [ptr & ~7, end & ~7) -- no serial head fold.  The o = ptr & 7 bytes in front of it in its
+// first word are not the buffer's: the scan clears them in the registers (list_mask_edges) and the head
+// state enters divided by x^(8 o), so it reaches ~seed exactly at ptr.  The tail (< 8 bytes) is folded.
+// (Masking the last word too -- [ptr & ~7, (end + 7) & ~7), the register leaving times x^(-8 k) -- made
+// unaligned 64 KiB buffers one 4 KiB group longer, 2 us per 256 MiB list slower; the code keeps the
+// k path for it.)  A shorter buffer has no main region and is folded whole (engine.cpp main_len_list).
+constexpr uint64_t kListMainMin = 16;
 struct LBuf {        // the cursor's buffer (wave-uniform)
     uint64_t b;      // buffer index
     uint64_t vb;     // virtual start of group 0 (main start - pad)
     uint32_t vg;     // groups (0: no main region)
     uint32_t pad;    // virtual zero bytes in front of main (< 4096)
-    uint64_t ptr, n; // the buffer (its head and tail folds need no second descriptor load)
-    __device__ __forceinline__ Edges edges() const { return edges8_of(ptr, n); }
+    uint64_t ptr, n; // the buffer
+    uint32_t o, k;   // bytes of the first / last main word outside the buffer
+    __device__ __forceinline__ Edges edges() const {  // the tail (< 8 bytes), or a whole short buffer, is folded
+        return vg ? Edges{ptr, ptr, (ptr + n) & ~7ull, ptr + n} : Edges{ptr, ptr + n, ptr + n, ptr + n};
+    }
 };
 __device__ __forceinline__ LBuf lbuf_at(const ScanParams &p, uint64_t b) {
     uint64_t ptr, n;
     list_desc(p, b, ptr, n);
-    const Edges e = edges8_of(ptr, n);
-    const uint64_t m = e.tail - e.headend;
+    if (n < kListMainMin) return LBuf{b, 0, 0, 0, ptr, n, 0, 0};
+    const uint64_t m0 = ptr & ~7ull, m1 = (ptr + n) & ~7ull, m = m1 - m0;
     const uint64_t vg = (m + kWaveGroupBytes - 1) / kWaveGroupBytes;
     const uint32_t pad = (uint32_t)(vg * kWaveGroupBytes - m);
-    return LBuf{b, e.headend - pad, (uint32_t)vg, pad, ptr, n};
+    return LBuf{b, m0 - pad, (uint32_t)vg, pad, ptr, n, (uint32_t)(ptr - m0), 0u};
+}
+// clears the bytes outside the buffer in its first word (group 0, row pad / 512, lane (pad mod 512) / 8)
+// and its last word (the last group's row 7, lane 63); only in those two groups (wave-uniform test)
+template <class G>
+__device__ __forceinline__ void list_mask_edges(G &cur, uint32_t g, const LBuf &sc, int lane) {
+    const bool head = g == 0 && sc.o, tail = g + 1 == sc.vg && sc.k;
+    if (!head && !tail) return;
+    const uint32_t jh = (sc.pad >> 9) & 7u, lh = (sc.pad & 511u) >> 3;
+    const uint64_t mh = head && (uint32_t)lane == lh ? ~0ull << (8 * sc.o) : ~0ull;
+    const uint64_t mt = tail && lane == 63 ? ~0ull >> (8 * sc.k) : ~0ull;
+#pragma unroll
+    for (int R = 0; R < 8; ++R) cur.w[R] &= ((uint32_t)R == jh ? mh : ~0ull) & (R == 7 ? mt : ~0ull);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint64_t base, uint32_t nrec) {
@@ -1911,13 +1927,14 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     const uint32_t *xinv = (const uint32_t *)p.d_kvals + kBraidNibXinvWord;  // nibble images (mul_nib32)
     const uint32_t *gsh = (const uint32_t *)p.d_kvals + kBraidNibGshiftWord;
     const uint32_t *gmc = (const uint32_t *)p.d_kvals + kBraidNibGmWord;
+    const uint32_t *xneg = (const uint32_t *)p.d_kvals + kBraidNibXneg8Word;  // x^(-8 t), t < 8
     const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
     uint64_t *const jslots = (uint64_t *)(cb + (kLocalOff - kBKOff));  // 9 x {value, parts << 32 | groups}
     if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;  // b0 < nbuf then (the host's wbuf is nbuf only past the groups)
-    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0, 0, 0};
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{};
     uint32_t fq = 0, fg = g0;
     if (nq)
         while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
@@ -1988,16 +2005,22 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         return;
     }
     uint32_t g = g0, ga = g0, u = 0, q = 0;
-    // a part's first group: the head state (group 0) enters its lane, divided by X^j
+    // a part's first group: the head state (group 0) enters its lane, divided by x^(8 o) and X^j
     auto part_begin = [&]() {
         ga = g;
         u = 0;
         if (g == 0) {
             uint32_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
+            if (sc.o) s_h = mul_nib32(s_h, xneg + 128 * sc.o);
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_nib32(s_h, xinv + 128 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
+    };
+    // the buffer's register at the end of its main words -> at its end (x^(-8 k)) -> stored (lane 0)
+    auto finish = [&](uint32_t r) {
+        if (sc.k) r = mul_nib32(r, xneg + 128 * sc.k);
+        finalize_e<true>(p, sc.b, sc.edges(), r, eng);
     };
     // value r of n groups of a buffer of vg groups into its accumulator; the part completing the count
     // finishes it (lane 0)
@@ -2007,7 +2030,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         if (c + n == vg) {
             const uint32_t fin = (uint32_t)sx_swap64_ret(&p.d_acc[b], 0ull);
             sx_store32(&p.d_cnt[b], 0u);
-            finalize_e<true>(p, b, sc.edges(), fin, eng);  // (b is sc.b at every call)
+            finish(fin);  // (b is sc.b at every call)
         }
     };
     uint32_t nparts = 0;  // parts this wave has finished
@@ -2024,7 +2047,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;
         if (ga == 0 && g == sc.vg) {
-            if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), r, eng);
+            if (lane == 0) finish(r);
             return;
         }
         if (lane != 0) return;
@@ -2036,7 +2059,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             if (d & 0x100u)
                 publish(sc.b, (uint32_t)v, groups, sc.vg);
             else
-                finalize_e<true>(p, sc.b, sc.edges(), (uint32_t)v, eng);
+                finish((uint32_t)v);
         });
     };
     part_begin();
@@ -2044,6 +2067,7 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
         const __amdgpu_buffer_rsrc_t rs = f_rsrc();
         const uint32_t fo = f_off(), fl = f_lim();
         f_next();
+        list_mask_edges(cur, g, sc, lane);
         u = list_rows_w8<0, B>(u, typename B::Hi{}, cur, nxt, rs, fo, fl, eng);
         if (first) publish_consts();
         ++q;
@@ -3111,13 +3135,14 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     const uint64_t *xinv = p.d_pcols + kXcdNibXinvU64;  // nibble images (mul_nib64)
     const uint64_t *gsh = p.d_pcols + kXcdNibGshiftU64;
     const uint64_t *gmc = p.d_pcols + kXcdNibGmU64;
+    const uint64_t *xneg = p.d_pcols + kXcdNibXneg8U64;  // x^(-8 t), t < 8
     const uint64_t jd = sload64(wq + (nw + 1) + gw);  // join descriptors of the first and last parts
     __shared__ uint64_t jslots[2 * kListJoinSlots];   // {value, parts << 32 | groups}
     if (threadIdx.x < 2 * kListJoinSlots) jslots[threadIdx.x] = 0;
 
     // prefetch cursor: buffer fc, group fg; it skips buffers without a main region (nq groups ahead)
     const bool owns = b0 < b_end || nq;
-    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{0, 0, 0, 0, 0, 0};
+    LBuf fc = owns ? lbuf_at(p, b0) : LBuf{};
     uint32_t fq = 0, fg = g0;
     if (nq)
         while (fc.vg == 0) fc = lbuf_at(p, fc.b + 1), fg = 0;
@@ -3182,10 +3207,15 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         u = 0;
         if (g == 0) {
             uint64_t s_h = head_state_e<true>(p, sc.b, sc.edges(), eng);
+            if (sc.o) s_h = mul_nib64(s_h, xneg + 256 * sc.o);
             const uint32_t j = (sc.pad >> 9) & 7u;
             if (j) s_h = mul_nib64(s_h, xinv + 256 * j);
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
+    };
+    auto finish = [&](uint64_t r) {  // at the end of the main words -> at the buffer's end -> stored
+        if (sc.k) r = mul_nib64(r, xneg + 256 * sc.k);
+        finalize_e<true>(p, sc.b, sc.edges(), r, eng);
     };
     auto publish = [&](uint64_t b, uint64_t r, uint32_t n, uint32_t vg) {  // lane 0
         (void)sx_xor64_ret(&p.d_acc[b], (unsigned long long)r);  // performed before it is counted
@@ -3193,7 +3223,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         if (c + n == vg) {
             const uint64_t fin = sx_swap64_ret(&p.d_acc[b], 0ull);
             sx_store32(&p.d_cnt[b], 0u);
-            finalize_e<true>(p, b, sc.edges(), fin, eng);  // (b is sc.b at every call)
+            finish(fin);  // (b is sc.b at every call)
         }
     };
     uint32_t nparts = 0;  // parts this wave has finished
@@ -3209,7 +3239,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         const uint32_t d = (uint32_t)(nparts == 0 ? jd : jd >> 16) & 0xffffu;
         ++nparts;
         if (ga == 0 && g == sc.vg) {
-            if (lane == 0) finalize_e<true>(p, sc.b, sc.edges(), r, eng);
+            if (lane == 0) finish(r);
             return;
         }
         if (lane != 0) return;
@@ -3222,7 +3252,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             if (d & 0x100u)
                 publish(sc.b, v, groups, sc.vg);
             else
-                finalize_e<true>(p, sc.b, sc.edges(), v, eng);
+                finish(v);
         });
     };
     part_begin();
@@ -3230,6 +3260,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
         const __amdgpu_buffer_rsrc_t rs = f_rsrc();
         const uint32_t fo = f_off(), fl = f_lim();
         f_next();
+        list_mask_edges(cur, g, sc, lane);
         u = xcd_rows<0>(u, cur, nxt, rs, fo, fl, eng);
         ++q;
         if (++g == sc.vg || q == nq) {

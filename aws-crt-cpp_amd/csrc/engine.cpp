@@ -333,6 +333,17 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
             nib_image<uint32_t, 32>(&c[kBraidNibGshiftWord + 128 * i], [&](int k) { return c[kBraidGshiftWord + 2 * (32 * i + k)]; });
         for (int m = 0; m < kBraidGmCount; ++m)
             nib_image<uint32_t, 32>(&c[kBraidNibGmWord + 128 * m], [&](int k) { return c[kBraidGmWord + 2 * (32 * m + k)]; });
+        // x^(-8 t), t < 8: the list scans' masked edges (crc_kernels.hip lbuf_at)
+        uint32_t xn = 0x80000000u;  // x^0, then x^(-8 t)
+        for (int t = 0; t < 8; ++t) {
+            const uint32_t base = xn;
+            nib_image<uint32_t, 32>(&c[kBraidNibXneg8Word + 128 * t], [&](int k) {
+                uint32_t col = base;
+                for (int i = 0; i < k; ++i) col = (uint32_t)gf2_mulx(col, poly);
+                return col;
+            });
+            for (int i = 0; i < 8; ++i) xn = inv_mulx32(xn, poly);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 4);
         if (rc) return rc;
@@ -441,6 +452,16 @@ int get_xcd_consts(Device *d, int alg, uint64_t nwx, const uint64_t **out) {
             nib_image<uint64_t, 64>(&c[kXcdNibGshiftU64 + 256 * m], [&](int k) { return c[kGsh + 64 * m + k]; });
         for (uint64_t m = 0; m < (uint64_t)kBraidGmCount; ++m)
             nib_image<uint64_t, 64>(&c[kXcdNibGmU64 + 256 * m], [&](int k) { return c[kGm + 64 * m + k]; });
+        uint64_t xn = 1ull << 63;  // x^0, then x^(-8 t), t < 8: the list scan's masked edges
+        for (int t = 0; t < 8; ++t) {
+            const uint64_t base = xn;
+            nib_image<uint64_t, 64>(&c[kXcdNibXneg8U64 + 256 * t], [&](int k) {
+                uint64_t col = base;
+                for (int i = 0; i < k; ++i) col = gf2_mulx(col, poly);
+                return col;
+            });
+            for (int i = 0; i < 8; ++i) xn = inv_mulx64(xn, poly);
+        }
         DevBuf b;
         int rc = upload_new(b, c.data(), c.size() * 8);
         if (rc) return rc;
@@ -520,10 +541,10 @@ inline uint64_t main_len(uint64_t ptr, uint64_t n) {
     const uint64_t H = (ptr + 15) & ~15ull, E = (ptr + n) & ~15ull;
     return E > H ? E - H : 0;
 }
-// the list streaming scans' main regions are 8-byte aligned (crc_kernels.hip edges8_of)
-inline uint64_t main_len8(uint64_t ptr, uint64_t n) {
-    const uint64_t H = (ptr + 7) & ~7ull, E = (ptr + n) & ~7ull;
-    return E > H ? E - H : 0;
+// the list streaming scans' main regions: a buffer of >= 16 bytes as the 8-byte words [ptr & ~7, end & ~7)
+// (crc_kernels.hip lbuf_at: the bytes in front of ptr are masked in the registers)
+inline uint64_t main_len_list(uint64_t ptr, uint64_t n) {
+    return n >= 16 ? ((ptr + n) & ~7ull) - (ptr & ~7ull) : 0;
 }
 
 // Bytes per lane per tile.  A tile is 64*seg bytes; pick the largest seg (fewest partials to
@@ -1177,7 +1198,7 @@ int stage_end(Device *d, hipStream_t s, size_t bytes, const void **dev) {
 }
 
 // Ragged CRC32 / CRC32C lists on crc32_list_stream_kernel.  Every buffer's main
-// region (8-byte aligned: main_len8) is front-padded to whole 4 KiB groups; the list is one sequence of groups, split evenly over
+// region (the 8-byte words covering it: main_len_list) is front-padded to whole 4 KiB groups; the list is one sequence of groups, split evenly over
 // the waves (cut anywhere, also inside a buffer).  Wave w walks buffers [wbuf[w], wbuf[w + 1]) from
 // group woff[w] of the first, scans groups [wq[w], wq[w + 1]) of the sequence and folds the buffers
 // without a main region whose place in the sequence falls in its range.  Descriptor block:
@@ -1306,7 +1327,7 @@ int list_impl(Device *d, int alg, const void *const *ptrs, const size_t *lens, s
         for (size_t i = 0; i < count && !padded64; ++i) padded64 = mains[i] % (kGroupBytes * kWave) != 0;
     if (kListStream && !xxh && (width_of(alg) == 32 || (kListStream64 && padded64))) {
         uint64_t total8 = 0;
-        for (size_t i = 0; i < count; ++i) total8 += (mains[i] = main_len8((uint64_t)(uintptr_t)ptrs[i], lens[i]));
+        for (size_t i = 0; i < count; ++i) total8 += (mains[i] = main_len_list((uint64_t)(uintptr_t)ptrs[i], lens[i]));
         return list_stream(d, alg, ptrs, lens, count, mains, total8, d_seeds, d_out, s);
     }
     if (!xxh) {

@@ -121,14 +121,16 @@ struct ScanParams {
 //                 entry (crc32_list_stream_kernel)
 //   [7936, 9984)  columns (u64) of x^(8*4096*2^i), i < 32: the list streaming scan's part shifts
 //   [9984, 14080) columns (u64) of x^(8*4096*m), m < 64: the same shifts in one product (round 4)
-//   [14080, 27392) round 5: the same three matrix sets as nibble images (u32), 128 words per matrix:
+//   [14080, 27392) round 5: the same three matrix sets as nibble images (u32), 128 words per matrix,
+//                 then [27392, 28416) the images of x^(-8 t), t < 8:
 //                 word 16 i + v = the product of nibble i's value v (bits 31-4i .. 28-4i of the
 //                 operand) -- a product is then 8 independent scalar loads, one round trip
 //                 (crc_kernels.hip mul_nib), against 4 dependent rounds of 8 columns (mul_pcols)
 constexpr int kShardBlocks = 8;        // workgroups per dynamic-pool shard (one per XCD under round-robin dispatch)
 constexpr int kBraidRow = 256;        // bytes per row: 64 lanes x one 4-byte word
 constexpr int kBraidRowsPerGroup = 16; // 4 KiB per wave per prefetch group
-constexpr int kBraidConstWords = 27392;
+constexpr int kBraidConstWords = 28416;
+constexpr int kBraidNibXneg8Word = 27392;   // nibble images of x^(-8 t), t < 8 (the list scans' masked edges)
 constexpr int kBraidNibXinvWord = 14080;    // nibble images of the X^(-j) matrices, j < 8
 constexpr int kBraidNibGshiftWord = 15104;  // nibble images of x^(8*4096*2^i), i < 32
 constexpr int kBraidNibGmWord = 19200;      // nibble images of x^(8*4096*m), m < kBraidGmCount
@@ -141,7 +143,8 @@ constexpr int kBraidGmCount = 64;
 constexpr uint64_t kXcdNibXinvU64 = 256 + 40 * 64 + 4 * 256 * 64 + 32 * 64 + 40 * 64 + kBraidGmCount * 64;
 constexpr uint64_t kXcdNibGshiftU64 = kXcdNibXinvU64 + 32 * 256;
 constexpr uint64_t kXcdNibGmU64 = kXcdNibGshiftU64 + 40 * 256;
-constexpr uint64_t kXcdConstU64 = kXcdNibGmU64 + kBraidGmCount * 256;
+constexpr uint64_t kXcdNibXneg8U64 = kXcdNibGmU64 + kBraidGmCount * 256;
+constexpr uint64_t kXcdConstU64 = kXcdNibXneg8U64 + 8 * 256;
 constexpr int kBraidK64Word = 3328;   // first word of the x^(-64 l) K image
 constexpr int kBraidK128Word = 5376;  // first word of the x^(-128 l) K image
 

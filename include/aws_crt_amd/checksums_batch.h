@@ -65,6 +65,9 @@ enum aws_crt_amd_status {
  * staged through the gfx950 kernels.  A GPU failure falls back to the host path in every mode and
  * is counted by aws_crt_amd_fallback_count().  Initial value from the environment variable
  * AWS_CRT_AMD_DISPATCH=auto|cpu|gpu.
+ * Memory kept: in GPU mode an xxHash of a host buffer stages the whole buffer in HBM; the staging
+ * buffer is cached per device up to 64 MiB (larger hashes use a temporary allocation), so at most
+ * 64 MiB of HBM per device stays allocated for the life of the process.
  */
 enum aws_crt_amd_dispatch {
     AWS_CRT_AMD_DISPATCH_AUTO = 0,

@@ -528,6 +528,37 @@ def test_ragged_list_workgroup_joins(engine, alg, nbuf, lo, hi):
     assert results(engine, alg, out) == want
 
 
+@pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
+def test_list_masked_edges(engine, alg):
+    """Round 5: the list streaming scans read a buffer of >= 16 bytes as the 8-byte words covering it
+    and clear the bytes outside it in the registers (the head state enters times x^(-8 o), the
+    register leaves times x^(-8 k)).  Every start offset mod 8 against lengths at the threshold
+    (15, 16, 17), around one and two words, around a 4 KiB group and a 512-byte row, neighbours
+    packed with no gap (the masked bytes are the neighbours' data), one 1 MiB buffer so that the
+    list takes the streaming scan; seeds on all."""
+    import torch
+
+    rng = random.Random(0x3A5C + ALG[alg])
+    base_lens = [15, 16, 17, 23, 24, 25, 31, 511, 512, 513, 4095, 4096, 4097, 4103, 8191, 12289]
+    lens, offs, pos = [], [], 3
+    for L in base_lens:
+        for o in range(8):
+            pos += (o - pos) % 8  # start at offset o mod 8, right after the previous buffer
+            offs.append(pos)
+            lens.append(L)
+            pos += L
+    offs.append(pos + 5)
+    lens.append(1 << 20)
+    pos += 5 + (1 << 20)
+    d = dev_random(pos + 64, 0x3A5C)
+    seeds = [rng.getrandbits(64 if alg in W64 else 32) for _ in lens]
+    out = engine.checksum_list(ALG[alg], [d.data_ptr() + o for o in offs], lens, seeds=seeds_tensor(alg, seeds))
+    torch.cuda.synchronize()
+    h = host_bytes(d)
+    want = [oracle.crc(alg, h[o: o + ln], s) for o, ln, s in zip(offs, lens, seeds)]
+    assert results(engine, alg, out) == want
+
+
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme", "xxh64", "xxh3_64", "xxh3_128"])
 def test_fuzz_lengths_alignments_seeds(engine, alg):
     """GPU-vs-oracle differential fuzzing: 2000 buffers of uniformly random length

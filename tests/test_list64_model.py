@@ -3,7 +3,7 @@ the oracle on ragged CRC64NVME lists.  The work split is test_list_partition_mod
 list's sequence of groups evenly over the waves, cut anywhere, also inside buffers); the row step, the
 lane shares and the byte tables are test_braid64_model's.  New at W = 64:
 
-  * a buffer's 8-byte-aligned main region (round 5: 16 before) is front-padded to whole groups with virtual zeros (the
+  * a buffer's main region (round 5: the 8-byte words covering it, bytes outside it masked) is front-padded to whole groups with virtual zeros (the
     kernel's buffer-resource loads return zeros there); the head state enters lane (pad mod 512) / 8
     of group 0 divided by X^j, X = x^(8 * 512), j = pad // 512 (the host's X^(-j) columns);
   * a part (a wave's groups ga..gz of one buffer) ends with the lane shares sum_l u_l K_l moved to the
@@ -40,24 +40,41 @@ def shift_bits(r, m):
     return r
 
 
+def xneg8(s, t):
+    """s * x^(-8 t)"""
+    for _ in range(8 * t):
+        s = inv_mulx(s)
+    return s
+
+
 def list64_model(br, data, ptrs, lens, seeds, nw):
+    # round 5: a buffer of >= 16 bytes is scanned as the 8-byte words [p & ~7, end & ~7); the o bytes in
+    # front are cleared (the kernel masks its registers) and the head state enters times x^(-8 o); the
+    # tail (< 8 bytes) is folded; shorter buffers fold whole
     edges = []
     for p, L in zip(ptrs, lens):
-        H, E = (p + 7) & ~7, (p + L) & ~7
-        main = E - H if E > H else 0
+        if L >= 16:
+            H, E = p & ~7, (p + L) & ~7
+            main = E - H
+        else:
+            H, main = p + L, 0
         vg = -(-main // GROUP)
-        edges.append((H if main else p + L, main, vg, vg * GROUP - main))
+        edges.append((H, main, vg, vg * GROUP - main))
     groups = [e[2] for e in edges]
     acc = [0] * len(ptrs)
     cnt = [0] * len(ptrs)
     out = [None] * len(ptrs)
 
     def head_state(b):
-        return br.bytes_(~seeds[b] & M64, data[ptrs[b]: edges[b][0]])
+        if edges[b][1]:
+            return xneg8(~seeds[b] & M64, ptrs[b] - edges[b][0])
+        return br.bytes_(~seeds[b] & M64, data[ptrs[b]: ptrs[b] + lens[b]])
 
     def finalize(b, s):
         H, main = edges[b][0], edges[b][1]
-        out[b] = ~br.bytes_(s, data[H + main: ptrs[b] + lens[b]]) & M64
+        if main:
+            s = br.bytes_(s, data[H + main: ptrs[b] + lens[b]])
+        out[b] = ~s & M64
 
     wbuf, woff, wq = host_split(groups, nw)
     for w in range(nw):
@@ -77,7 +94,10 @@ def list64_model(br, data, ptrs, lens, seeds, nw):
                 for row in range(ROWS):
                     for lane in range(64):
                         a = base + ROW * row + 8 * lane
-                        wd = int.from_bytes(data[a: a + 8], "little") if a >= H else 0
+                        wd = 0
+                        if a >= H:  # the buffer's own bytes only (the kernel's masks)
+                            p, e = ptrs[b], ptrs[b] + lens[b]
+                            wd = int.from_bytes(bytes(data[x] if p <= x < e else 0 for x in range(a, a + 8)), "little")
                         u[lane] = br.step(u[lane] ^ wd)
             r = 0
             for lane in range(64):
@@ -116,7 +136,7 @@ def test_list64_walk_matches_oracle(br, seed):
     for L in lens:
         ptrs.append(off)
         off += L + rng.randrange(24)
-    data = bytes(rng.getrandbits(8) for _ in range(off + 16))
+    data = bytes(rng.getrandbits(8) for _ in range(off + 24))
     seeds = [rng.getrandbits(64) for _ in range(count)]
     nw = rng.choice([1, 2, 3, 7])
     got = list64_model(br, data, ptrs, lens, seeds, nw)
