@@ -245,6 +245,7 @@ class BatchSet:
         # written by it
         self._keep = [t for b in batches for t in b if hasattr(t, "data_ptr")]
         self._cuda = [t for t in self._keep if getattr(t, "is_cuda", False)]
+        self._recorded = set()  # streams the tensors are already recorded on
         arr = (_Batch * max(self.n, 1))()
         for i, (base, seeds, out) in enumerate(batches):
             arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
@@ -268,11 +269,14 @@ class BatchSet:
         rc = self.fn(self._plan, _stream_handle(stream))
         if rc != 0:
             _check(rc)
-        if self._cuda and stream is not None and hasattr(stream, "cuda_stream"):
+        if self._cuda and stream is not None and hasattr(stream, "cuda_stream") and stream.cuda_stream not in self._recorded:
             # a launch on a side stream: the caching allocator must not hand these blocks out again
-            # before that stream has finished with them
+            # before that stream has finished with them.  Once per stream: the allocator waits for every
+            # recorded stream when the block is freed, so recording it again per launch only costs host
+            # time between launches
             for t in self._cuda:
                 t.record_stream(stream)
+            self._recorded.add(stream.cuda_stream)
 
     def __del__(self):
         if getattr(self, "_plan", None):

@@ -400,6 +400,7 @@ constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 // streaming scans: workgroup-local buffer slots (tile registers of buffers whose tiles all lie in one
 // workgroup's range are combined with LDS atomics instead of device-scope ones)
 constexpr uint32_t kLocalSlots = 128;
+static_assert(kLocalSlots == kStreamLocalSlots, "engine.cpp stream_local_only mirrors the slot count");
 constexpr uint32_t kLocalOff = kBraidLds;
 constexpr uint32_t kStreamLds = kLocalOff + 8 * kLocalSlots;
 constexpr int kBraidBlock = 512;                      // 8 waves; two workgroups per CU

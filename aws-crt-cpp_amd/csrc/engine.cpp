@@ -672,6 +672,22 @@ int launch_hash(int alg, XxhParams &xp, hipStream_t s) {
 // log2(v) + 1 when v is a power of two, else 0 (ScanParams::shifts1)
 uint8_t pow2_shift1(uint64_t v) { return v && (v & (v - 1)) == 0 ? (uint8_t)(__builtin_ctzll(v) + 1) : (uint8_t)0; }
 
+// crc32_stream_kernel needs no per-stream workspace when every buffer lies wholly inside one workgroup's
+// tiles and that workgroup combines it in LDS (crc_kernels.hip LocalBufs: T <= 32, at most kLocalSlots
+// whole buffers per workgroup): the C2 shapes, one batch or twenty.  The launch then takes no stream
+// state, so it records no fence event behind itself (round 5: one runtime call less per launch, the
+// cost that bounds one-batch-per-launch submission).
+bool stream_local_only(const ScanParams &p, uint64_t blocks) {
+    const uint64_t T = p.tiles_per_buf, nw = blocks * 8;
+    if (T < 2 || T > 32 || p.nstatic || p.xcd_order || p.list_mode) return false;
+    auto split_at = [&](uint64_t w) { return w * p.split_q + std::min<uint64_t>(w, p.split_r); };
+    for (uint64_t b = 0; b < blocks; ++b) {
+        const uint64_t t0 = split_at(8 * b), t1 = split_at(std::min(8 * b + 8, nw));
+        if (t0 % T || t1 % T || (t1 - t0) / T > kStreamLocalSlots) return false;
+    }
+    return true;
+}
+
 int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax, uint64_t total_main, hipStream_t s) {
     const uint64_t tile = (uint64_t)p.seg * kWave;
     int rc = width_of(alg) == 32 ? get_braid_consts(d, alg, &p.d_kvals) : get_braid64_consts(d, alg, &p.d_kvals);
@@ -683,12 +699,25 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     p.d_acc1 = nullptr;
     p.d_cnt1 = nullptr;
     p.d_claim = nullptr;
+    const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
+    uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
+    if (p.stream == 3) blocks = std::min<uint64_t>((p.nbuf + 4 * 8 - 1) / (4 * 8), 2 * (uint64_t)d->cus);  // 4 buffers per wave
+    if (p.list_mode && p.stream == 4) blocks = list_stream_blocks(d, p.ntiles, total_main);  // the waves list_stream split for
+    if (blocks == 0) return 0;
+    // crc32_stream_kernel's static split (ScanParams::split_q), now that the grid is known
+    const bool stream32 = width_of(alg) == 32 && p.stream == 1 && !p.list_mode;
+    if (stream32) {
+        const uint64_t nw = blocks * 8;
+        p.split_q = p.ntiles / nw;
+        p.split_r = (uint32_t)(p.ntiles % nw);
+        p.shifts1 = (p.shifts1 & ~0xFFu) | pow2_shift1(p.tiles_per_buf);
+    }
     bool ws = false;
     if (tmax > 1 || p.nstatic) {
         if ((rc = get_pcols(d, alg, tile, tmax, s, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
-        ws = true;
-        if (!t_plan) {
+        ws = !(stream32 && stream_local_only(p, blocks));
+        if (ws && !t_plan) {
             Workspace *w;
             if ((rc = get_workspace(d, s, nbuf, p.ntiles, &w))) return rc;
             p.d_acc = w->acc;
@@ -698,20 +727,8 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
             p.d_claim = w->claim;
         }
     }
-    const bool w64_half = width_of(alg) == 64 && p.stream;  // crc64_stream4_kernel
-    uint64_t blocks = scan_geometry(d, alg, p.ntiles, total_main, w64_half, p.stream == 2).blocks;
-    if (p.stream == 3) blocks = std::min<uint64_t>((p.nbuf + 4 * 8 - 1) / (4 * 8), 2 * (uint64_t)d->cus);  // 4 buffers per wave
-    if (p.list_mode && p.stream == 4) blocks = list_stream_blocks(d, p.ntiles, total_main);  // the waves list_stream split for
-    if (blocks == 0) return 0;
     // crc64_list_stream_kernel: the head-entry and part-shift columns
     if (p.list_mode && p.stream == 4 && width_of(alg) == 64 && (rc = get_xcd_consts(d, alg, 512, &p.d_pcols))) return rc;
-    // crc32_stream_kernel's static split (ScanParams::split_q), now that the grid is known
-    if (width_of(alg) == 32 && p.stream == 1 && !p.list_mode) {
-        const uint64_t nw = blocks * 8;
-        p.split_q = p.ntiles / nw;
-        p.split_r = (uint32_t)(p.ntiles % nw);
-        p.shifts1 = (p.shifts1 & ~0xFFu) | pow2_shift1(p.tiles_per_buf);
-    }
     if (t_plan) {
         PlannedLaunch pl;
         pl.alg = alg, pl.p = p, pl.blocks = blocks, pl.ws = ws, pl.ws_nbuf = nbuf, pl.ws_tiles = p.ntiles;

@@ -38,6 +38,7 @@ constexpr uint64_t kXcdChunkBytes = (uint64_t)AMDCRC_XCD_CHUNK_GROUPS * 4096;
 #endif
 constexpr int kXcdBlock = AMDCRC_XCD_BLOCK;
 constexpr int kMaxBatches = 32;  // batches per strided launch (kernel arguments, 768 bytes)
+constexpr uint64_t kStreamLocalSlots = 128;  // crc32_stream_kernel: LDS slots for a workgroup's whole buffers
 
 // The 16-byte-word CRC32 streaming scan (crc_kernels.hip Braid32W16: slice-by-16 rows, one
 // global_load_dwordx4 per lane per row, one 1024-thread workgroup per CU) for launches of >= 256 MiB.
