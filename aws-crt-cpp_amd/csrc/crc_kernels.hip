@@ -399,6 +399,25 @@ constexpr uint32_t kPoolOff = kConstFlagOff + 4;      // workgroup tile pool: ti
 constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 // streaming scans: workgroup-local buffer slots (tile registers of buffers whose tiles all lie in one
 // workgroup's range are combined with LDS atomics instead of device-scope ones)
+#ifndef AMDCRC_STREAM_PRIO  // compile-time only (A/B builds): crc32_stream_kernel issue priority by work left
+#define AMDCRC_STREAM_PRIO 1
+#endif
+#ifndef AMDCRC_PRIO_ALL  // compile-time only (A/B builds): the same in the CRC64 and list scans
+#define AMDCRC_PRIO_ALL 0
+#endif
+// Issue priority by the work a wave has left (round 5).  Two workgroups share a CU and the one
+// dispatched first is served first (oldest-first issue): its waves finished a 20-batch C2 launch at
+// ~144 us, the second workgroup's at ~190 us of ~200 (per-wave stamps), the launch's last 25 % running
+// on half the waves.  Every fourth group a wave sets s_setprio to (groups left * 4 / groups), so
+// the waves behind are issued first and the waves of a CU finish together (A/B: 0.845 -> 0.862).
+__device__ __forceinline__ void prio_by_work_left(uint32_t q, uint32_t nq) {
+    if (q & 3u) return;
+    const uint32_t pr = (uint32_t)(((uint64_t)(nq - q) * 4u) / ((uint64_t)nq + 1u));
+    if (pr >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 constexpr uint32_t kLocalSlots = 128;
 static_assert(kLocalSlots == kStreamLocalSlots, "engine.cpp stream_local_only mirrors the slot count");
 constexpr uint32_t kLocalOff = kBraidLds;
@@ -1736,6 +1755,9 @@ __global__ __launch_bounds__(StreamShape<WB>::kBlock, 4) void crc32_stream_kerne
     acc.slot = ~0ull;
     auto step = [&](Grp &cur, Grp &nxt, bool first) {
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0u;
+#if AMDCRC_STREAM_PRIO
+        prio_by_work_left(q, nq);
+#endif
         const uint64_t sn = f_addr();
         f_next();
         u = stream_rows<0, B>(u, cur, nxt, voff, sn, eng);
@@ -2065,6 +2087,9 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
     };
     part_begin();
     auto step = [&](W8Group &cur, W8Group &nxt, bool first) {
+#if AMDCRC_PRIO_ALL
+        prio_by_work_left(q, nq);
+#endif
         const __amdgpu_buffer_rsrc_t rs = f_rsrc();
         const uint32_t fo = f_off(), fl = f_lim();
         f_next();
@@ -2733,6 +2758,9 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_stream4_kernel(const ScanParam
     uint64_t u = 0;
     uint32_t q = 0;  // groups scanned
     auto step = [&](B64Group &cur, B64Group &nxt) {
+#if AMDCRC_PRIO_ALL
+        prio_by_work_left(q, nq);
+#endif
         if (g == 0) u = d.k == 0 && lane == 0 ? head_state<false>(p, d.b, eng) : 0ull;
         const uint64_t sn = f_addr();
         f_next();
@@ -3056,7 +3084,12 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint32_t jr = pad / kB64Row, l0 = (pad % kB64Row) / 8u;
     XcdCursor sc = cur_at(c0);
     uint32_t g = 0, q = 0;
+    // multi-batch launches: issue priority by the work left (crc32_stream_kernel's; A/B on one box:
+    // 20-batch C5 0.698-0.712 -> 0.723-0.731, but one-batch launches overlapping over three streams
+    // lost 8 %, so only here)
+    const bool prio = p.nbatch > 1;
     auto step = [&](B64Group &cur, B64Group &nxt) {
+        if (prio || AMDCRC_PRIO_ALL) prio_by_work_left(q, nq);
         if (g == 0) {
             if (pn && sc.b == pb) {
                 u = xcd_jump(lds, u);
@@ -3258,6 +3291,9 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
     };
     part_begin();
     auto step = [&](B64Group &cur, B64Group &nxt) {
+#if AMDCRC_PRIO_ALL
+        prio_by_work_left(q, nq);
+#endif
         const __amdgpu_buffer_rsrc_t rs = f_rsrc();
         const uint32_t fo = f_off(), fl = f_lim();
         f_next();
