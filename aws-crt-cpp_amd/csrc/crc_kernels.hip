@@ -3084,12 +3084,13 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint32_t jr = pad / kB64Row, l0 = (pad % kB64Row) / 8u;
     XcdCursor sc = cur_at(c0);
     uint32_t g = 0, q = 0;
-    // multi-batch launches: issue priority by the work left (crc32_stream_kernel's; A/B on one box:
-    // 20-batch C5 0.698-0.712 -> 0.723-0.731, but one-batch launches overlapping over three streams
-    // lost 8 %, so only here)
-    const bool prio = p.nbatch > 1;
+    // (issue priority by the work left, crc32_stream_kernel's, measured here in round 5: 20-batch C5
+    // 0.70 -> 0.72-0.73, but one-batch launches overlapping over three streams lost 8 %, and a
+    // run-time switch between the two cost the single launch 12 % -- profiles/r05/ab/r05ae_*)
     auto step = [&](B64Group &cur, B64Group &nxt) {
-        if (prio || AMDCRC_PRIO_ALL) prio_by_work_left(q, nq);
+#if AMDCRC_PRIO_ALL
+        prio_by_work_left(q, nq);
+#endif
         if (g == 0) {
             if (pn && sc.b == pb) {
                 u = xcd_jump(lds, u);
