@@ -410,9 +410,15 @@ constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 // ~144 us, the second workgroup's at ~190 us of ~200 (per-wave stamps), the launch's last 25 % running
 // on half the waves.  Every fourth group a wave sets s_setprio to (groups left * 4 / groups), so
 // the waves behind are issued first and the waves of a CU finish together (A/B: 0.845 -> 0.862).
+#ifndef AMDCRC_PRIO_EVERY  // compile-time only (A/B builds): groups between priority updates (power of two)
+#define AMDCRC_PRIO_EVERY 4
+#endif
+#ifndef AMDCRC_PRIO_SCALE  // compile-time only (A/B builds): priority = groups left * SCALE / groups, capped at 3
+#define AMDCRC_PRIO_SCALE 4
+#endif
 __device__ __forceinline__ void prio_by_work_left(uint32_t q, uint32_t nq) {
-    if (q & 3u) return;
-    const uint32_t pr = (uint32_t)(((uint64_t)(nq - q) * 4u) / ((uint64_t)nq + 1u));
+    if (q & (AMDCRC_PRIO_EVERY - 1u)) return;
+    const uint32_t pr = (uint32_t)(((uint64_t)(nq - q) * AMDCRC_PRIO_SCALE) / ((uint64_t)nq + 1u));
     if (pr >= 3) __builtin_amdgcn_s_setprio(3);
     else if (pr == 2) __builtin_amdgcn_s_setprio(2);
     else if (pr == 1) __builtin_amdgcn_s_setprio(1);
