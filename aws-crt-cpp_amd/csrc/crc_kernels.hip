@@ -408,13 +408,14 @@ constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 // Issue priority by the work a wave has left (round 5).  Two workgroups share a CU and the one
 // dispatched first is served first (oldest-first issue): its waves finished a 20-batch C2 launch at
 // ~144 us, the second workgroup's at ~190 us of ~200 (per-wave stamps), the launch's last 25 % running
-// on half the waves.  Every fourth group a wave sets s_setprio to (groups left * 4 / groups), so
-// the waves behind are issued first and the waves of a CU finish together (A/B: 0.845 -> 0.862).
+// on half the waves.  Every fourth group a wave sets s_setprio to min(3, groups left * 6 / groups),
+// so the waves behind are issued first and the waves of a CU finish together (A/B: 0.845 -> 0.862;
+// scale 6 against 4: +0.3 %, within the noise of two sessions).
 #ifndef AMDCRC_PRIO_EVERY  // compile-time only (A/B builds): groups between priority updates (power of two)
 #define AMDCRC_PRIO_EVERY 4
 #endif
 #ifndef AMDCRC_PRIO_SCALE  // compile-time only (A/B builds): priority = groups left * SCALE / groups, capped at 3
-#define AMDCRC_PRIO_SCALE 4
+#define AMDCRC_PRIO_SCALE 6
 #endif
 __device__ __forceinline__ void prio_by_work_left(uint32_t q, uint32_t nq) {
     if (q & (AMDCRC_PRIO_EVERY - 1u)) return;
