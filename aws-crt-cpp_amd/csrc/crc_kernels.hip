@@ -402,6 +402,9 @@ constexpr uint32_t kBraidLds = kConstFlagOff + 16;
 #ifndef AMDCRC_STREAM_PRIO  // compile-time only (A/B builds): crc32_stream_kernel issue priority by work left
 #define AMDCRC_STREAM_PRIO 1
 #endif
+#ifndef AMDCRC_R16_PRIO  // compile-time only (A/B builds): the same in crc64_rows16_kernel
+#define AMDCRC_R16_PRIO 1
+#endif
 #ifndef AMDCRC_PRIO_ALL  // compile-time only (A/B builds): the same in the CRC64 and list scans
 #define AMDCRC_PRIO_ALL 0
 #endif
@@ -3464,6 +3467,9 @@ __global__ __launch_bounds__(kR16Block, 4) void crc64_rows16_kernel(const ScanPa
     uint32_t g = 0, q = 0;
     uint64_t u = 0;
     auto step = [&](B64Group &cur, B64Group &nxt) {
+#if AMDCRC_R16_PRIO || AMDCRC_PRIO_ALL
+        prio_by_work_left(q, nq);  // (A/B on one box: C4 shard 0.786-0.795 -> 0.829-0.843)
+#endif
         if (g == 0) {
             // head states of the set's four buffers (wave-uniform), each entering its row's lane 0
             uint64_t h[4];
