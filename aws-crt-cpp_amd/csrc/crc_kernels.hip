@@ -2876,7 +2876,7 @@ __device__ __forceinline__ void xcd_issue(B64Group &g, __amdgpu_buffer_rsrc_t rs
 
 // PADDED: some main regions hold no whole number of chunks (ScanParams::xcd_pad != 0): every group
 // reads through a buffer resource.  Otherwise plain global loads (1-2 % shorter C5 launches).
-template <uint64_t POLY, int BLOCK, bool PADDED>
+template <uint64_t POLY, int BLOCK, bool PADDED, bool PRIO = false>
 __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p) {
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
@@ -3094,13 +3094,12 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     const uint32_t jr = pad / kB64Row, l0 = (pad % kB64Row) / 8u;
     XcdCursor sc = cur_at(c0);
     uint32_t g = 0, q = 0;
-    // (issue priority by the work left, crc32_stream_kernel's, measured here in round 5: 20-batch C5
-    // 0.70 -> 0.72-0.73, but one-batch launches overlapping over three streams lost 8 %, and a
-    // run-time switch between the two cost the single launch 12 % -- profiles/r05/ab/r05ae_*)
+    // PRIO (multi-batch launches): issue priority by the work left, crc32_stream_kernel's.  Measured
+    // here in round 5: 20-batch C5 0.70 -> 0.72-0.73, but one-batch launches overlapping over three
+    // streams lost 8 % with it and a run-time switch cost the single launch 12 % (profiles/r05/ab/
+    // r05ad_*, r05ae_*), hence a separate instantiation chosen at launch by batch count
     auto step = [&](B64Group &cur, B64Group &nxt) {
-#if AMDCRC_PRIO_ALL
-        prio_by_work_left(q, nq);
-#endif
+        if constexpr (PRIO || AMDCRC_PRIO_ALL) prio_by_work_left(q, nq);
         if (g == 0) {
             if (pn && sc.b == pb) {
                 u = xcd_jump(lds, u);
@@ -4169,7 +4168,8 @@ extern "C" int amdcrc_launch_scan(int alg, const ScanParams *p, int nblocks, voi
             else if (p->stream == 5 && !list && p->xcd_pad)  // long buffers: XCD-window chunks, front pads
                 launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, true>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream == 5 && !list)  // long buffers of whole chunks
-                launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false>, nblocks, kXcdBlock, s, p, ev);
+                p->nbatch > 1 ? launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false, true>, nblocks, kXcdBlock, s, p, ev)
+                              : launch(crc64_xcd_kernel<kPoly64Nvme, kXcdBlock, false>, nblocks, kXcdBlock, s, p, ev);
             else if (p->stream && !list)  // 4-copy tables
                 launch(crc64_stream4_kernel<kPoly64Nvme, kW64StreamBlock>, nblocks, kW64StreamBlock, s, p, ev);
             else if (list && p->stream == 4)  // ragged lists: the list streaming scan
