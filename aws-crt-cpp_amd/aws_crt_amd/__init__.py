@@ -1,6 +1,6 @@
 """ctypes binding of the MI355X checksum engine's C ABI (include/aws_crt_amd/checksums_batch.h,
 include/aws/checksums/crc.h).  Used by tests/ and bench.py; torch supplies device memory and
-streams only.  Every compute call goes through lib/libaws-crt-cpp-amd.so -- there is no Python
+streams only.  Every compute call goes through lib/libaws-checksums-amd.so -- there is no Python
 checksum code: if the library is missing, calls raise; device-batch calls raise without a gfx950
 device.  The library's own host path (csrc/cpu/) serves host memory per its dispatch mode.
 
@@ -14,7 +14,10 @@ import os
 from typing import Optional, Sequence
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-crt-cpp-amd.so")
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-checksums-amd.so")
+# aws-c-common stand-in: the engine's few aws-c-common calls (aws_raise_error, aws_mem_*) bind to the
+# process's aws-c-common, as aws-checksums' do; standalone that is this library, loaded globally first
+SHIM_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libaws-c-common-shim.so")
 
 CRC32, CRC32C, CRC64NVME, XXH64, XXH3_64, XXH3_128 = 0, 1, 2, 3, 4, 5
 DISPATCH_AUTO, DISPATCH_CPU, DISPATCH_GPU = 0, 1, 2
@@ -37,8 +40,10 @@ def lib() -> ctypes.CDLL:
         # Load it first so the engine's DT_NEEDED libamdhip64.so.7 binds to that same instance:
         # one HIP runtime per process, and torch's streams / allocations are valid handles for us.
         import torch  # noqa: F401
-        if not os.path.exists(LIB_PATH):
-            raise EngineError(f"native engine not built: {LIB_PATH} missing (run __graft_entry__.build())")
+        for p in (SHIM_PATH, LIB_PATH):
+            if not os.path.exists(p):
+                raise EngineError(f"native engine not built: {p} missing (run __graft_entry__.build())")
+        ctypes.CDLL(SHIM_PATH, mode=ctypes.RTLD_GLOBAL)
         L = ctypes.CDLL(LIB_PATH)
         vp, sz, u32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64
         L.aws_crt_amd_init.restype = ctypes.c_int

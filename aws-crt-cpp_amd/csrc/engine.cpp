@@ -30,8 +30,6 @@
 #include <tuple>
 #include <vector>
 
-#include <aws/crt/Types.h>
-
 #include "abi_guard.h"
 #include "cpu/cpu_checksums.h"
 #include "engine.h"
@@ -2173,6 +2171,22 @@ AWS_CRT_AMD_API int aws_crt_amd_crc_combine_batch(int alg, const void *d_crc1, c
     });
 }
 
+// The S3 wire form of a digest: standard base64 with padding (RFC 4648 §4), what the CRT's
+// Aws::Crt::Base64Encode (reference include/aws/crt/Types.h:70-75) gives for it.  The engine sits at
+// the aws-checksums level and does not call up into the C++ surface.
+static std::string wire_base64(const uint8_t *p, size_t n) {
+    static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    std::string out;
+    for (size_t i = 0; i < n; i += 3) {
+        const uint32_t v = (uint32_t)p[i] << 16 | (i + 1 < n ? (uint32_t)p[i + 1] << 8 : 0) | (i + 2 < n ? p[i + 2] : 0);
+        out += A[v >> 18];
+        out += A[(v >> 12) & 63];
+        out += i + 1 < n ? A[(v >> 6) & 63] : '=';
+        out += i + 2 < n ? A[v & 63] : '=';
+    }
+    return out;
+}
+
 // S3 multipart composition (checksums_batch.h): one batched scan over the parts, then the
 // Combine fold of the part values (4/8-byte scalars, no payload) into the full-object checksum.
 AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_parts, const size_t *lens, size_t count,
@@ -2242,7 +2256,7 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_crc(int alg, const void *const *d_part
         if (b64_out) {
             uint8_t be[8];
             for (int i = 0; i < w / 8; ++i) be[i] = (uint8_t)(obj >> (w - 8 * (i + 1)));
-            const Aws::Crt::String b64 = Aws::Crt::Base64Encode(aws_byte_cursor_from_array(be, (size_t)(w / 8)));
+            const std::string b64 = wire_base64(be, (size_t)(w / 8));
             std::memcpy(b64_out, b64.c_str(), b64.size() + 1);
         }
         return 0;
@@ -2314,8 +2328,7 @@ AWS_CRT_AMD_API int aws_crt_amd_multipart_checksum(int alg, int type, const void
         if (b64_out) {
             uint8_t be[16];
             for (size_t b = 0; b < dsz; ++b) be[b] = (uint8_t)(obj[b / 8] >> (dsz == 4 ? 8 * (3 - b) : 8 * (7 - (b & 7))));
-            const Aws::Crt::String b64 = Aws::Crt::Base64Encode(aws_byte_cursor_from_array(be, dsz));
-            const std::string wire = std::string(b64.c_str()) + "-" + std::to_string(count);
+            const std::string wire = wire_base64(be, dsz) + "-" + std::to_string(count);
             std::memcpy(b64_out, wire.c_str(), wire.size() + 1);
         }
         return 0;

@@ -45,15 +45,15 @@ for s in "$@"; do
     ab64)  step 900 $O/ab64.log env TAG=${TAG}/ab64 VARIANTS="${X64VARIANTS:-R W}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/ab64.log ;;
     ab64c1) step 900 $O/ab64c1.log env TAG=${TAG}/ab64c1 VARIANTS="${X64VARIANTS:-R W}" REPS=${REPS:-3} bash scripts/ab_lib.sh python -u bench.py --alg crc64nvme --buffers 8 --buffer-bytes 67108864 --steps 20 --warmup 5 --coalesce 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 8; rc=$?; cat $O/ab64c1.log ;;
     # the GPU parity tests that cover the uniform-batch scans, on variant $XLIB (then the release build back)
-    xtests) cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/librel.so && cp ab/lib${XLIB:-X}.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so &&
+    xtests) cp aws-crt-cpp_amd/lib/libaws-checksums-amd.so /tmp/librel.so && cp ab/lib${XLIB:-X}.so aws-crt-cpp_amd/lib/libaws-checksums-amd.so &&
             step 600 $O/xtests.log python -u -m pytest tests/test_gpu_parity.py tests/test_queue.py tests/test_multipart.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?;
-            cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so; tail -3 $O/xtests.log ;;
+            cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-checksums-amd.so; tail -3 $O/xtests.log ;;
     # event-stream bench on library variants (ab/lib$v.so, v in $ESVARIANTS), then the release build back
-    abes)  cp aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so /tmp/librel.so; rc=0
-           for v in ${ESVARIANTS:-R B}; do for r in 1 2; do cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so &&
+    abes)  cp aws-crt-cpp_amd/lib/libaws-checksums-amd.so /tmp/librel.so; rc=0
+           for v in ${ESVARIANTS:-R B}; do for r in 1 2; do cp ab/lib$v.so aws-crt-cpp_amd/lib/libaws-checksums-amd.so &&
              step 180 $O/abes_${v}_$r.log python -u aws-crt-cpp_amd/tools/bench_eventstream.py --device-frames || { rc=$?; break 2; }
              echo "$v $r $(grep '^{' $O/abes_${v}_$r.log | cut -c180-420)"; done; done
-           cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-crt-cpp-amd.so ;;
+           cp /tmp/librel.so aws-crt-cpp_amd/lib/libaws-checksums-amd.so ;;
     ingest) step 300 $O/ingest.log env AWS_CRT_AMD_INGEST_TRACE=${INGEST_TRACE:-0} python -u aws-crt-cpp_amd/tools/ingest_probe.py; rc=$?; grep '^{' $O/ingest.log | tail -1 | cut -c1-300 ;;
     tests:*) step 900 $O/pytest_sel.log python -u -m pytest $(echo ${s#tests:} | tr , " ") -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider; rc=$?; tail -3 $O/pytest_sel.log ;;
     py:*)  n=$(basename ${s#py:} .py); step 600 $O/$n.log python -u ${s#py:}; rc=$?; tail -5 $O/$n.log ;;

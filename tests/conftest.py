@@ -19,7 +19,7 @@ def pytest_configure(config):
 
 
 def _ensure_built():
-    lib = os.path.join(PKG, "lib", "libaws-crt-cpp-amd.so")
+    lib = os.path.join(PKG, "lib", "libaws-checksums-amd.so")
     if not os.path.exists(lib):
         subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
     from oracle import oracle  # noqa: E402  (test infrastructure)

@@ -18,10 +18,10 @@ from oracle import oracle
 from tests.golden.patterns import pattern
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
+from tests.libpaths import ENGINE as LIB, LOAD_SRC, load_engine  # noqa: E402
 # the diagnostic build (make -C aws-crt-cpp_amd diag): the same host path plus a hook that runs one CRC
 # on a chosen host tier, so every tier is checked on any host
-DIAG_LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd-diag.so")
+from tests.libpaths import DIAG as DIAG_LIB  # noqa: E402
 GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "vectors.json")))
 ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
 W64 = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
@@ -29,7 +29,7 @@ W64 = {"crc64nvme", "xxh64", "xxh3_64", "xxh3_128"}
 
 @pytest.fixture(scope="module")
 def L():
-    lib = ctypes.CDLL(LIB)
+    lib = load_engine()
     vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
     lib.aws_crt_amd_cpu_batch.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(sz), sz,
                                           ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.c_int]

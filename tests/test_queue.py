@@ -17,14 +17,13 @@ import pytest
 from oracle import oracle
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
+from tests.libpaths import ENGINE as LIB, LOAD_SRC, load_engine  # noqa: E402
 ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_128": 5}
 
 
 def test_queue_host_logic_without_device():
     code = (
-        "import ctypes\n"
-        f"L=ctypes.CDLL({LIB!r})\n"
+        LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t\n"
         "L.aws_crt_amd_queue_create.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push.argtypes=[vp,vp,vp,vp]\n"
@@ -54,8 +53,7 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
     error (AWS_CRT_AMD_ERR_NO_DEVICE) through its ticket, queued tickets report QUEUED, unknown
     tickets are refused; max_batches launches early; the age bound launches without a further push."""
     code = (
-        "import ctypes, time\n"
-        f"L=ctypes.CDLL({LIB!r})\n"
+        LOAD_SRC + "import time\n"
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
         "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
@@ -215,8 +213,7 @@ def test_queue_refused_tickets_never_report_complete():
     3,000 refused one-batch launches all still report the refusal; a ticket whose record is gone would
     report AWS_CRT_AMD_ERR_TICKET_EXPIRED (-5), never 0."""
     code = (
-        "import ctypes\n"
-        f"L=ctypes.CDLL({LIB!r})\n"
+        LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
         "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"

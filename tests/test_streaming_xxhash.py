@@ -14,7 +14,7 @@ import pytest
 from oracle import oracle
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "aws-crt-cpp_amd", "lib", "libaws-crt-cpp-amd.so")
+from tests.libpaths import ENGINE as LIB, LOAD_SRC, load_engine  # noqa: E402
 
 
 class Cursor(ctypes.Structure):
@@ -28,7 +28,7 @@ class Buf(ctypes.Structure):
 
 @pytest.fixture(scope="module")
 def L():
-    lib = ctypes.CDLL(LIB)
+    lib = load_engine()
     for k in ("aws_xxhash64_new", "aws_xxhash3_64_new", "aws_xxhash3_128_new"):
         f = getattr(lib, k)
         f.restype, f.argtypes = ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_uint64]
