@@ -250,7 +250,10 @@ class BatchSet:
         # written by it
         self._keep = [t for b in batches for t in b if hasattr(t, "data_ptr")]
         self._cuda = [t for t in self._keep if getattr(t, "is_cuda", False)]
-        self._recorded = set()  # streams the tensors are already recorded on
+        # streams the tensors are already recorded on, keyed by the stream OBJECT and holding it (ADVICE
+        # r05): a raw handle can be reused by a new stream once the old one is destroyed, an object
+        # kept alive here cannot be confused with another
+        self._recorded = {}
         arr = (_Batch * max(self.n, 1))()
         for i, (base, seeds, out) in enumerate(batches):
             arr[i].d_base = base.data_ptr() if hasattr(base, "data_ptr") else int(base)
@@ -274,14 +277,14 @@ class BatchSet:
         rc = self.fn(self._plan, _stream_handle(stream))
         if rc != 0:
             _check(rc)
-        if self._cuda and stream is not None and hasattr(stream, "cuda_stream") and stream.cuda_stream not in self._recorded:
+        if self._cuda and stream is not None and hasattr(stream, "cuda_stream") and id(stream) not in self._recorded:
             # a launch on a side stream: the caching allocator must not hand these blocks out again
             # before that stream has finished with them.  Once per stream: the allocator waits for every
             # recorded stream when the block is freed, so recording it again per launch only costs host
             # time between launches
             for t in self._cuda:
                 t.record_stream(stream)
-            self._recorded.add(stream.cuda_stream)
+            self._recorded[id(stream)] = stream
 
     def __del__(self):
         if getattr(self, "_plan", None):
@@ -310,21 +313,26 @@ def checksum_batches(alg: int, batches, stride: int, length: int, count: int, st
 
 
 class _QueueOptions(ctypes.Structure):
-    _fields_ = [("max_batches", ctypes.c_size_t), ("max_age_us", ctypes.c_uint64)]
+    _fields_ = [("max_batches", ctypes.c_size_t), ("max_age_us", ctypes.c_uint64), ("policy", ctypes.c_uint32),
+                ("max_inflight", ctypes.c_uint32)]
 
 
 TICKET_QUEUED, TICKET_LAUNCHED = 1, 2
+QUEUE_EAGER, QUEUE_BATCHED = 0, 1
 
 
 class Queue:
     """A submission queue (aws_crt_amd_queue_*): batches of one shape pushed one at a time are launched
-    together, at max_batches queued (32 by default), once the oldest has waited max_age_us (0: no age
-    bound), and at flush() / wait() / close().  push() returns the batch's ticket; status(ticket) /
-    wait(ticket) give its completion (0) or the error of the launch that dropped it.  The pushed tensors
-    stay referenced until the engine has launched them (every ticket below first_pending()); thread-safe."""
+    together.  policy QUEUE_EAGER (default): a push that finds fewer than max_inflight (default 1) of the
+    queue's launches running launches everything queued at once; QUEUE_BATCHED: only at max_batches
+    queued (32 by default), once the oldest has waited max_age_us (0: no age bound), and at flush() /
+    wait() / close() (which also launch under the eager policy).  push() returns the batch's ticket;
+    status(ticket) / wait(ticket) give its completion (0) or the error of the launch that dropped it.
+    The pushed tensors stay referenced until the engine has launched them (every ticket below
+    first_pending()); thread-safe."""
 
     def __init__(self, alg: int, stride: int, length: int, count: int, stream=None, max_batches: int = 0,
-                 max_age_us: int = 0):
+                 max_age_us: int = 0, policy: int = QUEUE_EAGER, max_inflight: int = 0):
         import threading
 
         L = lib()
@@ -337,6 +345,8 @@ class Queue:
         L.aws_crt_amd_queue_pending.restype = ctypes.c_size_t
         L.aws_crt_amd_queue_first_pending.argtypes = [vp]
         L.aws_crt_amd_queue_first_pending.restype = u64
+        L.aws_crt_amd_queue_launches.argtypes = [vp]
+        L.aws_crt_amd_queue_launches.restype = u64
         L.aws_crt_amd_queue_status.argtypes = [vp, u64]
         L.aws_crt_amd_queue_wait.argtypes = [vp, u64]
         L.aws_crt_amd_queue_destroy.argtypes = [vp]
@@ -345,7 +355,7 @@ class Queue:
         self._keep = {}  # ticket -> tensors, until the ticket is launched
         self._lock = threading.Lock()
         h = vp()
-        opt = _QueueOptions(max_batches, max_age_us)
+        opt = _QueueOptions(max_batches, max_age_us, policy, max_inflight)
         _check(L.aws_crt_amd_queue_create_ex(alg, stride, length, count, _stream_handle(stream), ctypes.byref(opt),
                                              ctypes.byref(h)))
         self._h = h
@@ -374,6 +384,9 @@ class Queue:
 
     def pending(self) -> int:
         return int(self._L.aws_crt_amd_queue_pending(self._h))
+
+    def launches(self) -> int:
+        return int(self._L.aws_crt_amd_queue_launches(self._h))
 
     def first_pending(self) -> int:
         return int(self._L.aws_crt_amd_queue_first_pending(self._h))

@@ -68,6 +68,31 @@ def split_buffer_crc(alg_name: str, total: int, compute_slice: Callable[[range],
     return crc if crc is not None else compute_slice(range(0, 0))
 
 
+def gather_round_robin(local, n: int, group=None):
+    """Every rank's results (rank r holds buffers r, r + world, ...: a 1-D tensor of result words) ->
+    all n results in buffer order, on every rank.  One all_gather of the padded result vectors (4-8
+    bytes per buffer, never payload), then a strided scatter.  `local` lives where the group's
+    backend wants it (CPU for gloo, the rank's GPU for RCCL); the result is on the same device.
+    With no process group initialised this is the single-GPU case."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return local[:n]
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if local.numel() != shard_count(n, rank, world):
+        raise ValueError("local results do not match this rank's shard")
+    width = shard_count(n, 0, world)  # rank 0's shard is the largest
+    pad = torch.zeros(width, dtype=local.dtype, device=local.device)
+    pad[: local.numel()] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    out = torch.empty(n, dtype=local.dtype, device=local.device)
+    for r, b in enumerate(bufs):
+        out[r::world] = b[: shard_count(n, r, world)]
+    return out
+
+
 def sharded_checksums(n: int, compute_shard: Callable[[range], Sequence[int]], group=None) -> List[int]:
     """Run `compute_shard(indices)` on this rank's shard, then gather every rank's results (a
     small all_gather of result words) and return them in buffer order.  With no process group
@@ -78,12 +103,50 @@ def sharded_checksums(n: int, compute_shard: Callable[[range], Sequence[int]], g
     if not (dist.is_available() and dist.is_initialized()):
         return list(compute_shard(range(n)))
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    mine = list(compute_shard(shard_indices(n, rank, world)))
-    width = max(shard_count(n, r, world) for r in range(world))
-    t = torch.zeros(width, dtype=torch.int64)
-    for j, v in enumerate(mine):
-        t[j] = v - (1 << 64) if v >= 1 << 63 else v
-    bufs = [torch.zeros(width, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(bufs, t, group=group)
-    per_rank = [[int(x) & ((1 << 64) - 1) for x in b.tolist()[: shard_count(n, r, world)]] for r, b in enumerate(bufs)]
-    return interleave(per_rank, n)
+    mine = [v - (1 << 64) if v >= 1 << 63 else v for v in compute_shard(shard_indices(n, rank, world))]
+    got = gather_round_robin(torch.tensor(mine, dtype=torch.int64), n, group)
+    return [int(x) & ((1 << 64) - 1) for x in got.tolist()]
+
+
+class RoundRobinShard:
+    """One rank's part of a uniform set of n device buffers of `length` bytes sharded round-robin over
+    the ranks (BASELINE.json config 4: buffer i on GPU i mod N).  The rank's buffers lie back to back
+    in its own GPU's memory (`data`, uint8, stride = length); `launch` scans them with one strided
+    call on the rank's stream; `gather` brings every rank's result words together in buffer order.
+    No payload byte leaves its GPU and the data path has no collective."""
+
+    def __init__(self, eng, alg: int, data, n: int, length: int, rank: int = 0, world: int = 1):
+        import torch
+
+        self.eng, self.alg, self.data, self.n, self.length = eng, alg, data, n, length
+        self.rank, self.world = rank, world
+        self.count = shard_count(n, rank, world)
+        if data.numel() < self.count * length:
+            raise ValueError("shard data smaller than the rank's buffers")
+        wide = alg in (eng.CRC64NVME, eng.XXH64, eng.XXH3_64)
+        if alg == eng.XXH3_128:
+            raise ValueError("one result word per buffer: XXH3-128 is not sharded this way")
+        self.out = torch.empty(self.count, dtype=torch.int64 if wide else torch.int32, device=data.device)
+        self.width = 8 if wide else 4
+
+    def launch(self, stream=None):
+        self.eng.checksum_strided(self.alg, self.data, self.length, self.length, self.count, out=self.out, stream=stream)
+
+    def gather(self, group=None, device=None):
+        """all n results in buffer order as int64 bit patterns (4-byte results zero-extended) on
+        `device` (default: CPU, as gloo wants; RCCL groups pass the rank's GPU)"""
+        import torch
+
+        local = self.out.to(device or "cpu").to(torch.int64)
+        if self.width == 4:
+            local = torch.bitwise_and(local, 0xFFFFFFFF)
+        return gather_round_robin(local, self.n, group)
+
+
+def results_digest(eng, results, width: int) -> int:
+    """The set's "checksum of checksums" (tests/golden/c4_digest.json): CRC64NVME, on the engine's host
+    path, over the results in buffer order as little-endian words of `width` bytes."""
+    import numpy as np
+
+    arr = results.cpu().numpy().astype("<u8" if width == 8 else "<u4")
+    return eng.crc("crc64nvme", arr.tobytes())

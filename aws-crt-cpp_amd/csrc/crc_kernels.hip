@@ -1864,8 +1864,8 @@ __device__ __forceinline__ void list_join(uint64_t *slot, uint32_t d, T r, uint3
 // first word are not the buffer's: the scan clears them in the registers (list_mask_edges) and the head
 // state enters divided by x^(8 o), so it reaches ~seed exactly at ptr.  The tail (< 8 bytes) is folded.
 // (Masking the last word too -- [ptr & ~7, (end + 7) & ~7), the register leaving times x^(-8 k) -- made
-// unaligned 64 KiB buffers one 4 KiB group longer, 2 us per 256 MiB list slower; the code keeps the
-// k path for it.)  A shorter buffer has no main region and is folded whole (engine.cpp main_len_list).
+// unaligned 64 KiB buffers one 4 KiB group longer, 2 us per 256 MiB list slower; that path is gone,
+// ADVICE r05.)  A shorter buffer has no main region and is folded whole (engine.cpp main_len_list).
 constexpr uint64_t kListMainMin = 16;
 struct LBuf {        // the cursor's buffer (wave-uniform)
     uint64_t b;      // buffer index
@@ -1873,7 +1873,7 @@ struct LBuf {        // the cursor's buffer (wave-uniform)
     uint32_t vg;     // groups (0: no main region)
     uint32_t pad;    // virtual zero bytes in front of main (< 4096)
     uint64_t ptr, n; // the buffer
-    uint32_t o, k;   // bytes of the first / last main word outside the buffer
+    uint32_t o;      // bytes of the first main word in front of the buffer
     __device__ __forceinline__ Edges edges() const {  // the tail (< 8 bytes), or a whole short buffer, is folded
         return vg ? Edges{ptr, ptr, (ptr + n) & ~7ull, ptr + n} : Edges{ptr, ptr + n, ptr + n, ptr + n};
     }
@@ -1881,23 +1881,21 @@ struct LBuf {        // the cursor's buffer (wave-uniform)
 __device__ __forceinline__ LBuf lbuf_at(const ScanParams &p, uint64_t b) {
     uint64_t ptr, n;
     list_desc(p, b, ptr, n);
-    if (n < kListMainMin) return LBuf{b, 0, 0, 0, ptr, n, 0, 0};
+    if (n < kListMainMin) return LBuf{b, 0, 0, 0, ptr, n, 0};
     const uint64_t m0 = ptr & ~7ull, m1 = (ptr + n) & ~7ull, m = m1 - m0;
     const uint64_t vg = (m + kWaveGroupBytes - 1) / kWaveGroupBytes;
     const uint32_t pad = (uint32_t)(vg * kWaveGroupBytes - m);
-    return LBuf{b, m0 - pad, (uint32_t)vg, pad, ptr, n, (uint32_t)(ptr - m0), 0u};
+    return LBuf{b, m0 - pad, (uint32_t)vg, pad, ptr, n, (uint32_t)(ptr - m0)};
 }
-// clears the bytes outside the buffer in its first word (group 0, row pad / 512, lane (pad mod 512) / 8)
-// and its last word (the last group's row 7, lane 63); only in those two groups (wave-uniform test)
+// clears the bytes in front of the buffer in its first word (group 0, row pad / 512, lane (pad mod 512)
+// / 8); only in that group (wave-uniform test)
 template <class G>
 __device__ __forceinline__ void list_mask_edges(G &cur, uint32_t g, const LBuf &sc, int lane) {
-    const bool head = g == 0 && sc.o, tail = g + 1 == sc.vg && sc.k;
-    if (!head && !tail) return;
+    if (g != 0 || !sc.o) return;
     const uint32_t jh = (sc.pad >> 9) & 7u, lh = (sc.pad & 511u) >> 3;
-    const uint64_t mh = head && (uint32_t)lane == lh ? ~0ull << (8 * sc.o) : ~0ull;
-    const uint64_t mt = tail && lane == 63 ? ~0ull >> (8 * sc.k) : ~0ull;
+    const uint64_t mh = (uint32_t)lane == lh ? ~0ull << (8 * sc.o) : ~0ull;
 #pragma unroll
-    for (int R = 0; R < 8; ++R) cur.w[R] &= ((uint32_t)R == jh ? mh : ~0ull) & (R == 7 ? mt : ~0ull);
+    for (int R = 0; R < 8; ++R) cur.w[R] &= (uint32_t)R == jh ? mh : ~0ull;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint64_t base, uint32_t nrec) {
@@ -2050,11 +2048,8 @@ __global__ __launch_bounds__(kBraidBlock, 4) void crc32_list_stream_kernel(const
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
-    // the buffer's register at the end of its main words -> at its end (x^(-8 k)) -> stored (lane 0)
-    auto finish = [&](uint32_t r) {
-        if (sc.k) r = mul_nib32(r, xneg + 128 * sc.k);
-        finalize_e<true>(p, sc.b, sc.edges(), r, eng);
-    };
+    // the buffer's register at the end of its main words -> its tail folded -> stored (lane 0)
+    auto finish = [&](uint32_t r) { finalize_e<true>(p, sc.b, sc.edges(), r, eng); };
     // value r of n groups of a buffer of vg groups into its accumulator; the part completing the count
     // finishes it (lane 0)
     auto publish = [&](uint64_t b, uint32_t r, uint32_t n, uint32_t vg) {
@@ -3257,8 +3252,7 @@ __global__ __launch_bounds__(512, 4) void crc64_list_stream_kernel(const ScanPar
             if ((uint32_t)lane == ((sc.pad & 511u) >> 3)) u = s_h;
         }
     };
-    auto finish = [&](uint64_t r) {  // at the end of the main words -> at the buffer's end -> stored
-        if (sc.k) r = mul_nib64(r, xneg + 256 * sc.k);
+    auto finish = [&](uint64_t r) {  // at the end of the main words -> its tail folded -> stored
         finalize_e<true>(p, sc.b, sc.edges(), r, eng);
     };
     auto publish = [&](uint64_t b, uint64_t r, uint32_t n, uint32_t vg) {  // lane 0

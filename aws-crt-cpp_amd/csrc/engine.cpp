@@ -675,12 +675,14 @@ uint8_t pow2_shift1(uint64_t v) { return v && (v & (v - 1)) == 0 ? (uint8_t)(__b
 // whole buffers per workgroup): the C2 shapes, one batch or twenty.  The launch then takes no stream
 // state, so it records no fence event behind itself (round 5: one runtime call less per launch, the
 // cost that bounds one-batch-per-launch submission).
-bool stream_local_only(const ScanParams &p, uint64_t blocks) {
-    const uint64_t T = p.tiles_per_buf, nw = blocks * 8;
+// wpb: waves per workgroup of the instantiation (8: 512-thread kBraidBlock; 16: the 1024-thread
+// kW16Block of the 16-byte-word variant, p.stream == 2).
+bool stream_local_only(const ScanParams &p, uint64_t blocks, uint64_t wpb) {
+    const uint64_t T = p.tiles_per_buf, nw = blocks * wpb;
     if (T < 2 || T > 32 || p.nstatic || p.xcd_order || p.list_mode) return false;
     auto split_at = [&](uint64_t w) { return w * p.split_q + std::min<uint64_t>(w, p.split_r); };
     for (uint64_t b = 0; b < blocks; ++b) {
-        const uint64_t t0 = split_at(8 * b), t1 = split_at(std::min(8 * b + 8, nw));
+        const uint64_t t0 = split_at(wpb * b), t1 = split_at(std::min(wpb * b + wpb, nw));
         if (t0 % T || t1 % T || (t1 - t0) / T > kStreamLocalSlots) return false;
     }
     return true;
@@ -702,10 +704,13 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     if (p.stream == 3) blocks = std::min<uint64_t>((p.nbuf + 4 * 8 - 1) / (4 * 8), 2 * (uint64_t)d->cus);  // 4 buffers per wave
     if (p.list_mode && p.stream == 4) blocks = list_stream_blocks(d, p.ntiles, total_main);  // the waves list_stream split for
     if (blocks == 0) return 0;
-    // crc32_stream_kernel's static split (ScanParams::split_q), now that the grid is known
-    const bool stream32 = width_of(alg) == 32 && p.stream == 1 && !p.list_mode;
+    // crc32_stream_kernel's static split (ScanParams::split_q), now that the grid is known.  Every
+    // instantiation takes its waves' tiles from the split (the 16-byte-word variant,
+    // p.stream == 2, had none and wrote no result), over its own waves per workgroup.
+    const bool stream32 = width_of(alg) == 32 && (p.stream == 1 || p.stream == 2) && !p.list_mode;
+    const uint64_t wpb = p.stream == 2 ? 16 : 8;
     if (stream32) {
-        const uint64_t nw = blocks * 8;
+        const uint64_t nw = blocks * wpb;
         p.split_q = p.ntiles / nw;
         p.split_r = (uint32_t)(p.ntiles % nw);
         p.shifts1 = (p.shifts1 & ~0xFFu) | pow2_shift1(p.tiles_per_buf);
@@ -714,7 +719,7 @@ int launch_scan(Device *d, int alg, ScanParams &p, uint64_t nbuf, uint64_t tmax,
     if (tmax > 1 || p.nstatic) {
         if ((rc = get_pcols(d, alg, tile, tmax, s, &p.d_pcols))) return rc;
         p.pcols_tmax = tmax;
-        ws = !(stream32 && stream_local_only(p, blocks));
+        ws = !(stream32 && stream_local_only(p, blocks, wpb));
         if (ws && !t_plan) {
             Workspace *w;
             if ((rc = get_workspace(d, s, nbuf, p.ntiles, &w))) return rc;
@@ -803,12 +808,30 @@ struct X64Job {
     std::atomic<bool> submitted{false};  // the submitting thread has queued everything (done recorded)
     bool seeds = false;
     uint64_t seed_all = 0;
+    hipStream_t stream = nullptr;  // the caller's stream: polled for errors while the worker waits on it
     std::vector<cpu::Xxh64State> xs;
 };
 
+// Route workers never block process exit: the runner is never destroyed (no join at
+// static destruction), an exit handler -- registered after the globals above exist, so it runs before
+// their destructors -- tells waiting workers to stop and gives running ones a moment to finish, and a
+// worker whose stream failed (or whose GPU stopped) gives up instead of spinning forever.
+std::atomic<bool> g_x64_stop{false};
+std::atomic<int> g_x64_active{0};
+std::atomic<unsigned long long> g_x64_abandoned{0};
+
+void x64_at_exit() {
+    g_x64_stop.store(true, std::memory_order_release);
+    for (int i = 0; i < 200 && g_x64_active.load(std::memory_order_acquire) > 0; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+}
+
 Runner &x64_runner() {
-    static Runner r;
-    return r;
+    static Runner *r = [] {
+        std::atexit(x64_at_exit);
+        return new Runner;
+    }();
+    return *r;
 }
 
 inline uint64_t sig_load(const uint64_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -818,6 +841,34 @@ inline void sig_store(uint64_t *p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC
 // stream reports it copied, one host thread per buffer; then the stage goes back once the caller's
 // stream has taken the results.
 // AWS_CRT_AMD_X64_TRACE=1 prints one line per job: time waiting for copies, time hashing.
+// Wait until *ctr >= want.  Gives up (false) when the process is exiting or the job's stream has
+// failed (hipStreamQuery reports an error other than "not ready", polled about every 5 ms).
+bool x64_wait(const X64Job *j, const uint64_t *ctr, uint64_t want) {
+    for (unsigned spin = 0; sig_load(ctr) < want; ++spin) {
+        if (g_x64_stop.load(std::memory_order_acquire)) return false;
+        if (spin < 64) {
+            std::this_thread::yield();
+            continue;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if ((spin & 255) == 0) {
+            const hipError_t q = hipStreamQuery(j->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) return false;
+        }
+    }
+    return true;
+}
+
+// A job whose copies will never land: release every wait the stream holds on the worker (the
+// counters jump past the job), drop the stage (the device may still write into it: never reused)
+// and count the job.  The stream's own error reports the failure to the caller.
+void x64_abandon(X64Job *j) {
+    sig_store(j->st->hashed, j->base + j->nslices);
+    g_x64_abandoned.fetch_add(1, std::memory_order_relaxed);
+    delete j;
+    g_x64_active.fetch_sub(1, std::memory_order_acq_rel);
+}
+
 void x64_work(X64Job *j) noexcept {
     X64Stage *st = j->st;
     static const bool trace = [] {
@@ -830,10 +881,7 @@ void x64_work(X64Job *j) noexcept {
     for (size_t k = 0; k < j->nslices; ++k) {
         const uint64_t want = j->base + k + 1;
         const auto w0 = clk::now();
-        for (unsigned spin = 0; sig_load(st->copied) < want; ++spin) {
-            if (spin < 64) std::this_thread::yield();
-            else std::this_thread::sleep_for(std::chrono::microseconds(20));
-        }
+        if (!x64_wait(j, st->copied, want)) return x64_abandon(j);
         const auto w1 = clk::now();
         if (k == 0) first_us = std::chrono::duration<double, std::micro>(w1 - w0).count();
         else wait_us += std::chrono::duration<double, std::micro>(w1 - w0).count();
@@ -853,8 +901,17 @@ void x64_work(X64Job *j) noexcept {
         fprintf(stderr, "[x64] buffers %zu slices %zu of %zu B: first copy %.0f us, copy waits %.0f us, hashing %.0f us, total %.0f us, threads %zu\n",
                 j->count, j->nslices, j->slice, first_us, wait_us, hash_us,
                 std::chrono::duration<double, std::micro>(clk::now() - t0).count(), cpu::share());
-    while (!j->submitted.load(std::memory_order_acquire)) std::this_thread::yield();
-    (void)hipEventSynchronize(st->done);  // the results' H2D has read h_res
+    while (!j->submitted.load(std::memory_order_acquire)) {
+        if (g_x64_stop.load(std::memory_order_acquire)) return x64_abandon(j);
+        std::this_thread::yield();
+    }
+    // the results' H2D has read h_res (polled: a stream that failed or a process exiting ends the wait)
+    for (unsigned spin = 0;; ++spin) {
+        const hipError_t q = hipEventQuery(st->done);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady || g_x64_stop.load(std::memory_order_acquire)) return x64_abandon(j);
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 64 ? 5 : 50));
+    }
     {
         std::lock_guard<std::mutex> g(g_x64_mu);
         try {
@@ -864,6 +921,7 @@ void x64_work(X64Job *j) noexcept {
         }
     }
     delete j;
+    g_x64_active.fetch_sub(1, std::memory_order_acq_rel);
 }
 
 int x64_take_stage(int dev, X64Stage **out) {
@@ -957,12 +1015,14 @@ int xxh64_host_route(int dev, uint64_t base, size_t stride, size_t len, size_t c
     const bool host_out = !is_device_ptr(d_out);
     j->out_host = host_out ? (uint64_t *)d_out : nullptr;
     uint64_t *const h_res = j->h_res;
+    j->stream = s;
     X64Job *jp = j.release();
     bool posted = true;
+    g_x64_active.fetch_add(1, std::memory_order_acq_rel);
     try {
         x64_runner().post([jp] { x64_work(jp); });
     } catch (...) {
-        posted = false;
+        posted = false;  // hashed on this thread below (x64_work ends the active count either way)
     }
     e = hipStreamWaitValue64(s, st->hashed, end, hipStreamWaitValueGte);  // every slice hashed
     if (!e && !host_out) e = hipMemcpyAsync(d_out, h_res, 8 * count, hipMemcpyHostToDevice, s);
@@ -1830,9 +1890,13 @@ AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(aws_crt_amd_plan *pl) { delete pl;
 
 // Submission queue (checksums_batch.h): pushes collect batches of one shape; a full queue
 // (max_batches, at most kMaxBatches), an age bound (a flusher thread), a flush or a wait hand them to
-// aws_crt_amd_checksum_batches, one launch per run of batches.  Every push gets a ticket; each launch
-// records an event after it on the queue's stream, so a ticket's completion (or the error of the
-// launch that dropped it) can be asked for and waited on.
+// aws_crt_amd_checksum_batches, one launch per run of batches -- and, under the eager policy (the
+// default since round 6), so does any push that finds fewer than max_inflight of
+// the queue's launches still running.  Round 5's queue launched only at 32 queued batches or at the
+// flush: a producer of one batch at a time left the GPU idle through all its pushes (4548-4689 GiB/s,
+// below one launch per batch).  Every push gets a ticket; each launch records an event after it on
+// the queue's stream, so a ticket's completion (or the error of the launch that dropped it) can be
+// asked for and waited on -- and the eager policy asks the newest events whether the stream is busy.
 struct aws_crt_amd_queue {
     int alg = 0;
     int device = 0;
@@ -1840,6 +1904,9 @@ struct aws_crt_amd_queue {
     void *stream = nullptr;
     size_t max_batches = kMaxBatches;
     uint64_t max_age_us = 0;
+    bool eager = true;        // AWS_CRT_AMD_QUEUE_EAGER
+    size_t max_inflight = 1;  // eager: launch on a push while fewer of the queue's launches are running
+    uint64_t nlaunches = 0;   // launches made (refused ones included)
     std::mutex mu;
     std::condition_variable cv;
     std::vector<aws_crt_amd_batch> pending;
@@ -1909,9 +1976,25 @@ int queue_flush_locked(aws_crt_amd_queue *q) {
     }
     // launched (with its completion event), or refused: its tickets carry the error; not retried
     q->launches.push_back({first, q->next_ticket, ev, rc});
+    ++q->nlaunches;
     q->pending.clear();
     queue_prune_locked(q);
     return rc;
+}
+
+// The queue's launches still running, newest first, counted up to `limit` (a stream completes its
+// launches in order: the first complete one ends the count; refused launches never ran)
+size_t queue_inflight_locked(aws_crt_amd_queue *q, size_t limit) {
+    size_t n = 0;
+    for (auto it = q->launches.rbegin(); it != q->launches.rend() && n < limit; ++it) {
+        if (it->rc || !it->ev) continue;
+        const hipError_t e = hipEventQuery(it->ev);
+        if (e == hipSuccess) break;
+        (void)hipGetLastError();
+        if (e != hipErrorNotReady) break;  // a failed stream: nothing of it is running any more
+        ++n;
+    }
+    return n;
 }
 
 // The age bound: launch what is queued once the oldest push is max_age_us old
@@ -1962,10 +2045,15 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(int alg, size_t stride, size_t l
             return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "strided batch needs stride % 16 == 0 (use the list API)");
         if (opt && opt->max_batches > (size_t)kMaxBatches)
             return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: max_batches above 32");
+        if (opt && opt->policy != AWS_CRT_AMD_QUEUE_EAGER && opt->policy != AWS_CRT_AMD_QUEUE_BATCHED)
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: unknown policy");
+        if (opt && opt->max_inflight > 8) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: max_inflight above 8");
         std::unique_ptr<aws_crt_amd_queue> q(new aws_crt_amd_queue);
         q->alg = alg, q->stride = stride, q->len = len, q->count = count, q->stream = hip_stream;
         if (opt && opt->max_batches) q->max_batches = opt->max_batches;
         if (opt) q->max_age_us = opt->max_age_us;
+        if (opt) q->eager = opt->policy == AWS_CRT_AMD_QUEUE_EAGER;
+        if (opt && opt->max_inflight) q->max_inflight = opt->max_inflight;
         if (hipGetDevice(&q->device) != hipSuccess) {
             (void)hipGetLastError();
             q->device = 0;
@@ -1996,7 +2084,10 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_push_ex(aws_crt_amd_queue *q, const void *
         q->pending.push_back({d_base, d_seeds, d_out});
         if (ticket) *ticket = q->next_ticket;
         ++q->next_ticket;
-        return q->pending.size() >= q->max_batches ? queue_flush_locked(q) : 0;
+        if (q->pending.size() >= q->max_batches) return queue_flush_locked(q);
+        // eager: the stream has room (none, or fewer than max_inflight, of the queue's launches running)
+        if (q->eager && queue_inflight_locked(q, q->max_inflight) < q->max_inflight) return queue_flush_locked(q);
+        return 0;
     });
 }
 
@@ -2016,6 +2107,12 @@ AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const aws_crt_amd_queue *q) {
     if (!q) return 0;
     std::lock_guard<std::mutex> g(const_cast<aws_crt_amd_queue *>(q)->mu);
     return q->pending.size();
+}
+
+AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_launches(const aws_crt_amd_queue *q) {
+    if (!q) return 0;
+    std::lock_guard<std::mutex> g(const_cast<aws_crt_amd_queue *>(q)->mu);
+    return q->nlaunches;
 }
 
 AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_first_pending(const aws_crt_amd_queue *q) {

@@ -24,12 +24,15 @@ one stream -- the interval rocprofv3's kernel trace reports.  `single_batch` giv
 for one-batch launches.  `traffic` is HBM bytes per launch from the committed rocprofv3 --pmc pass
 named in `traffic_source` (not measured in this run).
 
-Config legs (rank 0, N = 1; `configs`): C3 (16 x 256 MiB, CRC32 and CRC32C), C4's per-GPU shard
-(131072 x 8 KiB, 1/8 of 1M x 8 KiB; CRC32C and CRC64NVME), C5 (8 x 64 MiB, CRC64NVME and XXH64) and the north-star target
-shape (16 x 64 MiB CRC32C), each with value, kernel duration, roofline and cpu_baseline.  Never
-`value`.
+C4 (`configs.C4_crc32c`, `configs.C4_crc64nvme`; every N, every rank): the fixed set of 1,048,576 x
+8 KiB buffers, buffer i on rank i mod N (strong scaling), each rank's shard built on its own GPU; per-rank
+kernel fraction and parity sample, the gathered results' digest checked on rank 0, cpu_baseline on rank
+0's shard.  Config legs (rank 0, N = 1; `configs`): C3 (16 x 256 MiB, CRC32 and CRC32C), C5 (8 x 64 MiB,
+CRC64NVME and XXH64: the XXH64 host route's roofline is the PCIe D2H rate measured in the run, the kernel
+route beside it) and the north-star target shape (16 x 64 MiB CRC32C), each with value, kernel duration,
+roofline and cpu_baseline.  Never `value`.
 
-CPU baseline (`cpu_baseline`): the engine's own host path (csrc/cpu/: AVX-512
+CPU baseline (`cpu_baseline`; rank 0 at every N, after the timed region): the engine's own host path (csrc/cpu/: AVX-512
 VPCLMULQDQ / PCLMULQDQ folding, SSE4.2 crc32, vectorised XXH3 -- aws-checksums' technique class;
 aws-checksums itself cannot be built here) over a bounded sample of the same buffers, 1 thread and
 the box's CPU share (std::threads, buffers round-robin), median of >= 5 reps, CPU model stated,
@@ -76,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-read-ceiling", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C3 / C5 / target-shape legs")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 leg (the 1M x 8 KiB set sharded over the ranks)")
+    ap.add_argument("--c4-passes", type=int, default=3, help="timed passes over the C4 set")
     ap.add_argument("--e2e-batches", type=int, default=64, help="batches through the pinned-host pipeline (0: skip)")
     ap.add_argument("--inproc", action="store_true",
                     help="one process drives --gpus devices (the engine's in-process fan-out: one HIP stream per GPU, "
@@ -491,6 +496,71 @@ class E2EStep:
                     sample=f"one step ({self.nbuf} x {self.L} B) from pinned host memory, results to host memory")
 
 
+def d2h_rate(data, nbytes, dev, reps=3):
+    """GiB/s of plain device-to-pinned-host copies of nbytes (64 MiB pieces on one stream): the PCIe D2H
+    ceiling of this box, right now"""
+    import torch
+
+    piece = 64 << 20
+    host = torch.empty(min(nbytes, piece), dtype=torch.uint8, pin_memory=True)
+    cs = torch.cuda.Stream(device=dev)
+    rates = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(cs):
+            for off in range(0, nbytes, piece):
+                n = min(piece, nbytes - off)
+                host[:n].copy_(data[off:off + n], non_blocking=True)
+        torch.cuda.synchronize()
+        rates.append(nbytes / (time.perf_counter() - t0) / 2**30)
+    return statistics.median(rates[1:])
+
+
+def xxh64_route_roofline(eng, roof, data, step_bytes, per, dev):
+    """the XXH64 host route reads each byte once over PCIe (stream-ordered D2H
+    slices hashed by host threads), so its bound is the link's device-to-host rate, not
+    HBM.  peak = the D2H-only rate of the same bytes measured now; frac = the route's rate / that.  The
+    HBM fraction stays beside it as a side field."""
+    d2h = d2h_rate(data, per * step_bytes, dev)
+    ach = roof["achieved"]
+    peak = d2h * 2**30 / 1e9
+    return dict(roof, bound="pcie_d2h", peak=round(peak, 1), frac=round(ach / peak, 4), hbm_frac=roof["frac"],
+                peak_source="D2H-only rate of the same bytes into pinned host memory, measured in this run "
+                            f"({round(d2h, 2)} GiB/s)")
+
+
+def xxh64_kernel_route(eng, launch_group, outs, nb, steps, coalesce, streams, timing, step_bytes, per, nbuf, L):
+    """The same XXH64 leg on the gfx950 kernels (AWS_CRT_AMD_XXH64_ROUTE=0, read per call): the "same
+    kernel template" figure BASELINE configs[4] names, measured beside the route, with its results
+    checked against the route's"""
+    import torch
+
+    ref = [eng.as_unsigned(o) for o in outs]
+    os.environ["AWS_CRT_AMD_XXH64_ROUTE"] = "0"
+    try:
+        for o in outs:
+            o.zero_()
+        cuts = split(steps, coalesce)
+        for j in range(len(cuts) - 1):
+            launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for j in range(len(cuts) - 1):
+            launch_group(cuts[j], cuts[j + 1], streams[j % len(streams)])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kms, _ = time_launches(eng, lambda i, st: launch_group(i * per, i * per + per, st), streams[0], timing)
+        same = [eng.as_unsigned(o) for o in outs] == ref
+    finally:
+        del os.environ["AWS_CRT_AMD_XXH64_ROUTE"]
+    kn = "xxh64_row_kernel" if nbuf <= 1024 else "xxh64_wave_kernel"
+    return {"value": round(steps * step_bytes / el / 2**30, 2), "unit": "GiB/s",
+            "roofline": roofline(per * step_bytes, kms, kn), "parity_with_route": same,
+            "note": "AWS_CRT_AMD_XXH64_ROUTE=0: every buffer's serial XXH64 chain on the GPU (one wave per buffer); "
+                    "chain-latency bound, DESIGN.md §3.4"}
+
+
 def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2, timing=6, cpu_bufs=None,
                cpu_seconds=0.5, do_cpu=True, do_e2e=True):
     """One BASELINE config: `steps` steps of `nbuf` x L bytes (nb rotating batches), pipelined over
@@ -529,6 +599,10 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
     if alg == "xxh64":  # the host route is PCIe-bound: the link's state right after the timed launches
         bx = box_state(torch.cuda.get_device_properties(dev))
         rec["pcie_after"] = {"dpm": (bx.get("pcie") or {}).get("current"), "link": bx.get("link")}
+        if "host route" in rec["roofline"]["kernel"]:
+            rec["roofline"] = xxh64_route_roofline(eng, rec["roofline"], data, step_bytes, per, dev)
+            rec["kernel_route"] = xxh64_kernel_route(eng, launch_group, outs, nb, steps, coalesce, streams, timing,
+                                                     step_bytes, per, nbuf, L)
     trf = pmc_traffic(alg, nbuf, L, per)
     if trf:
         rec["roofline"]["traffic"], rec["roofline"]["traffic_source"] = trf
@@ -551,6 +625,95 @@ def config_leg(eng, name, alg, nbuf, L, streams, dev, coalesce=1, steps=12, nb=2
     del data
     torch.cuda.empty_cache()
     return rec
+
+
+def c4_leg(eng, args, dev, rank, world, streams, max_over_ranks, barrier, group_device, n=None, L=None, golden=None,
+           timer=None):
+    """BASELINE.json configs[3] as stated: the fixed set of 1,048,576 x 8 KiB
+    buffers (8 GiB), buffer i on rank i mod N -- strong scaling of one set over the job's GPUs.  Every
+    rank builds its shard on its own GPU (aws_crt_amd/synth.py: bytes are a function of the global
+    position, so every N scans the same set), scans it with one strided launch per pass, and reports
+    its kernel fraction and a parity sample (the engine's host path); rank 0 gathers every result in
+    buffer order (4-8 bytes per buffer) and checks the set's digest against tests/golden/c4_digest.json
+    (computed by the oracle on the CPU).  value = 8 GiB / the slowest rank's time per pass.
+    Returns {alg: record} on rank 0, None elsewhere.  (n, L, golden, timer: a smaller set and stand-ins
+    for the CPU plumbing test, tests/test_bench_plumbing.py.)"""
+    import torch
+
+    from aws_crt_amd import sharding, synth
+
+    n, L = n or synth.C4_COUNT, L or synth.C4_LEN
+    if golden is None:
+        golden = json.load(open(os.path.join(REPO, "tests", "golden", "c4_digest.json")))
+    timer = timer or time_launches
+    cnt = sharding.shard_count(n, rank, world)
+    data = torch.empty(cnt * L, dtype=torch.uint8, device=dev)
+    synth.fill_shard(data, rank, world, count=n, length=L)
+    sync = torch.cuda.synchronize if data.is_cuda else (lambda: None)
+    sync()
+    st = streams[0]
+    recs = {}
+    for alg in ("crc32c", "crc64nvme"):
+        sh = sharding.RoundRobinShard(eng, ALG[alg], data, n, L, rank, world)
+        sh.launch(st)  # warm-up (first launch of the shape)
+        sync()
+        reps = max(1, args.c4_passes)
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sh.launch(st)
+        sync()
+        own = (time.perf_counter() - t0) / reps
+        elapsed = max_over_ranks(own)
+        kms, _ = timer(eng, lambda i, s_: sh.launch(s_), st, max(2, args.timing_launches // 8))
+        # parity: a sample of this rank's buffers on the engine's host path; the whole set by digest
+        nchk = min(cnt, 1024)
+        hs = data[: nchk * L].cpu().numpy()
+        want = eng.cpu_batch(ALG[alg], [hs.ctypes.data + i * L for i in range(nchk)], [L] * nchk, threads=8)
+        sample_ok = eng.as_unsigned(sh.out)[:nchk] == want
+        allr = sh.gather(device=group_device)
+        digest = sharding.results_digest(eng, allr, sh.width) if rank == 0 else None
+        roof = roofline(cnt * L, kms, kernel_name(alg, cnt, L))
+        mine = {"rank": rank, "buffers": cnt, "value": round(cnt * L / own / 2**30, 2), "kernel_ms": roof["kernel_ms"],
+                "frac": roof["frac"], "parity_sample_buffers": nchk, "parity": sample_ok}
+        ranks = [None] * world
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_gather_object(ranks, mine)
+        else:
+            ranks = [mine]
+        if rank == 0:
+            want_digest = int(golden[alg]["digest"], 16)
+            value = n * L / elapsed / 2**30
+            recs[f"C4_{alg}"] = {
+                "workload": f"C4: {n} x {L >> 10} KiB {alg.upper()} ({n * L / 2**30:g} GiB), buffer i on rank i mod {world}, "
+                            f"device-resident, "
+                            f"one strided launch of {sharding.shard_count(n, 0, world)} buffers per rank per pass",
+                "value": round(value, 2), "unit": "GiB/s", "scaling": "strong", "n_gpus": world,
+                "per_gpu_gibs": round(value / world, 2), "passes": reps, "ms_per_pass": round(elapsed * 1e3, 4),
+                "pct_hbm_peak": round(100.0 * value * 2**30 / 1e9 / world / HBM_PEAK_GBS, 2),
+                "roofline": dict(roof, timing_launches=max(2, args.timing_launches // 8), rank=0),
+                "ranks": ranks,
+                "digest": hex(digest), "digest_expected": hex(want_digest), "digest_match": digest == want_digest,
+                "parity": digest == want_digest and all(r["parity"] for r in ranks),
+                "parity_rule": "gathered results in buffer order, CRC64NVME of the result words == "
+                               "tests/golden/c4_digest.json (oracle, CPU); plus 1024 buffers per rank on the host path"}
+            if not args.no_cpu_baseline:
+                # rank 0's shard (up to 131,072 buffers = 1 GiB, the 8-GPU shard) on the host cores,
+                # while the other ranks wait at the barrier below
+                cb = min(cnt, 131072)
+                host = host_sample(data, cb * L)
+                recs[f"C4_{alg}"]["cpu_baseline"] = cpu_baseline(eng, alg, host, cb, L, eng.as_unsigned(sh.out)[:cb],
+                                                                 args.cpu_seconds / 2, reps=3)
+                del host
+        barrier()
+        del sh
+    del data
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return recs if rank == 0 else None
 
 
 class E2EPinned:
@@ -879,25 +1042,42 @@ def main_rank(args):
                           "ms_per_step": round(el1 / args.steps * 1e3, 4),
                           "launch": f"one launch per batch, {args.steps} launches over {len(streams)} streams"}
 
-    # the same K steps pushed one at a time into a submission queue (aws_crt_amd_queue_*), which
-    # launches at 32 queued batches and at the flush: what a producer of one batch at a time gets
+    # the same K steps pushed one at a time into a submission queue (aws_crt_amd_queue_*): the rate a
+    # producer of one batch at a time gets.  The default (eager) policy launches a push at once when
+    # none of the queue's launches runs and coalesces pushes made while one does; beside it, a second
+    # launch allowed in flight, and round 5's batched policy (launch at 32 queued and at the flush).
+    # Median of 5 interleaved runs each; the eager default is the reported value.
     queued = None
     if G > 1 and args.steps > 0:
-        q = eng.Queue(ALG[alg], L, L, count, stream=streams[0])
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            b = rig.batch(i)
-            q.push(b[0], b[2])
-        q.flush()
-        torch.cuda.synchronize()
-        elq = max_over_ranks(time.perf_counter() - t0)
-        q.close()
-        queued = {"value": round(world * args.steps * step_bytes / max(elq, 1e-9) / 2**30, 2), "unit": "GiB/s",
-                  "ms_per_step": round(elq / args.steps * 1e3, 4),
-                  "launch": f"{args.steps} pushes of one batch into aws_crt_amd_queue (launch at 32 queued and at flush)"}
+        policies = (("eager", eng.QUEUE_EAGER, 1), ("eager_inflight2", eng.QUEUE_EAGER, 2),
+                    ("batched", eng.QUEUE_BATCHED, 0))
+        runs = {name: [] for name, _, _ in policies}
+        nl = {}
+        for rep in range(5):
+            for name, pol, depth in policies:
+                q = eng.Queue(ALG[alg], L, L, count, stream=streams[0], policy=pol, max_inflight=depth)
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    b = rig.batch(i)
+                    q.push(b[0], b[2])
+                q.flush()
+                torch.cuda.synchronize()
+                runs[name].append(max_over_ranks(time.perf_counter() - t0))
+                nl.setdefault(name, []).append(q.launches())
+                q.close()
+
+        def qrec(name):
+            el = statistics.median(runs[name])
+            return {"value": round(world * args.steps * step_bytes / max(el, 1e-9) / 2**30, 2), "unit": "GiB/s",
+                    "ms_per_step": round(el / args.steps * 1e3, 4), "launches": nl[name]}
+
+        queued = dict(qrec("eager"), launch=f"{args.steps} pushes of one batch into aws_crt_amd_queue, eager policy "
+                                           f"(launch on a push when none of the queue's launches runs; pushes made "
+                                           f"while one runs coalesce), then flush; median of 5",
+                      policies={name: qrec(name) for name, _, _ in policies})
 
     # every rank checks a sample of its own results against the engine's host path
     torch.cuda.synchronize()
@@ -936,10 +1116,25 @@ def main_rank(args):
     parity_all = all(r["parity"] for r in ranks)
     used = distinct_devices(ranks)
 
-    cpu = e2e = None
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # BASELINE configs[3] at every N: the fixed 1M x 8 KiB set, buffer i on rank i mod N (all ranks)
     configs = {}
-    if rank == 0 and world == 1:
-        e2e_legs = E2EPinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches) if args.e2e_batches > 0 else None
+    if not args.no_c4:
+        c4 = c4_leg(eng, args, dev, rank, world, streams, max_over_ranks, barrier,
+                    dev if world > 1 and args.dist_backend == "nccl" else None)
+        if rank == 0:
+            configs.update(c4)
+            parity_all = parity_all and all(v["parity"] for v in c4.values())
+
+    cpu = e2e = None
+    if rank == 0:
+        # the CPU baseline on rank 0's host cores at every N (the other ranks wait at the barrier below);
+        # the pinned-host legs and the single-GPU config legs at N = 1
+        e2e_legs = (E2EPinned(eng, ALG[alg], data, count, L, nb, args.e2e_batches)
+                    if args.e2e_batches > 0 and world == 1 else None)
         if not args.no_cpu_baseline:
             # the sample: every resident batch (as many bytes as the timed region streams, more than
             # the host's last-level cache, as the GPU's reads are beyond its caches), with one step
@@ -952,6 +1147,8 @@ def main_rank(args):
         if e2e_legs is not None:
             e2e = e2e_legs.record()
             del e2e_legs
+    barrier()
+    if rank == 0 and world == 1:
         if not args.no_configs:
             del data, rig
             torch.cuda.empty_cache()
@@ -959,10 +1156,6 @@ def main_rank(args):
             legs = {"do_cpu": do_cpu, "do_e2e": args.e2e_batches > 0}
             configs["C3_crc32c"] = config_leg(eng, "C3", "crc32c", 16, 256 << 20, streams, dev, **legs)
             configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, **legs)
-            configs["C4_shard_crc32c"] = config_leg(eng, "C4 per-GPU shard", "crc32c", 131072, 8192, streams, dev,
-                                                    steps=20, **legs)
-            configs["C4_shard_crc64nvme"] = config_leg(eng, "C4 per-GPU shard", "crc64nvme", 131072, 8192, streams, dev,
-                                                       steps=20, **legs)
             configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, **legs)
             configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, **legs)
             configs["target_16x64MiB_crc32c"] = config_leg(eng, "north-star target", "crc32c", 16, 64 << 20, streams, dev,

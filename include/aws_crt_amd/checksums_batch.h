@@ -171,11 +171,15 @@ AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(struct aws_crt_amd_plan *plan);
 
 /*
  * Submission queue: a producer that gets one uniform batch at a time (aws-c-s3 checksumming parts as
- * they arrive, source/s3/S3.cpp:1133-1149) pushes each batch and the engine launches them together:
- * a push queues (base, seeds, out) without launching; the queue launches on its stream when it holds
- * 32 batches (one launch, as aws_crt_amd_checksum_batches), and at aws_crt_amd_queue_flush or
- * aws_crt_amd_queue_destroy.  Work is on the stream only after the launch that holds it: a caller
- * that synchronises the stream, records an event on it or reads a result flushes first.  Every
+ * they arrive, source/s3/S3.cpp:1133-1149) pushes each batch and the engine launches them together.
+ * Default (eager) policy, round 6: a push that finds none of the queue's launches still running on its
+ * stream launches at once, with every batch queued so far; batches pushed while a launch runs coalesce
+ * and go out with the first push that finds it done, at 32 queued batches, or at
+ * aws_crt_amd_queue_flush / _wait / _destroy (or the age bound, below).  So the GPU is never left idle
+ * while batches wait, and a busy GPU gets them in ever larger launches (one launch of up to 32, as
+ * aws_crt_amd_checksum_batches).  The batched policy (options below) launches only at max_batches, the
+ * age bound, flush, wait or destroy.  Work is on the stream only after the launch that holds it: a
+ * caller that synchronises the stream, records an event on it or reads a result flushes first.  Every
  * batch of a queue has the queue's algorithm and shape (stride, len, count).  Push, flush, pending,
  * status and wait may be called from several threads; destroy must not overlap any other call on the
  * same queue.  A refused launch (e.g. a HIP error) drops the batches it held: the push or flush that
@@ -197,10 +201,13 @@ AWS_CRT_AMD_API size_t aws_crt_amd_queue_pending(const struct aws_crt_amd_queue 
 AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
 
 /*
- * Queue policy and per-push completion (round 4).
+ * Queue policy and per-push completion (round 4; policy and max_inflight round 6).
  *   max_batches  launch when this many batches are queued (1..32; 0 = 32)
  *   max_age_us   0 = no age bound; otherwise a flusher thread launches the queued batches once the
  *                oldest has waited this long, so no push waits for later pushes indefinitely
+ *   policy       AWS_CRT_AMD_QUEUE_EAGER (0, the default) or AWS_CRT_AMD_QUEUE_BATCHED (1)
+ *   max_inflight eager policy: a push launches while fewer than this many of the queue's launches
+ *                are running (1..8; 0 = 1)
  * Each push_ex returns a ticket (1, 2, ... per queue).  queue_status(ticket):
  *   AWS_CRT_AMD_TICKET_QUEUED    pushed, not launched yet
  *   AWS_CRT_AMD_TICKET_LAUNCHED  on the stream, not complete
@@ -216,9 +223,12 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
  * been launched or refused).  Status and wait may be called from any thread.
  */
 enum { AWS_CRT_AMD_TICKET_QUEUED = 1, AWS_CRT_AMD_TICKET_LAUNCHED = 2 };
+enum { AWS_CRT_AMD_QUEUE_EAGER = 0, AWS_CRT_AMD_QUEUE_BATCHED = 1 };
 struct aws_crt_amd_queue_options {
     size_t max_batches;
     uint64_t max_age_us;
+    uint32_t policy;
+    uint32_t max_inflight;
 };
 AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(
     int algorithm,
@@ -237,6 +247,8 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_push_ex(
 AWS_CRT_AMD_API int aws_crt_amd_queue_status(struct aws_crt_amd_queue *queue, uint64_t ticket);
 AWS_CRT_AMD_API int aws_crt_amd_queue_wait(struct aws_crt_amd_queue *queue, uint64_t ticket);
 AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_first_pending(const struct aws_crt_amd_queue *queue);
+/* launches the queue has made so far (refused ones included) */
+AWS_CRT_AMD_API uint64_t aws_crt_amd_queue_launches(const struct aws_crt_amd_queue *queue);
 
 /*
  * Ragged batch: buffer i = [d_ptrs[i], + lens[i]).  d_ptrs and lens are HOST arrays describing

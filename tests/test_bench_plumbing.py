@@ -86,3 +86,124 @@ def test_split_is_weak_scaling_per_rank():
     assert bench.split(20, 32) == [0, 20]
     assert bench.split(20, 1) == list(range(21))
     assert bench.widest(200, 32) == 29
+
+
+class _HostEngine:
+    """The engine with checksum_strided served by its own host path on CPU tensors: bench.py's C4 leg
+    driven without a GPU (the record's plumbing, not a measurement)"""
+
+    def __init__(self):
+        import aws_crt_amd
+
+        self._e = aws_crt_amd
+
+    def __getattr__(self, k):
+        return getattr(self._e, k)
+
+    def checksum_strided(self, alg, base, stride, length, count, seeds=None, out=None, stream=None):
+        import torch
+
+        vals = self._e.cpu_batch(alg, [base.data_ptr() + i * stride for i in range(count)], [length] * count, threads=4)
+        bits = 64 if out.dtype == torch.int64 else 32
+        out.copy_(torch.tensor([v - (1 << bits) if v >> (bits - 1) else v for v in vals], dtype=out.dtype))
+        return out
+
+
+def _c4_golden(n, L):
+    from aws_crt_amd import synth
+    from oracle import oracle
+
+    buf = synth.buffers_np(0, n, L)
+    g = {}
+    for alg, w in (("crc32c", "<u4"), ("crc64nvme", "<u8")):
+        res = oracle.batch(alg, [buf.ctypes.data + i * L for i in range(n)], [L] * n, 4)
+        import numpy as np
+
+        g[alg] = {"digest": hex(oracle.crc("crc64nvme", np.asarray(res, dtype=np.uint64).astype(w).tobytes()))}
+    return g
+
+
+def _c4_args():
+    import argparse
+
+    return argparse.Namespace(c4_passes=1, timing_launches=8, no_cpu_baseline=False, cpu_seconds=0.05)
+
+
+def _fake_timer(eng, launch, st, nt):
+    launch(0, st)
+    return 0.5, 0.5
+
+
+def _check_c4_records(recs, world, n):
+    assert set(recs) == {"C4_crc32c", "C4_crc64nvme"}
+    for r in recs.values():
+        assert r["digest_match"] is True and r["parity"] is True, r
+        assert r["scaling"] == "strong" and r["n_gpus"] == world and r["value"] > 0
+        assert [x["rank"] for x in r["ranks"]] == list(range(world))
+        assert sum(x["buffers"] for x in r["ranks"]) == n
+        assert r["cpu_baseline"] is not None and r["cpu_baseline"]["value"] > 0
+        assert r["cpu_baseline"]["parity_with_gpu"] is True
+        assert r["roofline"]["bound"] == "hbm" and 0 < r["roofline"]["frac"]
+
+
+def test_c4_leg_record_world1_cpu():
+    """bench.py's C4 leg (the fixed set, buffer i on rank i mod N) assembles its
+    record -- digest of the gathered results against the golden rule, per-rank records, cpu_baseline --
+    here on a 2,048-buffer set with the host path standing in for the kernels"""
+    import torch
+
+    import bench
+
+    n, L = 2048, 8192
+    recs = bench.c4_leg(_HostEngine(), _c4_args(), torch.device("cpu"), 0, 1, [None], lambda x: x, lambda: None, None,
+                        n=n, L=L, golden=_c4_golden(n, L), timer=_fake_timer)
+    _check_c4_records(recs, 1, n)
+
+
+def _c4_rank(rank, world, port, q, golden):
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def mx(x):
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    try:
+        recs = bench.c4_leg(_HostEngine(), _c4_args(), torch.device("cpu"), rank, world, [None], mx, dist.barrier, None,
+                            n=2047, L=8192, golden=golden, timer=_fake_timer)
+        q.put((rank, recs))
+    except Exception as e:
+        q.put((rank, repr(e)))
+    dist.destroy_process_group()
+
+
+def test_c4_leg_record_two_gloo_ranks_cpu():
+    """the same leg at world 2 over gloo: each rank builds and scans its own shard (odd set size:
+    unequal shards), rank 0 gathers every result and carries both ranks' records"""
+    import random
+
+    import torch.multiprocessing as mp
+
+    n, L = 2047, 8192
+    golden = _c4_golden(n, L)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 32800 + random.Random().randrange(1000)
+    procs = [ctx.Process(target=_c4_rank, args=(r, 2, port, q, golden)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert res[1] is None, res[1]
+    assert isinstance(res[0], dict), res[0]
+    _check_c4_records(res[0], 2, n)

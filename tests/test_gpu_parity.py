@@ -531,8 +531,8 @@ def test_ragged_list_workgroup_joins(engine, alg, nbuf, lo, hi):
 @pytest.mark.parametrize("alg", ["crc32", "crc32c", "crc64nvme"])
 def test_list_masked_edges(engine, alg):
     """Round 5: the list streaming scans read a buffer of >= 16 bytes as the 8-byte words covering it
-    and clear the bytes outside it in the registers (the head state enters times x^(-8 o), the
-    register leaves times x^(-8 k)).  Every start offset mod 8 against lengths at the threshold
+    and clear the bytes in front of it in the registers (the head state enters times x^(-8 o)); the
+    tail (< 8 bytes past the last whole word) is folded.  Every start offset mod 8 against lengths at the threshold
     (15, 16, 17), around one and two words, around a 4 KiB group and a 512-byte row, neighbours
     packed with no gap (the masked bytes are the neighbours' data), one 1 MiB buffer so that the
     list takes the streaming scan; seeds on all."""

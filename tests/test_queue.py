@@ -1,11 +1,14 @@
 """The submission queue (include/aws_crt_amd/checksums_batch.h, aws_crt_amd_queue_*): batches of one
-shape pushed one at a time are launched together -- at 32 queued batches, at flush and at destroy --
-so a producer that gets one part batch at a time (aws-c-s3's part Write, source/s3/S3.cpp:1133-1149)
-reaches the multi-batch launch rate without building batch arrays itself.
+shape pushed one at a time are launched together, so a producer that gets one part batch at a time
+(aws-c-s3's part Write, source/s3/S3.cpp:1133-1149) reaches the multi-batch launch rate without
+building batch arrays itself.  Eager policy (default, round 6): a push that finds the queue's stream
+free launches at once; pushes made while a launch runs coalesce into the next one.  Batched policy: at
+32 queued batches, at flush and at destroy only.
 
-CPU: the queue's host logic with no device visible (pushes queue without launching, a flush then
-reports AWS_CRT_AMD_ERR_NO_DEVICE and empties the queue, argument checks).  GPU: results of queued
-batches against the oracle, the automatic launch at 32, CRC64NVME long buffers, hashes, seeds.
+CPU: the queue's host logic with no device visible (batched: pushes queue without launching, a flush
+then reports AWS_CRT_AMD_ERR_NO_DEVICE and empties the queue; eager: every push launches -- refused --
+at once; argument checks).  GPU: results of queued batches against the oracle, the automatic launch at
+32, CRC64NVME long buffers, hashes, seeds, eager launches and their tickets.
 """
 import os
 import random
@@ -22,10 +25,13 @@ ALG = {"crc32": 0, "crc32c": 1, "crc64nvme": 2, "xxh64": 3, "xxh3_64": 4, "xxh3_
 
 
 def test_queue_host_logic_without_device():
+    """the batched policy without a device: pushes queue, the flush's launch is refused"""
     code = (
         LOAD_SRC +
-        "vp=ctypes.c_void_p; sz=ctypes.c_size_t\n"
-        "L.aws_crt_amd_queue_create.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(vp)]\n"
+        "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
+        "L.aws_crt_amd_queue_create=lambda a,st,l,c,s_,q: L.aws_crt_amd_queue_create_ex(a,st,l,c,s_,ctypes.byref(O(0,0,1,0)),q)\n"
         "L.aws_crt_amd_queue_push.argtypes=[vp,vp,vp,vp]\n"
         "L.aws_crt_amd_queue_flush.argtypes=[vp]\n"
         "L.aws_crt_amd_queue_pending.argtypes=[vp]; L.aws_crt_amd_queue_pending.restype=sz\n"
@@ -48,6 +54,42 @@ def test_queue_host_logic_without_device():
                    "flush": "-1", "pending_after": "0", "destroy_empty": "0"}
 
 
+def test_queue_eager_policy_without_device():
+    """the default (eager) policy without a device: nothing of the queue is running, so every push
+    launches at once -- refused (AWS_CRT_AMD_ERR_NO_DEVICE), reported by the push and by its ticket --
+    and nothing stays pending; unknown policies and depths are refused at create"""
+    code = (
+        LOAD_SRC +
+        "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "L.aws_crt_amd_queue_create.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(vp)]\n"
+        "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
+        "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
+        "L.aws_crt_amd_queue_status.argtypes=[vp,u64]\n"
+        "L.aws_crt_amd_queue_pending.argtypes=[vp]; L.aws_crt_amd_queue_pending.restype=sz\n"
+        "L.aws_crt_amd_queue_launches.argtypes=[vp]; L.aws_crt_amd_queue_launches.restype=u64\n"
+        "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
+        "q=vp(); t=u64()\n"
+        "print('bad_policy', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,2,0)),ctypes.byref(q)))\n"
+        "print('bad_depth', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,9)),ctypes.byref(q)))\n"
+        "print('create', L.aws_crt_amd_queue_create(1,65536,65536,4,None,ctypes.byref(q)))\n"
+        "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(5)]\n"
+        "print('push_rcs', ','.join(map(str,r)), 'pending', L.aws_crt_amd_queue_pending(q), 'launches', L.aws_crt_amd_queue_launches(q))\n"
+        "print('st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,6)))\n"
+        "print('destroy', L.aws_crt_amd_queue_destroy(q))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+    assert r.returncode == 0, r.stderr
+    got = {}
+    for line in r.stdout.split("\n"):
+        f = line.split()
+        for i in range(0, len(f) - 1, 2):
+            got[f[i]] = f[i + 1]
+    assert got["bad_policy"] == "-2" and got["bad_depth"] == "-2" and got["create"] == "0"
+    assert got["push_rcs"] == "-1,-1,-1,-1,-1" and got["pending"] == "0" and got["launches"] == "5"
+    assert got["st"] == "-1,-1,-1,-1,-1" and got["destroy"] == "0"
+
+
 def test_queue_tickets_refused_launch_and_age_flush_without_device():
     """Tickets and completion without a device: every batch of a refused launch reports the launch's
     error (AWS_CRT_AMD_ERR_NO_DEVICE) through its ticket, queued tickets report QUEUED, unknown
@@ -55,7 +97,7 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
     code = (
         LOAD_SRC + "import time\n"
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
         "L.aws_crt_amd_queue_status.argtypes=[vp,u64]; L.aws_crt_amd_queue_wait.argtypes=[vp,u64]\n"
@@ -63,8 +105,8 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
         "L.aws_crt_amd_queue_first_pending.argtypes=[vp]; L.aws_crt_amd_queue_first_pending.restype=u64\n"
         "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
         "q=vp(); t=u64()\n"
-        "print('too_many', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(33,0)),ctypes.byref(q)))\n"
-        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(3,0)),ctypes.byref(q)))\n"
+        "print('too_many', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(33,0,1,0)),ctypes.byref(q)))\n"
+        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(3,0,1,0)),ctypes.byref(q)))\n"
         "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(4)]\n"
         "print('push_rcs', ','.join(map(str,r)), 'last_ticket', t.value)\n"
         "print('st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,5)))\n"
@@ -72,7 +114,7 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
         "print('first_pending', L.aws_crt_amd_queue_first_pending(q))\n"
         "print('wait4', L.aws_crt_amd_queue_wait(q,4), 'pending', L.aws_crt_amd_queue_pending(q))\n"
         "print('destroy', L.aws_crt_amd_queue_destroy(q))\n"
-        "print('create_age', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,2000)),ctypes.byref(q)))\n"
+        "print('create_age', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,2000,1,0)),ctypes.byref(q)))\n"
         "for i in range(3): L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t))\n"
         "dl=time.time()+5\n"
         "while L.aws_crt_amd_queue_pending(q) and time.time()<dl: time.sleep(0.002)\n"
@@ -115,7 +157,7 @@ def test_queue_crc32c_auto_launch_and_flush(engine):
     rng = random.Random(0x9E)
     seeds = {j: [rng.getrandbits(32) for _ in range(n)] for j in (3, 33)}
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(nb)]
-    q = engine.Queue(ALG["crc32c"], L, L, n)
+    q = engine.Queue(ALG["crc32c"], L, L, n, policy=engine.QUEUE_BATCHED)
     for j in range(nb):
         st = torch.tensor([v - (1 << 32) if v >= 1 << 31 else v for v in seeds[j]], dtype=torch.int32,
                           device="cuda") if j in seeds else None
@@ -144,7 +186,7 @@ def test_queue_close_flushes(engine, alg, n, L):
     nb = 3
     d = _dev_random(n * L * nb, 0x9F)
     outs = [torch.empty(n, dtype=torch.int64, device="cuda") for _ in range(nb)]
-    q = engine.Queue(ALG[alg], L, L, n)
+    q = engine.Queue(ALG[alg], L, L, n, policy=engine.QUEUE_BATCHED)
     for j in range(nb):
         q.push(d[j * n * L:], outs[j])
     assert q.pending() == nb
@@ -172,7 +214,7 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
     d = _dev_random(n * L * 4, 0xA1)
     h = d.cpu().numpy()
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(4)]
-    q = engine.Queue(ALG["crc32c"], L, L, n, max_batches=2)
+    q = engine.Queue(ALG["crc32c"], L, L, n, max_batches=2, policy=engine.QUEUE_BATCHED)
     t = [q.push(d[j * n * L:], outs[j]) for j in range(3)]
     assert t == [1, 2, 3] and q.status(3) == engine.TICKET_QUEUED
     assert q.wait(1) == 0 and q.wait(3) == 0 and q.status(2) == 0
@@ -180,7 +222,7 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
         assert engine.as_unsigned(outs[j])[5] == oracle.crc("crc32c", h[(j * n + 5) * L:(j * n + 6) * L]), j
     q.close()
     # age bound: a single push is launched by the flusher
-    qa = engine.Queue(ALG["crc32c"], L, L, n, max_age_us=500)
+    qa = engine.Queue(ALG["crc32c"], L, L, n, max_age_us=500, policy=engine.QUEUE_BATCHED)
     ta = qa.push(d[3 * n * L:], outs[3])
     deadline = time.time() + 5
     while qa.pending() and time.time() < deadline:
@@ -197,7 +239,7 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
     g = torch.cuda.CUDAGraph()
     qr = None
     with torch.cuda.graph(g, stream=cs):
-        qr = engine.Queue(ALG["crc32c"], 6 << 30, 6 << 30, 1, stream=cs)
+        qr = engine.Queue(ALG["crc32c"], 6 << 30, 6 << 30, 1, stream=cs, policy=engine.QUEUE_BATCHED)
         tr = [qr.push(big, bo[j]) for j in range(2)]
         with pytest.raises(engine.EngineError):
             qr.flush()
@@ -205,6 +247,39 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
     assert qr.wait(tr[1]) == -2
     qr.close()
     del big
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [1, 2])
+def test_queue_eager_launches(engine, depth):
+    """the eager policy launches a push at once when nothing of the queue runs
+    (the first push leaves nothing pending), coalesces the pushes made while launches run (fewer
+    launches than pushes: a one-batch launch of 64 MiB takes ~15 us, a push a few), and every ticket
+    completes with results equal to the oracle; the flush launches the rest."""
+    import torch
+
+    n, L, nb = 1024, 65536, 60  # C2 batches (64 MiB), 6 resident ones reused (the results are per push)
+    d = _dev_random(n * L * 6, 0xE1)
+    outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(nb)]
+    q = engine.Queue(ALG["crc32c"], L, L, n, max_inflight=depth)
+    tickets = []
+    for j in range(nb):
+        tickets.append(q.push(d[(j % 6) * n * L:], outs[j]))
+        if j == 0:
+            assert q.pending() == 0 and q.launches() == 1
+    q.flush()
+    assert q.pending() == 0
+    launches = q.launches()
+    assert 2 <= launches < nb, launches
+    assert all(q.wait(t) == 0 for t in tickets)
+    assert all(q.status(t) == 0 for t in tickets)
+    q.close()
+    h = d.cpu().numpy()
+    for j in range(0, nb, 7):
+        got = engine.as_unsigned(outs[j])
+        for i in (0, n // 2, n - 1):
+            o = ((j % 6) * n + i) * L
+            assert got[i] == oracle.crc("crc32c", h[o:o + L]), (j, i)
 
 
 def test_queue_refused_tickets_never_report_complete():
@@ -215,13 +290,13 @@ def test_queue_refused_tickets_never_report_complete():
     code = (
         LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
         "L.aws_crt_amd_queue_status.argtypes=[vp,u64]\n"
         "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
         "q=vp(); t=u64()\n"
-        "assert L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(1,0)),ctypes.byref(q))==0\n"
+        "assert L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(1,0,1,0)),ctypes.byref(q))==0\n"
         "rc=[L.aws_crt_amd_queue_push_ex(q,4096,None,8192,ctypes.byref(t)) for i in range(3000)]\n"
         "st=[L.aws_crt_amd_queue_status(q,k) for k in range(1,3001)]\n"
         "print('pushes', set(rc), 'status', sorted(set(st)), 'last', t.value)\n"
