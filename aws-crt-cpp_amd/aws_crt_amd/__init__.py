@@ -314,7 +314,7 @@ def checksum_batches(alg: int, batches, stride: int, length: int, count: int, st
 
 class _QueueOptions(ctypes.Structure):
     _fields_ = [("max_batches", ctypes.c_size_t), ("max_age_us", ctypes.c_uint64), ("policy", ctypes.c_uint32),
-                ("max_inflight", ctypes.c_uint32)]
+                ("max_inflight", ctypes.c_uint32), ("min_launch", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 TICKET_QUEUED, TICKET_LAUNCHED = 1, 2
@@ -324,7 +324,7 @@ QUEUE_EAGER, QUEUE_BATCHED = 0, 1
 class Queue:
     """A submission queue (aws_crt_amd_queue_*): batches of one shape pushed one at a time are launched
     together.  policy QUEUE_EAGER (default): a push that finds fewer than max_inflight (default 1) of the
-    queue's launches running launches everything queued at once; QUEUE_BATCHED: only at max_batches
+    queue's launches running launches everything queued at once (once at least min_launch are queued); QUEUE_BATCHED: only at max_batches
     queued (32 by default), once the oldest has waited max_age_us (0: no age bound), and at flush() /
     wait() / close() (which also launch under the eager policy).  push() returns the batch's ticket;
     status(ticket) / wait(ticket) give its completion (0) or the error of the launch that dropped it.
@@ -332,7 +332,7 @@ class Queue:
     first_pending()); thread-safe."""
 
     def __init__(self, alg: int, stride: int, length: int, count: int, stream=None, max_batches: int = 0,
-                 max_age_us: int = 0, policy: int = QUEUE_EAGER, max_inflight: int = 0):
+                 max_age_us: int = 0, policy: int = QUEUE_EAGER, max_inflight: int = 0, min_launch: int = 0):
         import threading
 
         L = lib()
@@ -355,7 +355,7 @@ class Queue:
         self._keep = {}  # ticket -> tensors, until the ticket is launched
         self._lock = threading.Lock()
         h = vp()
-        opt = _QueueOptions(max_batches, max_age_us, policy, max_inflight)
+        opt = _QueueOptions(max_batches, max_age_us, policy, max_inflight, min_launch, 0)
         _check(L.aws_crt_amd_queue_create_ex(alg, stride, length, count, _stream_handle(stream), ctypes.byref(opt),
                                              ctypes.byref(h)))
         self._h = h

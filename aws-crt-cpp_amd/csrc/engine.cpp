@@ -1897,6 +1897,7 @@ AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(aws_crt_amd_plan *pl) { delete pl;
 // below one launch per batch).  Every push gets a ticket; each launch records an event after it on
 // the queue's stream, so a ticket's completion (or the error of the launch that dropped it) can be
 // asked for and waited on -- and the eager policy asks the newest events whether the stream is busy.
+constexpr size_t kQueueMinLaunch = 1;  // eager launches' default minimum batch count
 struct aws_crt_amd_queue {
     int alg = 0;
     int device = 0;
@@ -1906,6 +1907,7 @@ struct aws_crt_amd_queue {
     uint64_t max_age_us = 0;
     bool eager = true;        // AWS_CRT_AMD_QUEUE_EAGER
     size_t max_inflight = 1;  // eager: launch on a push while fewer of the queue's launches are running
+    size_t min_launch = kQueueMinLaunch;  // eager: ... and at least this many batches are queued
     uint64_t nlaunches = 0;   // launches made (refused ones included)
     std::mutex mu;
     std::condition_variable cv;
@@ -2048,12 +2050,15 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(int alg, size_t stride, size_t l
         if (opt && opt->policy != AWS_CRT_AMD_QUEUE_EAGER && opt->policy != AWS_CRT_AMD_QUEUE_BATCHED)
             return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: unknown policy");
         if (opt && opt->max_inflight > 8) return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: max_inflight above 8");
+        if (opt && (opt->min_launch > (uint32_t)kMaxBatches || opt->reserved))
+            return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "queue: min_launch above 32 or reserved field set");
         std::unique_ptr<aws_crt_amd_queue> q(new aws_crt_amd_queue);
         q->alg = alg, q->stride = stride, q->len = len, q->count = count, q->stream = hip_stream;
         if (opt && opt->max_batches) q->max_batches = opt->max_batches;
         if (opt) q->max_age_us = opt->max_age_us;
         if (opt) q->eager = opt->policy == AWS_CRT_AMD_QUEUE_EAGER;
         if (opt && opt->max_inflight) q->max_inflight = opt->max_inflight;
+        if (opt && opt->min_launch) q->min_launch = opt->min_launch;
         if (hipGetDevice(&q->device) != hipSuccess) {
             (void)hipGetLastError();
             q->device = 0;
@@ -2086,7 +2091,8 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_push_ex(aws_crt_amd_queue *q, const void *
         ++q->next_ticket;
         if (q->pending.size() >= q->max_batches) return queue_flush_locked(q);
         // eager: the stream has room (none, or fewer than max_inflight, of the queue's launches running)
-        if (q->eager && queue_inflight_locked(q, q->max_inflight) < q->max_inflight) return queue_flush_locked(q);
+        if (q->eager && q->pending.size() >= q->min_launch && queue_inflight_locked(q, q->max_inflight) < q->max_inflight)
+            return queue_flush_locked(q);
         return 0;
     });
 }

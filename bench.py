@@ -1049,13 +1049,14 @@ def main_rank(args):
     # Median of 5 interleaved runs each; the eager default is the reported value.
     queued = None
     if G > 1 and args.steps > 0:
-        policies = (("eager", eng.QUEUE_EAGER, 1), ("eager_inflight2", eng.QUEUE_EAGER, 2),
-                    ("batched", eng.QUEUE_BATCHED, 0))
-        runs = {name: [] for name, _, _ in policies}
+        policies = (("eager", eng.QUEUE_EAGER, 0, 0), ("eager_min2", eng.QUEUE_EAGER, 1, 2),
+                    ("eager_min4", eng.QUEUE_EAGER, 1, 4), ("eager_inflight2", eng.QUEUE_EAGER, 2, 1),
+                    ("batched", eng.QUEUE_BATCHED, 0, 0))
+        runs = {name: [] for name, _, _, _ in policies}
         nl = {}
         for rep in range(5):
-            for name, pol, depth in policies:
-                q = eng.Queue(ALG[alg], L, L, count, stream=streams[0], policy=pol, max_inflight=depth)
+            for name, pol, depth, mn in policies:
+                q = eng.Queue(ALG[alg], L, L, count, stream=streams[0], policy=pol, max_inflight=depth, min_launch=mn)
                 if world > 1:
                     dist.barrier()
                 torch.cuda.synchronize()
@@ -1077,7 +1078,7 @@ def main_rank(args):
         queued = dict(qrec("eager"), launch=f"{args.steps} pushes of one batch into aws_crt_amd_queue, eager policy "
                                            f"(launch on a push when none of the queue's launches runs; pushes made "
                                            f"while one runs coalesce), then flush; median of 5",
-                      policies={name: qrec(name) for name, _, _ in policies})
+                      policies={name: qrec(name) for name, _, _, _ in policies})
 
     # every rank checks a sample of its own results against the engine's host path
     torch.cuda.synchronize()

@@ -208,6 +208,8 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
  *   policy       AWS_CRT_AMD_QUEUE_EAGER (0, the default) or AWS_CRT_AMD_QUEUE_BATCHED (1)
  *   max_inflight eager policy: a push launches while fewer than this many of the queue's launches
  *                are running (1..8; 0 = 1)
+ *   min_launch   eager policy: a push launches only with at least this many batches queued (1..32;
+ *                0 = the default, 1); fewer wait for a later push, flush, wait, destroy or the age bound
  * Each push_ex returns a ticket (1, 2, ... per queue).  queue_status(ticket):
  *   AWS_CRT_AMD_TICKET_QUEUED    pushed, not launched yet
  *   AWS_CRT_AMD_TICKET_LAUNCHED  on the stream, not complete
@@ -229,6 +231,8 @@ struct aws_crt_amd_queue_options {
     uint64_t max_age_us;
     uint32_t policy;
     uint32_t max_inflight;
+    uint32_t min_launch;
+    uint32_t reserved; /* 0 */
 };
 AWS_CRT_AMD_API int aws_crt_amd_queue_create_ex(
     int algorithm,

@@ -29,9 +29,9 @@ def test_queue_host_logic_without_device():
     code = (
         LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32),('min_launch',ctypes.c_uint32),('reserved',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
-        "L.aws_crt_amd_queue_create=lambda a,st,l,c,s_,q: L.aws_crt_amd_queue_create_ex(a,st,l,c,s_,ctypes.byref(O(0,0,1,0)),q)\n"
+        "L.aws_crt_amd_queue_create=lambda a,st,l,c,s_,q: L.aws_crt_amd_queue_create_ex(a,st,l,c,s_,ctypes.byref(O(0,0,1,0,0,0)),q)\n"
         "L.aws_crt_amd_queue_push.argtypes=[vp,vp,vp,vp]\n"
         "L.aws_crt_amd_queue_flush.argtypes=[vp]\n"
         "L.aws_crt_amd_queue_pending.argtypes=[vp]; L.aws_crt_amd_queue_pending.restype=sz\n"
@@ -61,7 +61,7 @@ def test_queue_eager_policy_without_device():
     code = (
         LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32),('min_launch',ctypes.c_uint32),('reserved',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
@@ -70,8 +70,8 @@ def test_queue_eager_policy_without_device():
         "L.aws_crt_amd_queue_launches.argtypes=[vp]; L.aws_crt_amd_queue_launches.restype=u64\n"
         "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
         "q=vp(); t=u64()\n"
-        "print('bad_policy', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,2,0)),ctypes.byref(q)))\n"
-        "print('bad_depth', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,9)),ctypes.byref(q)))\n"
+        "print('bad_policy', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,2,0,0,0)),ctypes.byref(q)))\n"
+        "print('bad_depth', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,9,0,0)),ctypes.byref(q)))\n"
         "print('create', L.aws_crt_amd_queue_create(1,65536,65536,4,None,ctypes.byref(q)))\n"
         "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(5)]\n"
         "print('push_rcs', ','.join(map(str,r)), 'pending', L.aws_crt_amd_queue_pending(q), 'launches', L.aws_crt_amd_queue_launches(q))\n"
@@ -97,7 +97,7 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
     code = (
         LOAD_SRC + "import time\n"
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32),('min_launch',ctypes.c_uint32),('reserved',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
         "L.aws_crt_amd_queue_status.argtypes=[vp,u64]; L.aws_crt_amd_queue_wait.argtypes=[vp,u64]\n"
@@ -105,8 +105,8 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
         "L.aws_crt_amd_queue_first_pending.argtypes=[vp]; L.aws_crt_amd_queue_first_pending.restype=u64\n"
         "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
         "q=vp(); t=u64()\n"
-        "print('too_many', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(33,0,1,0)),ctypes.byref(q)))\n"
-        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(3,0,1,0)),ctypes.byref(q)))\n"
+        "print('too_many', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(33,0,1,0,0,0)),ctypes.byref(q)))\n"
+        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(3,0,1,0,0,0)),ctypes.byref(q)))\n"
         "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(4)]\n"
         "print('push_rcs', ','.join(map(str,r)), 'last_ticket', t.value)\n"
         "print('st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,5)))\n"
@@ -114,7 +114,7 @@ def test_queue_tickets_refused_launch_and_age_flush_without_device():
         "print('first_pending', L.aws_crt_amd_queue_first_pending(q))\n"
         "print('wait4', L.aws_crt_amd_queue_wait(q,4), 'pending', L.aws_crt_amd_queue_pending(q))\n"
         "print('destroy', L.aws_crt_amd_queue_destroy(q))\n"
-        "print('create_age', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,2000,1,0)),ctypes.byref(q)))\n"
+        "print('create_age', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,2000,1,0,0,0)),ctypes.byref(q)))\n"
         "for i in range(3): L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t))\n"
         "dl=time.time()+5\n"
         "while L.aws_crt_amd_queue_pending(q) and time.time()<dl: time.sleep(0.002)\n"
@@ -290,13 +290,13 @@ def test_queue_refused_tickets_never_report_complete():
     code = (
         LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
-        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32)]\n"
+        "class O(ctypes.Structure): _fields_=[('max_batches',sz),('max_age_us',u64),('policy',ctypes.c_uint32),('max_inflight',ctypes.c_uint32),('min_launch',ctypes.c_uint32),('reserved',ctypes.c_uint32)]\n"
         "L.aws_crt_amd_queue_create_ex.argtypes=[ctypes.c_int,sz,sz,sz,vp,ctypes.POINTER(O),ctypes.POINTER(vp)]\n"
         "L.aws_crt_amd_queue_push_ex.argtypes=[vp,vp,vp,vp,ctypes.POINTER(u64)]\n"
         "L.aws_crt_amd_queue_status.argtypes=[vp,u64]\n"
         "L.aws_crt_amd_queue_destroy.argtypes=[vp]\n"
         "q=vp(); t=u64()\n"
-        "assert L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(1,0,1,0)),ctypes.byref(q))==0\n"
+        "assert L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(1,0,1,0,0,0)),ctypes.byref(q))==0\n"
         "rc=[L.aws_crt_amd_queue_push_ex(q,4096,None,8192,ctypes.byref(t)) for i in range(3000)]\n"
         "st=[L.aws_crt_amd_queue_status(q,k) for k in range(1,3001)]\n"
         "print('pushes', set(rc), 'status', sorted(set(st)), 'last', t.value)\n"
