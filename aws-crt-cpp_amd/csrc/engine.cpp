@@ -1897,7 +1897,11 @@ AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(aws_crt_amd_plan *pl) { delete pl;
 // below one launch per batch).  Every push gets a ticket; each launch records an event after it on
 // the queue's stream, so a ticket's completion (or the error of the launch that dropped it) can be
 // asked for and waited on -- and the eager policy asks the newest events whether the stream is busy.
-constexpr size_t kQueueMinLaunch = 1;  // eager launches' default minimum batch count
+// Eager launches' default minimum batch count.  Measured on the driver's command (20 pushes of one
+// C2 batch from Python, then flush; profiles/r06/c/driver1.log): min 1 4955 GiB/s (the first push
+// launches a lone one-batch launch at frac ~0.55, 3-4 launches), min 2 5381 (2 launches), min 4 5358,
+// two launches in flight 4636, the batched policy 4953, one launch per batch 4834.
+constexpr size_t kQueueMinLaunch = 2;
 struct aws_crt_amd_queue {
     int alg = 0;
     int device = 0;

@@ -19,8 +19,9 @@ from collections import defaultdict
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)
-    return name.replace("(anonymous namespace)::", "").strip()
+    name = name.replace("(anonymous namespace)::", "")
+    name = re.sub(r"^void ", "", name)
+    return re.sub(r"\(.*", "", name).strip()
 
 
 def main(paths, min_grid=0):

@@ -173,7 +173,8 @@ AWS_CRT_AMD_API void aws_crt_amd_plan_destroy(struct aws_crt_amd_plan *plan);
  * Submission queue: a producer that gets one uniform batch at a time (aws-c-s3 checksumming parts as
  * they arrive, source/s3/S3.cpp:1133-1149) pushes each batch and the engine launches them together.
  * Default (eager) policy, round 6: a push that finds none of the queue's launches still running on its
- * stream launches at once, with every batch queued so far; batches pushed while a launch runs coalesce
+ * stream launches at once, with every batch queued so far (once at least min_launch, default 2, are
+ * queued); batches pushed while a launch runs coalesce
  * and go out with the first push that finds it done, at 32 queued batches, or at
  * aws_crt_amd_queue_flush / _wait / _destroy (or the age bound, below).  So the GPU is never left idle
  * while batches wait, and a busy GPU gets them in ever larger launches (one launch of up to 32, as
@@ -209,7 +210,8 @@ AWS_CRT_AMD_API int aws_crt_amd_queue_destroy(struct aws_crt_amd_queue *queue);
  *   max_inflight eager policy: a push launches while fewer than this many of the queue's launches
  *                are running (1..8; 0 = 1)
  *   min_launch   eager policy: a push launches only with at least this many batches queued (1..32;
- *                0 = the default, 1); fewer wait for a later push, flush, wait, destroy or the age bound
+ *                0 = the default, 2: a lone one-batch launch runs at about half the rate of a
+ *                multi-batch one); fewer wait for a later push, flush, wait, destroy or the age bound
  * Each push_ex returns a ticket (1, 2, ... per queue).  queue_status(ticket):
  *   AWS_CRT_AMD_TICKET_QUEUED    pushed, not launched yet
  *   AWS_CRT_AMD_TICKET_LAUNCHED  on the stream, not complete

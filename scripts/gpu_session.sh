@@ -78,6 +78,8 @@ for s in "$@"; do
     pmc64) step 420 $O/pmc64.log env TAG=${TAG}/pmc64 bash scripts/pmc_crc64.sh; rc=$?; tail -2 $O/pmc64.log ;;
     # the LDS chain microbenchmark of the CRC64 row step (experiments/crc64_rowbench.hip)
     rowb)  step 120 $O/rowb.log experiments/build/crc64_rowbench; rc=$?; cat $O/rowb.log ;;
+    # A/B of checksum-library builds (ab/lib$v.so) on any command: ABVARIANTS, ABCMD
+    abc)   step 900 $O/abc.log env TAG=${TAG}/abc VARIANTS="${ABVARIANTS:-R X}" REPS=${REPS:-2} bash scripts/ab_cmd.sh $ABCMD; rc=$?; cat $O/abc.log ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }

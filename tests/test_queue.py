@@ -55,9 +55,10 @@ def test_queue_host_logic_without_device():
 
 
 def test_queue_eager_policy_without_device():
-    """the default (eager) policy without a device: nothing of the queue is running, so every push
-    launches at once -- refused (AWS_CRT_AMD_ERR_NO_DEVICE), reported by the push and by its ticket --
-    and nothing stays pending; unknown policies and depths are refused at create"""
+    """the eager policy without a device: nothing of the queue is running, so with min_launch 1 every
+    push launches at once -- refused (AWS_CRT_AMD_ERR_NO_DEVICE), reported by the push and by its
+    ticket -- and nothing stays pending; with the default minimum of two, every second push launches
+    (destroy then flushes the last one, refused); unknown policies, depths and minimums are refused"""
     code = (
         LOAD_SRC +
         "vp=ctypes.c_void_p; sz=ctypes.c_size_t; u64=ctypes.c_uint64\n"
@@ -72,11 +73,17 @@ def test_queue_eager_policy_without_device():
         "q=vp(); t=u64()\n"
         "print('bad_policy', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,2,0,0,0)),ctypes.byref(q)))\n"
         "print('bad_depth', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,9,0,0)),ctypes.byref(q)))\n"
-        "print('create', L.aws_crt_amd_queue_create(1,65536,65536,4,None,ctypes.byref(q)))\n"
+        "print('create', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,0,1,0)),ctypes.byref(q)))\n"
         "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(5)]\n"
         "print('push_rcs', ','.join(map(str,r)), 'pending', L.aws_crt_amd_queue_pending(q), 'launches', L.aws_crt_amd_queue_launches(q))\n"
         "print('st', ','.join(str(L.aws_crt_amd_queue_status(q,k)) for k in range(1,6)))\n"
-        "print('destroy', L.aws_crt_amd_queue_destroy(q))\n")
+        "print('destroy', L.aws_crt_amd_queue_destroy(q))\n"
+        "print('create_default', L.aws_crt_amd_queue_create(1,65536,65536,4,None,ctypes.byref(q)))\n"
+        "r=[L.aws_crt_amd_queue_push_ex(q,4096*(i+1),None,8192*(i+1),ctypes.byref(t)) for i in range(5)]\n"
+        "print('dpush_rcs', ','.join(map(str,r)), 'dpending', L.aws_crt_amd_queue_pending(q), 'dlaunches', L.aws_crt_amd_queue_launches(q))\n"
+        "print('bad_min', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,0,33,0)),ctypes.byref(vp())))\n"
+        "print('bad_reserved', L.aws_crt_amd_queue_create_ex(1,65536,65536,4,None,ctypes.byref(O(0,0,0,0,0,1)),ctypes.byref(vp())))\n"
+        "print('destroy2', L.aws_crt_amd_queue_destroy(q))\n")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
                        env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
     assert r.returncode == 0, r.stderr
@@ -88,6 +95,10 @@ def test_queue_eager_policy_without_device():
     assert got["bad_policy"] == "-2" and got["bad_depth"] == "-2" and got["create"] == "0"
     assert got["push_rcs"] == "-1,-1,-1,-1,-1" and got["pending"] == "0" and got["launches"] == "5"
     assert got["st"] == "-1,-1,-1,-1,-1" and got["destroy"] == "0"
+    # the default minimum of two batches per eager launch: every second push launches
+    assert got["create_default"] == "0" and got["dpush_rcs"] == "0,-1,0,-1,0"
+    assert got["dpending"] == "1" and got["dlaunches"] == "2" and got["destroy2"] == "-1"
+    assert got["bad_min"] == "-2" and got["bad_reserved"] == "-2"
 
 
 def test_queue_tickets_refused_launch_and_age_flush_without_device():
@@ -250,8 +261,8 @@ def test_queue_tickets_age_bound_and_refused_flush(engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("depth", [1, 2])
-def test_queue_eager_launches(engine, depth):
+@pytest.mark.parametrize("depth,min_launch", [(1, 1), (2, 1), (1, 0)])
+def test_queue_eager_launches(engine, depth, min_launch):
     """the eager policy launches a push at once when nothing of the queue runs
     (the first push leaves nothing pending), coalesces the pushes made while launches run (fewer
     launches than pushes: a one-batch launch of 64 MiB takes ~15 us, a push a few), and every ticket
@@ -261,11 +272,14 @@ def test_queue_eager_launches(engine, depth):
     n, L, nb = 1024, 65536, 60  # C2 batches (64 MiB), 6 resident ones reused (the results are per push)
     d = _dev_random(n * L * 6, 0xE1)
     outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(nb)]
-    q = engine.Queue(ALG["crc32c"], L, L, n, max_inflight=depth)
+    q = engine.Queue(ALG["crc32c"], L, L, n, max_inflight=depth, min_launch=min_launch)
+    first = 1 if min_launch == 1 else 2  # the default minimum is two batches
     tickets = []
     for j in range(nb):
         tickets.append(q.push(d[(j % 6) * n * L:], outs[j]))
-        if j == 0:
+        if j + 1 < first:
+            assert q.pending() == j + 1 and q.launches() == 0
+        elif j + 1 == first:
             assert q.pending() == 0 and q.launches() == 1
     q.flush()
     assert q.pending() == 0
