@@ -2872,7 +2872,7 @@ __device__ __forceinline__ void xcd_issue(B64Group &g, __amdgpu_buffer_rsrc_t rs
 // PADDED: some main regions hold no whole number of chunks (ScanParams::xcd_pad != 0): every group
 // reads through a buffer resource.  Otherwise plain global loads (1-2 % shorter C5 launches).
 template <uint64_t POLY, int BLOCK, bool PADDED, bool PRIO = false>
-__global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p) {
+__global__ __launch_bounds__(BLOCK, AMDCRC_XCD_WPE) void crc64_xcd_kernel(const ScanParams p) {
     using B = Braid64<POLY, 4>;
     __shared__ __attribute__((aligned(16))) char lds[kXcdLds];
     constexpr int kWaves = BLOCK / 64;
@@ -3024,6 +3024,7 @@ __global__ __launch_bounds__(BLOCK, 4) void crc64_xcd_kernel(const ScanParams p)
     // crossing with three returning atomics, each a vmcnt(0): 20-batch C5 launches at 0.66 against 0.77
     // for one batch).  A full table -- more than kXcdSlots buffers in one workgroup -- publishes directly.
     auto part_put = [&](uint64_t b, uint64_t v, uint32_t n) {
+#pragma unroll 1
         for (uint32_t i = 0; i < kXcdSlots; ++i) {
             const uint32_t e = ((uint32_t)b + i) & (kXcdSlots - 1);
             uint64_t t = ~0ull;

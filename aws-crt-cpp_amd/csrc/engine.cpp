@@ -1179,7 +1179,7 @@ int scan_batches(Device *d, int alg, const Batch *bs, size_t nb, size_t stride, 
     }
     // long CRC64NVME buffers of whole chunks: XCD-window chunk order (crc64_xcd_kernel)
     if (!w32 && kXcd && ml >= kXcdMinChunks * kXcdChunkBytes) {
-        const uint64_t blocks = ((uint64_t)d->cus * (kXcdBlock > 640 ? 1 : 2)) & ~7ull, nwx = blocks * (kXcdBlock / 64) / 8;
+        const uint64_t blocks = ((uint64_t)d->cus * kXcdBpc) & ~7ull, nwx = blocks * (kXcdBlock / 64) / 8;
         if (blocks >= 8) {
             p.stream = 5;
             p.tiles_per_buf = (ml + kXcdChunkBytes - 1) / kXcdChunkBytes;

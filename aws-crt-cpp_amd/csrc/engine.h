@@ -37,6 +37,13 @@ constexpr uint64_t kXcdChunkBytes = (uint64_t)AMDCRC_XCD_CHUNK_GROUPS * 4096;
 #define AMDCRC_XCD_BLOCK 512
 #endif
 constexpr int kXcdBlock = AMDCRC_XCD_BLOCK;
+#ifndef AMDCRC_XCD_BPC  // compile-time only (A/B builds): crc64_xcd_kernel workgroups per CU
+#define AMDCRC_XCD_BPC (AMDCRC_XCD_BLOCK > 640 ? 1 : 2)
+#endif
+#ifndef AMDCRC_XCD_WPE  // compile-time only (A/B builds): crc64_xcd_kernel launch bound, waves per SIMD
+#define AMDCRC_XCD_WPE 4
+#endif
+constexpr int kXcdBpc = AMDCRC_XCD_BPC;
 constexpr int kMaxBatches = 32;  // batches per strided launch (kernel arguments, 768 bytes)
 constexpr uint64_t kStreamLocalSlots = 128;  // crc32_stream_kernel: LDS slots for a workgroup's whole buffers
 

@@ -1,7 +1,9 @@
 /*
  * Aws::Crt::Checksum CRC API (reference source/checksum/CRC.cpp:13-45) over the MI355X engine.
- * Each call forwards to the aws-checksums-named C ABI (include/aws/checksums/crc.h), which scans
- * on the GPU: host inputs are staged through pinned memory, device inputs are scanned in place.
+ * Each call forwards to the aws-checksums-named C ABI (include/aws/checksums/crc.h): device inputs
+ * are scanned in place by the gfx950 kernels; host inputs run on the engine's host path in the
+ * default (AUTO) dispatch, and are staged through pinned memory to the GPU only when the GPU
+ * dispatch is forced (AWS_CRT_AMD_DISPATCH=gpu).
  */
 #include <aws/checksums/crc.h>
 #include <aws/crt/checksum/CRC.h>

@@ -80,6 +80,7 @@ for s in "$@"; do
     rowb)  step 120 $O/rowb.log experiments/build/crc64_rowbench; rc=$?; cat $O/rowb.log ;;
     # A/B of checksum-library builds (ab/lib$v.so) on any command: ABVARIANTS, ABCMD
     abc)   step 900 $O/abc.log env TAG=${TAG}/abc VARIANTS="${ABVARIANTS:-R X}" REPS=${REPS:-2} bash scripts/ab_cmd.sh $ABCMD; rc=$?; cat $O/abc.log ;;
+    pmces) step 600 $O/pmces.log env TAG=${TAG}/pmces VARIANTS="${ESVARIANTS:-C ESL}" bash scripts/pmc_es.sh; rc=$?; tail -2 $O/pmces.log ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac
   [ $rc -ne 0 ] && { echo "session stopped at $s rc=$rc"; exit $rc; }

@@ -1,5 +1,6 @@
-"""CPU model of the chunked event-stream framing kernel (crc_kernels.hip eventstream_chunk_kernel, round
-6), checked against zlib: the algebra the kernel relies on, restated in Python.
+"""CPU model of the chunked event-stream framing kernel (round 6; measured slower than
+the lane kernel and kept as experiments/patches/eventstream_chunk.patch), checked against zlib: the
+algebra the kernel relies on, restated in Python.
 
 A message's CRC'd span [A, E) (A = its offset, E = A + total_length - 4) is cut on the 8-byte grid:
 head [A, A8) with A8 = A rounded up to 8, whole words [A8, W) with W = E rounded down to 8, tail [W, E).
