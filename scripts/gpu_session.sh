@@ -10,7 +10,7 @@ O=$R/gpurun_out/${TAG:-run}; mkdir -p $O
 export TMPDIR=/tmp
 step() { bash $R/scripts/gpu_step.sh "$@"; }
 # profiling runs: driver-shaped launches only (20 batches per launch), no CPU baseline or extra legs
-P="--steps 20 --warmup 20 --only-coalesced --branches 1 --no-configs --no-cpu-baseline --e2e-batches 0 --timing-launches 16"
+P="--steps 20 --warmup 20 --only-coalesced --branches 1 --no-configs --no-c4 --no-cpu-baseline --e2e-batches 0 --timing-launches 16"
 rc=0
 for s in "$@"; do
   case $s in
@@ -18,7 +18,9 @@ for s in "$@"; do
     tsel)  step 600 $O/pytest_sel.log python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -k "${TESTK:-xcd}"; rc=$?; tail -3 $O/pytest_sel.log ;;
     smoke) step 180 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; tail -2 $O/smoke.log ;;
     bench) step 400 $O/bench.log python -u bench.py ${BENCH_ARGS:-}; rc=$?; tail -1 $O/bench.log ;;
-    driver*) step 400 $O/$s.log python -u bench.py --gpus 1 --steps 20 --warmup 5; rc=$?; grep '^{' $O/$s.log | cut -c1-400 ;;
+    driver*) t0=$(date +%s); step 400 $O/$s.log python -u bench.py --gpus 1 --steps 20 --warmup 5; rc=$?; echo "[driver] wall $(( $(date +%s) - t0 )) s" >> $O/$s.log; grep '^{' $O/$s.log | cut -c1-400; tail -1 $O/$s.log ;;
+    # the N > 1 rank path rehearsed on the one GPU: two gloo ranks, the full bench (C4 legs, CPU baseline)
+    gloo2) t0=$(date +%s); step 600 $O/gloo2.log python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --e2e-batches 0; rc=$?; echo "[gloo2] wall $(( $(date +%s) - t0 )) s" >> $O/gloo2.log; grep '^{' $O/gloo2.log | cut -c1-300; tail -1 $O/gloo2.log ;;
     # the timed region decomposed: kernel + HIP API trace of the driver's timed region (legs trimmed)
     trace) (cd /tmp && step 300 $O/trace.log rocprofv3 --kernel-trace --hip-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-configs --no-cpu-baseline --e2e-batches 0); rc=$? ;;
     # kernel trace of the driver's exact command
