@@ -57,6 +57,10 @@ def test_bench_c4_leg_one_gpu():
         c4 = d["configs"][f"C4_{alg}"]
         assert c4["digest_match"] is True and c4["parity"] is True and c4["n_gpus"] == 1
         assert c4["ranks"][0]["buffers"] == 1 << 20 and 0 < c4["roofline"]["frac"] <= 1
+        # burst, from-idle and sustained regimes
+        rg = c4["regimes"]
+        assert rg["burst_ms_per_pass"] > 0 and rg["from_idle_ms_per_pass"] > 0 and rg["preload_passes"] >= 1
+        assert 0 < c4["ranks"][0]["burst_frac"] <= 1 and 0 < c4["roofline_burst"]["frac"] <= 1
 
 
 def _bench(args, timeout=300, cpu=False, c4=False):

@@ -126,7 +126,8 @@ def _c4_golden(n, L):
 def _c4_args():
     import argparse
 
-    return argparse.Namespace(c4_passes=1, timing_launches=8, no_cpu_baseline=False, cpu_seconds=0.05)
+    return argparse.Namespace(c4_passes=1, timing_launches=8, no_cpu_baseline=False, cpu_seconds=0.05,
+                              c4_preload_ms=5.0, c4_window_ms=0.0)
 
 
 def _fake_timer(eng, launch, st, nt):
