@@ -28,6 +28,9 @@
 #ifndef AMDCRC_R16_XCD  // compile-time only: crc64_rows16_kernel's sets in XCD-window order (1) or contiguous (0)
 #define AMDCRC_R16_XCD 1
 #endif
+#ifndef AMDCRC_ES_FLAT  // compile-time only: event-stream frames on the balanced flat kernel (1) or one lane per message (0)
+#define AMDCRC_ES_FLAT 1
+#endif
 #ifndef AMDCRC_STREAM_W8  // compile-time only: the W=32 streaming scan on 8-byte words (1) or 4-byte words (0)
 #define AMDCRC_STREAM_W8 1
 #endif
@@ -4025,6 +4028,299 @@ __global__ __launch_bounds__(256) void eventstream_kernel(const EventStreamParam
     p.d_status[m] = st;
 }
 
+// ------------------------------------------------------------------------------------------
+// Balanced event-stream framing check (round 6).  A wave takes 64
+// consecutive messages.  When they are well formed and packed back to back (a stream of frames), the
+// wave's region -- the messages' bytes widened to 64-byte alignment -- is cut into 64 equal chunks
+// (C bytes, a multiple of 16) and lane l folds chunk l as ONE flat loop of 8-byte words from register
+// 0: no masks, no resets, the stored CRCs and each next message's first bytes folded along.  At a
+// message's end word the lane records the fold's two halves (lo4: the lookups of bytes 0..3, which
+// carry the register; hi4: bytes 4..7); after the loop, message i's CRC is assembled from its record,
+// the previous message's record, the lanes' chunk-end registers and a few corrections, all linear
+// (tests/test_eventstream_flat_model.py restates the algebra against zlib):
+//
+//   rec_i = lo4 (a_i <= 4) or lo4 ^ hi4, a_i = e_i - P_i, e_i the span end, P_i its end word
+//   Y_i   = word(rec_(i-1) ^ word(0, V1), V2)   V1, V2: the words at B_i = P_(i-1) and B_i + 8 with the
+//           previous stored-CRC bytes outside rec_(i-1) and 0xFF over message i's first four bytes
+//   Z_i   = rec_i ^ word(0, stored-CRC bytes inside rec_i) ^ Y_i x^(8 (P_i - B_i - 8))
+//           ^ sum over the chunks k between: end_k x^(8 (P_i + 8 - c0_(k+1)))
+//   CRC_i = ~(Z_i x^(-8 (8 - a_i)))
+//
+// Products are nibble images of x^(64 v 16^d) (digits 0, 1 and x^(-8 t) in LDS, digits 2, 3 read from
+// the image buffer).  The chunks are loaded by lane quads (four lanes read one chunk's 64-byte block:
+// 16 blocks per load instruction, not 64) and handed to their owners through the wave's LDS rows.
+// Waves whose messages are malformed, not packed back to back, or span more than kEsMaxRegion take the
+// one-lane-per-message path of eventstream_kernel.  Probe: experiments/esload.hip.
+constexpr uint32_t kEsBlock = 512;                     // one workgroup of 8 waves per CU
+constexpr uint32_t kEsRow = 80;                        // transposition row: 64 B + 16 (bank spread)
+constexpr uint32_t kEsMaxRegion = 256u << 10;          // word distances < 32768: four hex digits
+constexpr uint32_t kEsLdsImgs = 37;                    // images 0..29 (digits 0, 1), then x^(-8 t)
+struct EsWave {
+    char rows[64 * kEsRow];
+    uint32_t rec[64];           // message i's register at its end word
+    uint32_t P[68], endst[64];  // P[64..67]: sentinels
+};
+constexpr uint32_t kEsLds = kLaneW8Lds + kEsLdsImgs * 512 + (kEsBlock / 64) * sizeof(EsWave);
+static_assert(kEsLds <= 160 * 1024, "event-stream LDS");
+
+// r * K for a per-lane K from its nibble image in LDS (entry 16 i + v: nibble i's value v times K)
+__device__ __forceinline__ uint32_t es_mul(uint32_t r, const uint32_t *img) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = img[16 * i + ((r >> (28 - 4 * i)) & 15u)];
+    return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
+}
+__device__ __forceinline__ uint32_t es_mul_g(uint32_t r, gu32 *img) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = img[16 * i + ((r >> (28 - 4 * i)) & 15u)];
+    return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
+}
+// r * x^(64 m), m < 65536
+__device__ __forceinline__ uint32_t es_shift_words(uint32_t r, uint32_t m, const uint32_t *limg, gu32 *gimg) {
+    if (m & 15u) r = es_mul(r, limg + 128 * ((m & 15u) - 1));
+    if ((m >> 4) & 15u) r = es_mul(r, limg + 128 * (14 + ((m >> 4) & 15u)));
+    if ((m >> 8) & 15u) r = es_mul_g(r, gimg + 128 * (29 + ((m >> 8) & 15u)));
+    if ((m >> 12) & 15u) r = es_mul_g(r, gimg + 128 * (44 + ((m >> 12) & 15u)));
+    return r;
+}
+__device__ __forceinline__ uint32_t es_word(const LaneW8 &f, uint32_t s, uint64_t v) { return f.word(s, v); }
+
+__global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventStreamParams p) {
+    __shared__ __attribute__((aligned(16))) char lds[kEsLds];
+    {  // tables (the 256-thread build's stores, split over the two halves) and images
+        constexpr LaneW8Basis<kPoly32> B{};
+        const uint32_t i = threadIdx.x & 255u, tl = (i & 7u) >> 1, half = i & 1u, k0 = 8u * (threadIdx.x >> 8);
+        uint32_t bl[8], bh[8];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            bl[b] = tl == 0 ? B.b[0][b] : tl == 1 ? B.b[1][b] : tl == 2 ? B.b[2][b] : B.b[3][b];
+            bh[b] = tl == 0 ? B.b[4][b] : tl == 1 ? B.b[5][b] : tl == 2 ? B.b[6][b] : B.b[7][b];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t k = k0 + kk, e = (i >> 3) + 32u * (k >> 1), t = tl + 4u * (k & 1);
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) v ^= ((e >> b) & 1u) ? ((k & 1) ? bh[b] : bl[b]) : 0u;
+            *(uint4 *)(lds + (e << 8) + (t << 5) + (half << 4)) = make_uint4(v, v, v, v);
+        }
+        v4u *li = (v4u *)(lds + kLaneW8Lds);
+        for (uint32_t j = threadIdx.x; j < kEsLdsImgs * 32; j += kEsBlock)
+            li[j] = ((gv4u *)p.d_imgs)[j < 30 * 32 ? j : j + 30 * 32];
+    }
+    __syncthreads();
+    LaneW8 f;
+    const uint32_t lane = threadIdx.x & 63u;
+    f.init(lds, lane);
+    const uint32_t *limg = (const uint32_t *)(lds + kLaneW8Lds);
+    EsWave &W = ((EsWave *)(lds + kLaneW8Lds + kEsLdsImgs * 512))[threadIdx.x >> 6];
+
+    const uint64_t m = (uint64_t)blockIdx.x * kEsBlock + threadIdx.x;
+    const bool in = m < p.count;
+    const uint64_t off = in ? p.d_offsets[m] : 0;
+    uint32_t total = 0, headers = 0, pre_stored = 0;
+    uint64_t w8 = 0;  // the prelude's 8 bytes
+    bool ok = false;
+    const uint8_t *q = p.base + off;
+    // four bytes at any address from the aligned dwords holding them (never a dword past the last byte)
+    auto u32_at = [](const uint8_t *a) {
+        const uintptr_t x = (uintptr_t)a, o = x & 3u;
+        const uint32_t lo = *(gu32 *)(x & ~(uintptr_t)3), hi = *(gu32 *)((x & ~(uintptr_t)3) + (o ? 4 : 0));
+        return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)o);
+    };
+    if (in && off <= p.limit && p.limit - off >= 16) {
+        const uint32_t b0 = u32_at(q), b1 = u32_at(q + 4), b2 = u32_at(q + 8);
+        total = __builtin_bswap32(b0);
+        headers = __builtin_bswap32(b1);
+        pre_stored = __builtin_bswap32(b2);
+        w8 = (uint64_t)b0 | (uint64_t)b1 << 32;
+        ok = total >= 16 && total <= p.limit - off && headers <= total - 16;
+    }
+    if (!ok) total = 0;
+    // the flat path: every lane's message well formed, packed back to back, the region bounded
+    const uint64_t off_next = __shfl_down(off, 1), off0 = __shfl(off, 0);
+    const uint64_t end63 = __shfl(off + total, 63);
+    const bool flat = __all(ok && (lane == 63 || off + total == off_next) && end63 - off0 <= kEsMaxRegion);
+    const uint32_t s8 = ok ? f.word(~0u, w8) : 0u;  // the register after the prelude
+    const uint32_t pre = ok ? ~s8 : 0u;
+    uint32_t st = ok ? (pre_stored == pre ? 1u : 0u) : 4u, msg = 0;
+    if (!flat) {
+        if (!in) return;
+        if (ok) {
+            msg = ~lane_scan<uint32_t>(s8, q + 8, total - 12, f);
+            st |= __builtin_bswap32(u32_at(q + total - 4)) == msg ? 2u : 0u;
+        }
+        p.d_prelude_crc[m] = pre;
+        p.d_message_crc[m] = msg;
+        p.d_status[m] = st;
+        return;
+    }
+    // wave-uniform values in SGPRs (the shuffles' results are VGPRs to the compiler)
+    const uintptr_t rs = rfl64((uintptr_t)(p.base + off0) & ~(uintptr_t)15);  // 16-aligned: message 0 starts < 16 in
+    const uint32_t s_i = (uint32_t)((uintptr_t)q - rs), e_i = s_i + total - 4;
+    const uint32_t P_i = (e_i - 1) & ~7u, a_i = e_i - P_i;
+    // region end relative to rs, 16-aligned (so never past the page of the last message's last byte)
+    const uint32_t re = __builtin_amdgcn_readfirstlane((__shfl(e_i, 63) + 4 + 15) & ~15u);
+    const uint32_t C = (((re + 63) >> 6) + 15) & ~15u;  // 64 C >= re, C a multiple of 16
+    const uint32_t nb = (C + 63) >> 6, wl = (C & 63u) ? (C & 63u) >> 3 : 8u;
+    const uint32_t c0 = lane * C;
+    // the ends, ascending: P in bits 0..23, a in bits 24..31; sentinels past the last
+    W.P[lane] = P_i | a_i << 24;
+    if (lane < 4) W.P[64 + lane] = 0x00ffffffu;
+    constexpr uint32_t kPMask = 0x00ffffffu;
+    // the lane's first end at or after its chunk start
+    uint32_t i0 = (W.P[63] & kPMask) < c0 ? 64u : 0u;
+    if (i0 == 0)
+#pragma unroll
+        for (uint32_t sp = 32; sp; sp >>= 1)
+            if ((W.P[i0 + sp - 1] & kPMask) < c0) i0 += sp;
+    // the next four ends (a 64-byte block holds at most four: spans of >= 12 bytes, 4-byte gaps)
+    uint32_t pw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pw[j] = W.P[i0 + j];
+
+    // the stored message CRC's two dwords, loaded now and used after the scan
+    const uintptr_t crc_a = (uintptr_t)(q + total - 4);
+    const uint32_t crc_lo = *(gu32 *)(crc_a & ~(uintptr_t)3), crc_hi = *(gu32 *)((crc_a & ~(uintptr_t)3) + ((crc_a & 3u) ? 4 : 0));
+    const uint32_t raw = __builtin_amdgcn_alignbyte(crc_hi, crc_lo, (uint32_t)(crc_a & 3u));  // its bytes in memory order
+
+    // This message's end patch: the stored CRC's four bytes at [e_i, e_i + 4) XORed with themselves
+    // (cleared) and the next message's first four bytes XORed with 0xFF (CRC32's ~0 start), so that
+    // with the register reset at each end word every record is its message's own register.  The three
+    // dwords are XORed into their owners' LDS rows (ds_xor) in the block step that holds them.
+    uint32_t pt_b[3], pt_a[3], pt_x[3];
+    {
+        const uint64_t pat = (uint64_t)raw | 0xffffffff00000000ull;  // bytes e_i .. e_i + 7
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const uint32_t y = (e_i & ~3u) + 4u * d;
+            const int rel = (int)y - (int)e_i;
+            pt_x[d] = rel >= 8 ? 0u : rel >= 0 ? (uint32_t)(pat >> (8 * rel)) : (uint32_t)(pat << (-8 * rel));
+            const uint32_t o = y / C, yo = y - o * C;
+            pt_b[d] = rel < 8 && o < 64 ? yo >> 6 : ~0u;  // the block step, or never
+            pt_a[d] = (uint32_t)(o * kEsRow + (yo & 63u)) >> 2;  // a dword of the owner's row
+        }
+    }
+
+    const uintptr_t rea = rs + re;
+    const uintptr_t qbase = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
+    auto qaddr = [&](uint32_t j, uint32_t b) {  // always a readable address (past the region: its last block)
+        const uintptr_t a = qbase + (uintptr_t)(16u * j) * C + ((uintptr_t)b << 6);
+        return a < rea ? a : rea - 64 + 16u * (lane & 3u);
+    };
+    v4u v[4], nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *(gv4u *)qaddr(j, 0);
+    char *wrow = W.rows + (lane >> 2) * kEsRow + 16 * (lane & 3);
+    const char *rrow = W.rows + lane * kEsRow;
+    uint32_t *rows32 = (uint32_t *)W.rows;
+    const uint32_t s0 = __builtin_amdgcn_readfirstlane(__shfl(s_i, 0));  // message 0's start (< 16)
+    uint32_t u = 0;
+    // one block's words.  Bit k of `ends`: word k is an end word; its record (lo4 for a <= 4, which
+    // leaves the next message's head in hi4, else lo4 ^ hi4) goes to message r0 + (the ends before
+    // it) and the register restarts with hi4 or 0.  FEW: no lane has two ends in the block (two need
+    // a message of < 64 bytes): the end word is handled by selects and the record stored after the
+    // block, so the fold is straight-line code.
+    auto fold_words = [&](auto few_c, const v4u(&w)[4], uint32_t ends, uint32_t r0, auto nw) {
+        constexpr bool few = decltype(few_c)::value;
+        const uint32_t kend = ends ? (uint32_t)__builtin_ctz(ends) : 8u;
+        const uint32_t m5 = (pw[0] >> 24) >= 5 ? ~0u : 0u;  // FEW: the block's end (window entry 0)
+        uint32_t rv = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            if (k < nw) {
+                const uint32_t lo = w[k >> 1][2 * (k & 1)] ^ u, hi = w[k >> 1][2 * (k & 1) + 1];
+                uint32_t x[8];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    x[t] = lds32(f.L, __builtin_amdgcn_perm(f.cst8[t], lo, f.sel8[t]));
+                    x[4 + t] = lds32(f.L, __builtin_amdgcn_perm(f.cst8[4 + t], hi, f.sel8[4 + t]));
+                }
+                const uint32_t lo4 = xor3(x[0], x[1], x[2]) ^ x[3], hi4 = xor3(x[4], x[5], x[6]) ^ x[7];
+                if constexpr (few) {  // selects only (no asm: the compiler would branch around it)
+                    const bool hit = k == kend;
+                    const uint32_t rec = lo4 ^ (hi4 & m5), nxt = hi4 & ~m5, run = lo4 ^ hi4;
+                    rv = hit ? rec : rv;
+                    u = hit ? nxt : run;
+                } else {
+                    if ((ends >> k) & 1u) {
+                        const uint32_t j = __builtin_popcount(ends & ((1u << k) - 1u));
+                        const uint32_t pj = j == 0 ? pw[0] : j == 1 ? pw[1] : j == 2 ? pw[2] : pw[3];
+                        const bool a5 = (pj >> 24) >= 5;
+                        W.rec[r0 + j] = a5 ? lo4 ^ hi4 : lo4;
+                        u = a5 ? 0u : hi4;
+                    } else {
+                        u = lo4 ^ hi4;
+                    }
+                }
+            }
+        }
+        if constexpr (few) {
+            if (ends) W.rec[r0] = rv;
+        }
+    };
+    using few_t = std::integral_constant<bool, true>;
+    using many_t = std::integral_constant<bool, false>;
+    for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nv[j] = *(gv4u *)qaddr(j, b + 1);  // unconditional: exact vmcnt waits
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(v4u *)(wrow + j * 16 * kEsRow) = v[j];
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            if (pt_b[d] == b) __hip_atomic_fetch_xor(rows32 + pt_a[d], pt_x[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        v4u w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = *(const v4u *)(rrow + 16 * j);
+        if (b == 0) {  // the bytes in front of message 0 (< 16) cleared, its first four flipped (~0 start)
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                const int rel = (int)(c0 + 4 * d) - (int)s0;
+                const uint32_t keep = rel >= 0 ? ~0u : rel <= -4 ? 0u : ~0u << (-8 * rel);
+                const uint32_t flip = rel >= 4 || rel <= -4 ? 0u : rel >= 0 ? 0xffffffffu >> (8 * rel) : 0xffffffffu << (-8 * rel);
+                w[d >> 2][d & 3] = (w[d >> 2][d & 3] & keep) ^ flip;
+            }
+        }
+        const uint32_t bs = c0 + 64 * b, be = min(bs + 64, c0 + C);
+        uint32_t ends = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t pj = pw[j] & kPMask;
+            ends |= pj < be ? 1u << ((pj - bs) >> 3) : 0u;
+        }
+        const uint32_t r0 = i0;
+        const uint32_t nw = b + 1 < nb ? 8u : wl;
+        if (__any(ends & (ends - 1)))
+            fold_words(many_t(), w, ends, r0, nw);
+        else if (nw == 8)
+            fold_words(few_t(), w, ends, r0, std::integral_constant<uint32_t, 8>());
+        else
+            fold_words(few_t(), w, ends, r0, nw);
+        i0 += __builtin_popcount(ends);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pw[j] = W.P[i0 + j];  // the next block's window
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = nv[j];
+    }
+    W.endst[lane] = u;
+    __builtin_amdgcn_wave_barrier();
+
+    // message `lane`: its record, plus the pieces of the chunks it began in (chunks lane(B) ..
+    // lane(P_i) - 1, B = the previous end word or message 0's first word), moved to its end word;
+    // then the end word's overshoot past e_i taken off
+    uint32_t z = (uint32_t)W.rec[lane];
+    const uint32_t B = lane ? (W.P[lane - 1] & kPMask) : 0u;
+    gu32 *gimg = (gu32 *)p.d_imgs;
+    for (uint32_t k = B / C, kp = P_i / C; k < kp; ++k) z ^= es_shift_words(W.endst[k], (P_i + 8 - (k + 1) * C) >> 3, limg, gimg);
+    if (a_i < 8) z = es_mul(z, limg + 128 * (30 + (7 - a_i)));  // x^(-8 (8 - a_i))
+    msg = ~z;
+    st |= __builtin_bswap32(raw) == msg ? 2u : 0u;
+    p.d_prelude_crc[m] = pre;
+    p.d_message_crc[m] = msg;
+    p.d_status[m] = st;
+}
+
 }  // namespace
 
 #if AWS_CRT_AMD_DIAG  // diagnostic library only (lib/libaws-crt-cpp-amd-diag.so)
@@ -4194,8 +4490,12 @@ extern "C" int amdcrc_launch_lanes(int alg, const LaneParams *p, void *stream, v
 
 extern "C" int amdcrc_launch_eventstream(const EventStreamParams *p, void *stream, void *const *ev) {
     if (p->count == 0) return 0;
-    const uint64_t blocks = (p->count + 255) / 256;
-    launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
+    if (AMDCRC_ES_FLAT && p->d_imgs) {
+        launch(eventstream_flat_kernel, (int)((p->count + kEsBlock - 1) / kEsBlock), kEsBlock, (hipStream_t)stream, p, ev);
+    } else {
+        const uint64_t blocks = (p->count + 255) / 256;
+        launch(eventstream_kernel, (int)blocks, 256, (hipStream_t)stream, p, ev);
+    }
     return (int)hipGetLastError();
 }
 

@@ -160,6 +160,7 @@ struct Device {
     DevBuf hash_stage;        // whole-buffer device copy for GPU-dispatched host xxHash
     DevBuf xstream_sums;      // streaming XXH3 on device chunks: block sums of one pass
     DevBuf ceil_sink;         // read-ceiling diagnostics: one word per wave
+    DevBuf es_imgs;           // eventstream_flat_kernel's nibble images (get_es_images)
     void *d_small = nullptr;  // results / seeds for the single path
     void *h_res = nullptr;    // pinned, coherent host slot the single path's last launch stores into
     std::mutex single_mu;
@@ -348,6 +349,34 @@ int get_braid_consts(Device *d, int alg, const uint64_t **out) {
         it = d->braid.emplace(alg, b).first;
     }
     *out = (const uint64_t *)it->second.p;
+    return 0;
+}
+
+// eventstream_flat_kernel's products (engine.h kEsImages): nibble images of x^(64 v 16^d) -- the word
+// distances between a message's end word and its previous record or a chunk end, one image per hex
+// digit -- and of x^(-8 t), t = 1..7 (the end word's overshoot past the span end).  CRC32 only.
+int get_es_images(Device *d, const uint32_t **out) {
+    if (!d->es_imgs.p) {
+        const uint32_t poly = (uint32_t)alg_poly(ALG_CRC32);
+        std::vector<uint32_t> c(128 * kEsImages, 0);
+        auto image = [&](int slot, uint32_t k) {
+            nib_image<uint32_t, 32>(&c[128 * slot], [&](int j) {
+                uint32_t col = k;
+                for (int i = 0; i < j; ++i) col = (uint32_t)gf2_mulx(col, poly);
+                return col;
+            });
+        };
+        for (int dg = 0; dg < 4; ++dg)
+            for (uint32_t v = 1; v < 16; ++v) image(15 * dg + (int)v - 1, (uint32_t)gf2_xpow8n(8ull * v << (4 * dg), poly, 32));
+        uint32_t xn = 0x80000000u;  // x^0, then x^(-8 t)
+        for (int t = 1; t < 8; ++t) {
+            for (int i = 0; i < 8; ++i) xn = inv_mulx32(xn, poly);
+            image(60 + t - 1, xn);
+        }
+        int rc = upload_new(d->es_imgs, c.data(), c.size() * 4);
+        if (rc) return rc;
+    }
+    *out = (const uint32_t *)d->es_imgs.p;
     return 0;
 }
 
@@ -2206,7 +2235,15 @@ AWS_CRT_AMD_API int aws_crt_amd_eventstream_crcs(const void *base, uint64_t limi
         Device *d;
         int rc = get_device(&d);
         if (rc) return rc;
-        EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status};
+        const uint32_t *imgs = nullptr;
+        {
+            std::lock_guard<std::mutex> g(d->mu);
+            if (!d->es_imgs.p && capturing((hipStream_t)hip_stream))
+                return fail(AWS_CRT_AMD_ERR_INVALID_ARG, "event-stream images must be warmed up before stream capture");
+            rc = get_es_images(d, &imgs);
+        }
+        if (rc) return rc;
+        EventStreamParams ep{(const uint8_t *)base, d_offsets, count, limit, d_prelude_crc, d_message_crc, d_status, imgs};
         int e = amdcrc_launch_eventstream(&ep, hip_stream, g_time_events);
         g_time_events[0] = g_time_events[1] = nullptr;
         return e ? fail(AWS_CRT_AMD_ERR_HIP, std::string("event-stream kernel launch: ") + hipGetErrorString((hipError_t)e)) : 0;

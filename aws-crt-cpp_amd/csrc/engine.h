@@ -196,7 +196,11 @@ struct EventStreamParams {
     const uint64_t *d_offsets;  // message starts, bytes from base
     uint64_t count, limit;      // limit: bytes readable from base
     uint32_t *d_prelude_crc, *d_message_crc, *d_status;
+    const uint32_t *d_imgs;     // eventstream_flat_kernel's nibble images (engine.cpp get_es_images); null: lane kernel
 };
+// eventstream_flat_kernel's image buffer: x^(64 v 16^d), d < 4, v = 1..15 (image 15 d + v - 1), then
+// x^(-8 t), t = 1..7 (image 60 + t - 1); 128 words each (nib_image)
+constexpr int kEsImages = 67;
 
 }  // namespace amdcrc
 

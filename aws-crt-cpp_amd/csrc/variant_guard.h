@@ -15,7 +15,7 @@
     defined(AMDCRC_LIST_STREAM) || defined(AMDCRC_LIST_TWO_PER_CU) || defined(AMDCRC_LIST_STREAM64) ||            \
     defined(AMDCRC_X64_HOST_MAX) || defined(AMDCRC_R16_XCD) || defined(AMDCRC_STREAM_W8) || defined(AMDCRC_GUARD) ||     \
     defined(AMDCRC_STREAM_PRIO) || defined(AMDCRC_PRIO_ALL) || defined(AMDCRC_PRIO_EVERY) || defined(AMDCRC_PRIO_SCALE) ||   \
-    defined(AMDCRC_R16_PRIO) || defined(AMDCRC_XCD_BPC) || defined(AMDCRC_XCD_WPE)
+    defined(AMDCRC_R16_PRIO) || defined(AMDCRC_XCD_BPC) || defined(AMDCRC_XCD_WPE) || defined(AMDCRC_ES_FLAT)
 #error "an AMDCRC_* A/B knob is set in a build that is not a variant build (define AMDCRC_VARIANT_BUILD: scripts/build_variant.sh)"
 #endif
 #endif

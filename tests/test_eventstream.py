@@ -171,3 +171,90 @@ def test_check_frames_argument_types():
         check_frames(base, torch.zeros(2, dtype=torch.int32))
     with pytest.raises(TypeError):
         check_frames(base, torch.zeros(4, dtype=torch.int64)[::2])
+
+
+def _packed(lens, seed, lead=0, corrupt=False):
+    """messages packed back to back after `lead` bytes (a stream of frames, eventstream_flat_kernel's
+    shape), with correct stored CRCs unless corrupted; returns blob, offsets, expected (pre, msg, st)"""
+    import zlib
+
+    rng = random.Random(seed)
+    blob = bytearray(rng.randbytes(lead))
+    offs, want = [], []
+    for i, total in enumerate(lens):
+        offs.append(len(blob))
+        m = bytearray(struct.pack(">II", total, rng.randint(0, total - 16)) + bytes(4) + rng.randbytes(total - 12))
+        pre = zlib.crc32(bytes(m[:8]))
+        m[8:12] = struct.pack(">I", pre)
+        msg = zlib.crc32(bytes(m[:total - 4]))
+        m[total - 4:] = struct.pack(">I", msg)
+        st = 3
+        if corrupt and i % 5 == 1:  # stored prelude CRC wrong
+            m[9] ^= 0x10
+            msg = zlib.crc32(bytes(m[:total - 4]))
+            m[total - 4:] = struct.pack(">I", msg)
+            st = 2
+        elif corrupt and i % 5 == 2:  # body flipped after the message CRC was stored
+            m[rng.randrange(12, total - 4) if total > 16 else 12] ^= 0x04
+            msg = zlib.crc32(bytes(m[:total - 4]))
+            st = 1
+        elif corrupt and i % 5 == 3:  # stored message CRC wrong
+            m[total - 1] ^= 0x80
+            st = 1
+        blob += m
+        want.append((pre, msg, st))
+    blob += rng.randbytes(64)
+    return blob, offs, want
+
+
+def _run_frames(blob, offs, order=None):
+    import numpy as np
+    import torch
+
+    from aws_crt_amd.eventstream import check_frames
+
+    d = torch.from_numpy(np.frombuffer(bytes(blob), dtype=np.uint8).copy()).cuda()
+    o_t = torch.tensor(offs if order is None else [offs[i] for i in order], dtype=torch.int64, device="cuda")
+    pre, msg, st = check_frames(d, o_t)
+    torch.cuda.synchronize()
+    u = lambda t: [int(x) & 0xFFFFFFFF for x in t.cpu().tolist()]  # noqa: E731
+    return list(zip(u(pre), u(msg), u(st)))
+
+
+@pytest.mark.gpu
+def test_check_frames_packed(engine):
+    """packed streams (the balanced flat kernel): every start alignment of the first message, random
+    16..1024-byte mixes with a partial last wave, the shortest messages (several ends per 64-byte block),
+    messages spanning many chunks, corrupted CRCs, all against zlib"""
+    rng = random.Random(0xF1A)
+    for lead in (0, 1, 7, 8, 13, 31, 47, 63):
+        lens = [rng.randint(16, 1024) for _ in range(64 * 6 + 5)]
+        blob, offs, want = _packed(lens, lead, lead, corrupt=lead % 2 == 1)
+        assert _run_frames(blob, offs) == want, lead
+    for lens in ([16] * 640, [rng.randint(16, 40) for _ in range(640)], [16 + i % 9 for i in range(640)],
+                 [rng.choice([16, 17, 4000, 20000, 70000]) for _ in range(200)]):
+        blob, offs, want = _packed(lens, len(lens), 5, corrupt=True)
+        assert _run_frames(blob, offs) == want
+
+
+@pytest.mark.gpu
+def test_check_frames_packed_fallbacks(engine):
+    """waves the flat kernel must leave to the lane path: a malformed frame inside a packed wave, offsets
+    out of order, a region beyond the flat kernel's bound; every other wave unaffected"""
+    rng = random.Random(0xF1B)
+    lens = [rng.randint(16, 1024) for _ in range(64 * 5)]
+    blob, offs, want = _packed(lens, 11, 3)
+    # headers_length > total - 16 in wave 1 (the frame stays packed): malformed
+    o = offs[70]
+    blob[o + 4:o + 8] = struct.pack(">I", lens[70] - 15)
+    want[70] = (0, 0, 4)
+    # wave 3's offsets swapped: not back to back
+    order = list(range(len(offs)))
+    order[200], order[201] = 201, 200
+    got = _run_frames(blob, offs, order)
+    assert got == [want[i] for i in order]
+    # one wave spanning more than 256 KiB (a 300 KB message): lane path
+    lens = [rng.randint(16, 1024) for _ in range(64 * 3)]
+    lens[100] = 300000
+    blob, offs, want = _packed(lens, 12, 9)
+    assert _run_frames(blob, offs) == want
