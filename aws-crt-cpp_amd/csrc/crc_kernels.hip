@@ -4117,45 +4117,52 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     EsWave &W = ((EsWave *)(lds + kLaneW8Lds + kEsLdsImgs * 512))[threadIdx.x >> 6];
 
     const uint64_t m = (uint64_t)blockIdx.x * kEsBlock + threadIdx.x;
-    const bool in = m < p.count;
-    const uint64_t off = in ? p.d_offsets[m] : 0;
-    uint32_t total = 0, headers = 0, pre_stored = 0;
-    uint64_t w8 = 0;  // the prelude's 8 bytes
-    bool ok = false;
+    const bool in = m < p.count, has_next = m + 1 < p.count;
+    const uint64_t off = in ? p.d_offsets[m] : 0, off_next = has_next ? p.d_offsets[m + 1] : 0;
     const uint8_t *q = p.base + off;
-    // four bytes at any address from the aligned dwords holding them (never a dword past the last byte)
-    auto u32_at = [](const uint8_t *a) {
-        const uintptr_t x = (uintptr_t)a, o = x & 3u;
-        const uint32_t lo = *(gu32 *)(x & ~(uintptr_t)3), hi = *(gu32 *)((x & ~(uintptr_t)3) + (o ? 4 : 0));
-        return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)o);
-    };
-    if (in && off <= p.limit && p.limit - off >= 16) {
-        const uint32_t b0 = u32_at(q), b1 = u32_at(q + 4), b2 = u32_at(q + 8);
-        total = __builtin_bswap32(b0);
-        headers = __builtin_bswap32(b1);
-        pre_stored = __builtin_bswap32(b2);
-        w8 = (uint64_t)b0 | (uint64_t)b1 << 32;
-        ok = total >= 16 && total <= p.limit - off && headers <= total - 16;
+    // the prelude's first 12 bytes from the four aligned dwords holding them (issued now, used after
+    // the scan on the flat path)
+    const bool readable = in && off <= p.limit && p.limit - off >= 16;
+    uint32_t pd[4] = {0, 0, 0, 0};
+    if (readable) {
+        const uintptr_t qa = (uintptr_t)q & ~(uintptr_t)3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pd[j] = *(gu32 *)(qa + 4 * j);
     }
-    if (!ok) total = 0;
-    // the flat path: every lane's message well formed, packed back to back, the region bounded
-    const uint64_t off_next = __shfl_down(off, 1), off0 = __shfl(off, 0);
-    const uint64_t end63 = __shfl(off + total, 63);
-    const bool flat = __all(ok && (lane == 63 || off + total == off_next) && end63 - off0 <= kEsMaxRegion);
-    const uint32_t s8 = ok ? f.word(~0u, w8) : 0u;  // the register after the prelude
-    const uint32_t pre = ok ? ~s8 : 0u;
-    uint32_t st = ok ? (pre_stored == pre ? 1u : 0u) : 4u, msg = 0;
-    if (!flat) {
+    const uint32_t qo = (uint32_t)((uintptr_t)q & 3u);
+    // the lane path: lengths from the preludes, one lane per message (eventstream_kernel's walk)
+    auto lane_path = [&]() {
         if (!in) return;
-        if (ok) {
-            msg = ~lane_scan<uint32_t>(s8, q + 8, total - 12, f);
-            st |= __builtin_bswap32(u32_at(q + total - 4)) == msg ? 2u : 0u;
+        uint32_t pre = 0, msg = 0, st = 4u;
+        if (readable) {
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
+            const uint32_t b2 = __builtin_amdgcn_alignbyte(pd[3], pd[2], qo);
+            const uint32_t total = __builtin_bswap32(b0), headers = __builtin_bswap32(b1);
+            if (total >= 16 && total <= p.limit - off && headers <= total - 16) {
+                const uint32_t s8 = f.word(~0u, (uint64_t)b0 | (uint64_t)b1 << 32);
+                pre = ~s8;
+                msg = ~lane_scan<uint32_t>(s8, q + 8, total - 12, f);
+                const uintptr_t x = (uintptr_t)(q + total - 4), xa = x & ~(uintptr_t)3;
+                const uint32_t stored = __builtin_bswap32(__builtin_amdgcn_alignbyte(*(gu32 *)(xa + ((x & 3u) ? 4 : 0)), *(gu32 *)xa, (uint32_t)(x & 3u)));
+                st = (__builtin_bswap32(b2) == pre ? 1u : 0u) | (stored == msg ? 2u : 0u);
+            }
         }
         p.d_prelude_crc[m] = pre;
         p.d_message_crc[m] = msg;
         p.d_status[m] = st;
+    };
+    // The flat path is taken on the offsets alone (the preludes are still in flight): every message
+    // of the wave followed by the next one's offset, at least 16 bytes apart, the region bounded and
+    // readable.  Message i's length is then off_(i+1) - off_i; after the scan the preludes must agree
+    // (total_length equal to it, headers within it), or the wave is redone on the lane path.
+    const uint64_t off0 = __shfl(off, 0), end63 = __shfl(off_next, 63);
+    const bool flat = __all(in && has_next && off_next >= off + 16 && off_next - off <= 0xffffffffull && end63 <= p.limit &&
+                            end63 - off0 <= kEsMaxRegion);
+    if (!flat) {
+        lane_path();
         return;
     }
+    const uint32_t total = (uint32_t)(off_next - off);
     // wave-uniform values in SGPRs (the shuffles' results are VGPRs to the compiler)
     const uintptr_t rs = rfl64((uintptr_t)(p.base + off0) & ~(uintptr_t)15);  // 16-aligned: message 0 starts < 16 in
     const uint32_t s_i = (uint32_t)((uintptr_t)q - rs), e_i = s_i + total - 4;
@@ -4302,6 +4309,13 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
         for (int j = 0; j < 4; ++j) pw[j] = W.P[i0 + j];  // the next block's window
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = nv[j];
+        if (b == 0) {  // the preludes (loaded before the first block) must agree with the offsets
+            const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
+            if (!__all(__builtin_bswap32(b0) == total && __builtin_bswap32(b1) <= total - 16)) {
+                lane_path();
+                return;
+            }
+        }
     }
     W.endst[lane] = u;
     __builtin_amdgcn_wave_barrier();
@@ -4309,12 +4323,16 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     // message `lane`: its record, plus the pieces of the chunks it began in (chunks lane(B) ..
     // lane(P_i) - 1, B = the previous end word or message 0's first word), moved to its end word;
     // then the end word's overshoot past e_i taken off
+    const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
+    const uint32_t b2 = __builtin_amdgcn_alignbyte(pd[3], pd[2], qo);
+    const uint32_t pre = ~f.word(~0u, (uint64_t)b0 | (uint64_t)b1 << 32);
+    uint32_t st = __builtin_bswap32(b2) == pre ? 1u : 0u;
     uint32_t z = (uint32_t)W.rec[lane];
     const uint32_t B = lane ? (W.P[lane - 1] & kPMask) : 0u;
     gu32 *gimg = (gu32 *)p.d_imgs;
     for (uint32_t k = B / C, kp = P_i / C; k < kp; ++k) z ^= es_shift_words(W.endst[k], (P_i + 8 - (k + 1) * C) >> 3, limg, gimg);
     if (a_i < 8) z = es_mul(z, limg + 128 * (30 + (7 - a_i)));  // x^(-8 (8 - a_i))
-    msg = ~z;
+    const uint32_t msg = ~z;
     st |= __builtin_bswap32(raw) == msg ? 2u : 0u;
     p.d_prelude_crc[m] = pre;
     p.d_message_crc[m] = msg;

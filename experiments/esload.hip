@@ -253,6 +253,59 @@ __global__ __launch_bounds__(TPB) void k_balq(Args a) {
     if (x == 0x9E3779B9u) a.sink[m] = x;
 }
 
+// two chunks per lane (128 chunks per wave: lane l folds chunks l and l + 64 as two independent
+// chains, interleaved): the same quad loads, eight per block step, through 128 LDS rows
+template <int TPB>
+__global__ __launch_bounds__(TPB) void k_bal2c(Args a) {
+    constexpr uint32_t kRow = 80, kWave = 128 * kRow;
+    __shared__ __attribute__((aligned(16))) char lds[65536 + (TPB / 64) * kWave];
+    char *tr = lds + 65536 + (threadIdx.x >> 6) * kWave;
+    Fold f;
+    load_tables(lds, a.img);
+    const uint32_t lane = threadIdx.x & 63u;
+    f.init(lds, lane);
+    const uint32_t m = blockIdx.x * TPB + threadIdx.x;
+    const uint64_t off = a.offs[m];
+    const uint32_t len = a.lens[m];
+    const uint64_t o0 = __shfl(off, 0), o63 = __shfl(off, 63);
+    const uint32_t l63 = __shfl(len, 63);
+    const uintptr_t rs = (uintptr_t)(a.base + o0) & ~(uintptr_t)63;
+    const uintptr_t re = ((uintptr_t)(a.base + o63 + l63) + 63) & ~(uintptr_t)63;
+    const uint32_t units = (uint32_t)((re - rs) >> 6), nb = (units + 127) >> 7, C = nb << 6;
+    const uintptr_t rsub = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
+    auto addr = [&](uint32_t j, uint32_t b) {
+        const uintptr_t p = rsub + (uintptr_t)(16 * j) * C + ((uintptr_t)b << 6);
+        return p < re ? p : re - 64 + 16u * (lane & 3u);
+    };
+    u32x4 v[8], nv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ld16(addr(j, 0));
+    uint32_t ua = 0, ub = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nv[j] = ld16(addr(j, b + 1));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *(u32x4 *)(tr + (16 * j + (lane >> 2)) * kRow + 16 * (lane & 3)) = v[j];
+        u32x4 wa[4], wb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            wa[q] = *(const u32x4 *)(tr + lane * kRow + 16 * q);
+            wb[q] = *(const u32x4 *)(tr + (lane + 64) * kRow + 16 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ua = f.word(ua, wa[q].x, wa[q].y);
+            ub = f.word(ub, wb[q].x, wb[q].y);
+            ua = f.word(ua, wa[q].z, wa[q].w);
+            ub = f.word(ub, wb[q].z, wb[q].w);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = nv[j];
+    }
+    const uint32_t x = ua ^ ub;
+    if (x == 0x9E3779B9u) a.sink[m] = x;
+}
+
 // the wave's region as 1 KiB rows, D rows in flight
 template <int D>
 __global__ __launch_bounds__(256) void k_coal(Args a) {
@@ -337,6 +390,7 @@ int main(int argc, char **argv) {
         {"balq", k_balq<false, 256, 1>, 256},   {"balq+fold/512", k_balq<true, 512, 1>, 512},
         {"balq2+fold/512", k_balq<true, 512, 2>, 512}, {"balq/512", k_balq<false, 512, 1>, 512},
         {"balfold-only/512", k_balq<true, 512, 1, true>, 512}, {"coal4", k_coal<4>, 256},
+        {"bal2c+fold/512", k_bal2c<512>, 512},
     };
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
