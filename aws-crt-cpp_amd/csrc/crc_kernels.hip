@@ -4212,10 +4212,17 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
 
     const uintptr_t rea = rs + re;
     const uintptr_t qbase = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
-    auto qaddr = [&](uint32_t j, uint32_t b) {  // always a readable address (past the region: its last block)
-        const uintptr_t a = qbase + (uintptr_t)(16u * j) * C + ((uintptr_t)b << 6);
-        return a < rea ? a : rea - 64 + 16u * (lane & 3u);
-    };
+    // quad load j of a block step reads chunk 16 j + lane / 4; past the region's last 16 bytes it
+    // re-reads the chunk's last readable block (folded as garbage after the last message: harmless)
+    uintptr_t qb[4];
+    uint32_t qlast[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uintptr_t b0 = qbase + (uintptr_t)(16u * j) * C;
+        qb[j] = b0 + 16 <= rea ? b0 : rs + 16u * (lane & 3u);
+        qlast[j] = b0 + 16 <= rea ? (uint32_t)((rea - 16 - b0) >> 6) : 0u;
+    }
+    auto qaddr = [&](uint32_t j, uint32_t b) { return qb[j] + ((uintptr_t)min(b, qlast[j]) << 6); };
     v4u v[4], nv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = *(gv4u *)qaddr(j, 0);
