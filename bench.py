@@ -1212,14 +1212,16 @@ def main_rank(args):
             configs["C3_crc32c"] = config_leg(eng, "C3", "crc32c", 16, 256 << 20, streams, dev, **legs)
             configs["C3_crc32"] = config_leg(eng, "C3", "crc32", 16, 256 << 20, streams, dev, **legs)
             configs["C5_crc64nvme"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev, **legs)
-            # the same C5 steps through the multi-batch launch (12 queued batches = 6 GiB per launch, as the
-            # headline coalesces C2): the batched API's rate for S3's default algorithm
-            configs["C5_crc64nvme_multi_batch"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev,
-                                                             coalesce=12, timing=2, do_cpu=False, do_e2e=False)
             configs["C5_xxh64"] = config_leg(eng, "C5", "xxh64", 8, 64 << 20, streams, dev, steps=4, timing=2, **legs)
             configs["target_16x64MiB_crc32c"] = config_leg(eng, "north-star target", "crc32c", 16, 64 << 20, streams, dev,
                                                            steps=20, **legs)
             configs["target_16x64MiB_crc32c"]["target_pct"] = 80.0
+            # the same C5 steps through the multi-batch launch (12 queued batches = 6 GiB per launch, as the
+            # headline coalesces C2): the batched API's rate for S3's default algorithm.  Last: the XXH64
+            # host route measured right after these launches runs at ~17 GiB/s instead of 41-50 for the
+            # next ~0.3 s (tools/x64_leg_order.py, profiles/r06/x64order), so no leg follows them.
+            configs["C5_crc64nvme_multi_batch"] = config_leg(eng, "C5", "crc64nvme", 8, 64 << 20, streams, dev,
+                                                             coalesce=12, timing=2, do_cpu=False, do_e2e=False)
 
     if rank == 0:
         rec = {
