@@ -4153,7 +4153,7 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     };
     // The flat path is taken on the offsets alone (the preludes are still in flight): every message
     // of the wave followed by the next one's offset, at least 16 bytes apart, the region bounded and
-    // readable.  Message i's length is then off_(i+1) - off_i; after the scan the preludes must agree
+    // readable.  Message i's length is then off_(i+1) - off_i; once the first block's loads are issued the preludes must agree
     // (total_length equal to it, headers within it), or the wave is redone on the lane path.
     const uint64_t off0 = __shfl(off, 0), end63 = __shfl(off_next, 63);
     const bool flat = __all(in && has_next && off_next >= off + 16 && off_next - off <= 0xffffffffull && end63 <= p.limit &&
@@ -4226,6 +4226,13 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     v4u v[4], nv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = *(gv4u *)qaddr(j, 0);
+    {  // the preludes (issued before these loads, so they land first) must agree with the offsets
+        const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
+        if (!__all(__builtin_bswap32(b0) == total && __builtin_bswap32(b1) <= total - 16)) {
+            lane_path();
+            return;
+        }
+    }
     char *wrow = W.rows + (lane >> 2) * kEsRow + 16 * (lane & 3);
     const char *rrow = W.rows + lane * kEsRow;
     uint32_t *rows32 = (uint32_t *)W.rows;
@@ -4316,13 +4323,6 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
         for (int j = 0; j < 4; ++j) pw[j] = W.P[i0 + j];  // the next block's window
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = nv[j];
-        if (b == 0) {  // the preludes (loaded before the first block) must agree with the offsets
-            const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
-            if (!__all(__builtin_bswap32(b0) == total && __builtin_bswap32(b1) <= total - 16)) {
-                lane_path();
-                return;
-            }
-        }
     }
     W.endst[lane] = u;
     __builtin_amdgcn_wave_barrier();

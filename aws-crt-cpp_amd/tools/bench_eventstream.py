@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--timing-launches", type=int, default=8)
     ap.add_argument("--timing-only", action="store_true",
                     help="skip the zlib check (A/B builds whose results are wrong by design: experiments/patches)")
+    ap.add_argument("--gap-max", type=int, default=0,
+                    help="random gaps of 0..N bytes between messages (frames not packed back to back)")
     ap.add_argument("--device-frames", action="store_true",
                     help="aws_crt_amd_eventstream_crcs: device offsets, lengths read from the preludes, CRCs checked")
     a = ap.parse_args()
@@ -41,7 +43,7 @@ def main():
     offs, pos = [], 0
     for n in lens:
         offs.append(pos)
-        pos += n
+        pos += n + (rng.randint(0, a.gap_max) if a.gap_max else 0)
     data = torch.randint(0, 256, (a.batches * pos,), dtype=torch.uint8, device="cuda")
     fbs = [FrameBatch(data.data_ptr() + b * pos, offs, lens) for b in range(a.batches)]
     for fb in fbs:
@@ -73,7 +75,7 @@ def main():
             def __init__(self, b):
                 self.b = b
                 self.n = 2 * a.messages
-                self.payload_bytes = sum(lens) - 4 * a.messages  # bytes read once: [0, total - 4)
+                self.payload_bytes = sum(lens) - 4 * a.messages  # bytes CRC'd: [0, total - 4) of each message
 
             def run(self, out, stream):
                 r = res[self.b]
