@@ -253,6 +253,51 @@ __global__ __launch_bounds__(TPB) void k_balq(Args a) {
     if (x == 0x9E3779B9u) a.sink[m] = x;
 }
 
+// MPW messages per wave (32: twice the waves, 16 per CU in one 1024-thread workgroup beside the
+// tables), the wave's region in 64 equal chunks, quad loads through LDS rows, the fold
+template <int TPB, int MPW>
+__global__ __launch_bounds__(TPB) void k_balq_mpw(Args a) {
+    constexpr uint32_t kRow = 80, kWave = 64 * kRow;
+    __shared__ __attribute__((aligned(16))) char lds[65536 + (TPB / 64) * kWave];
+    char *tr = lds + 65536 + (threadIdx.x >> 6) * kWave;
+    Fold f;
+    load_tables(lds, a.img);
+    const uint32_t lane = threadIdx.x & 63u;
+    f.init(lds, lane);
+    const uint32_t wave = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+    const uint32_t m = wave * MPW + (lane < MPW ? lane : MPW - 1);
+    const uint64_t off = a.offs[m];
+    const uint32_t len = a.lens[m];
+    const uint64_t o0 = __shfl(off, 0), ol = __shfl(off, MPW - 1);
+    const uint32_t ll = __shfl(len, MPW - 1);
+    const uintptr_t rs = (uintptr_t)(a.base + o0) & ~(uintptr_t)63;
+    const uintptr_t re = ((uintptr_t)(a.base + ol + ll) + 63) & ~(uintptr_t)63;
+    const uint32_t units = (uint32_t)((re - rs) >> 6), nb = (units + 63) >> 6, C = nb << 6;
+    const uintptr_t rsub = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
+    auto addr = [&](uint32_t j, uint32_t b) {
+        const uintptr_t p = rsub + (uintptr_t)(16 * j) * C + ((uintptr_t)b << 6);
+        return p < re ? p : re - 64 + 16u * (lane & 3u);
+    };
+    u32x4 v[4], nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ld16(addr(j, 0));
+    uint32_t u = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nv[j] = ld16(addr(j, b + 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(u32x4 *)(tr + (16 * j + (lane >> 2)) * kRow + 16 * (lane & 3)) = v[j];
+        u32x4 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = *(const u32x4 *)(tr + lane * kRow + 16 * q);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u = f.vec(u, w[q]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = nv[j];
+    }
+    if (u == 0x9E3779B9u) a.sink[m] = u;
+}
+
 // two chunks per lane (128 chunks per wave: lane l folds chunks l and l + 64 as two independent
 // chains, interleaved): the same quad loads, eight per block step, through 128 LDS rows
 template <int TPB>
@@ -383,6 +428,7 @@ int main(int argc, char **argv) {
         const char *name;
         void (*k)(Args);
         int tpb;
+        int mpb = 0;  // messages per workgroup (default: one per thread)
     };
     const std::vector<V> vs = {
         {"lane", k_lane<false>, 256},    {"lane+fold", k_lane<true>, 256},  {"bal1", k_bal<false, 1>, 256},
@@ -391,6 +437,7 @@ int main(int argc, char **argv) {
         {"balq2+fold/512", k_balq<true, 512, 2>, 512}, {"balq/512", k_balq<false, 512, 1>, 512},
         {"balfold-only/512", k_balq<true, 512, 1, true>, 512}, {"coal4", k_coal<4>, 256},
         {"bal2c+fold/512", k_bal2c<512>, 512},
+        {"balq+fold/512 mpw64", k_balq_mpw<512, 64>, 512}, {"balq+fold/1024 mpw32", k_balq_mpw<1024, 32>, 1024, 512},
     };
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -405,10 +452,10 @@ int main(int argc, char **argv) {
         for (size_t vi = 0; vi < vs.size(); ++vi) {
             const V &v = vs[vi];
             for (int i = 0; i < 4; ++i)
-                hipLaunchKernelGGL(v.k, dim3(n / v.tpb), dim3(v.tpb), 0, s, Args{buf + (i % copies) * span, d_offs, d_lens, n, sink, img});
+                hipLaunchKernelGGL(v.k, dim3(n / (v.mpb ? v.mpb : v.tpb)), dim3(v.tpb), 0, s, Args{buf + (i % copies) * span, d_offs, d_lens, n, sink, img});
             CK(hipStreamSynchronize(s));
             for (int i = 0; i < iso; ++i)
-                hipExtLaunchKernelGGL(v.k, dim3(n / v.tpb), dim3(v.tpb), 0, s, e0[i], e1[i], 0,
+                hipExtLaunchKernelGGL(v.k, dim3(n / (v.mpb ? v.mpb : v.tpb)), dim3(v.tpb), 0, s, e0[i], e1[i], 0,
                                       Args{buf + (i % copies) * span, d_offs, d_lens, n, sink, img});
             CK(hipStreamSynchronize(s));
             double sum = 0, mn = 1e9;
