@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--timing-launches", type=int, default=8)
     ap.add_argument("--timing-only", action="store_true",
                     help="skip the zlib check (A/B builds whose results are wrong by design: experiments/patches)")
+    ap.add_argument("--no-hold", action="store_true",
+                    help="time the launches without the GPU-side hold in front of them (the probe's way)")
     ap.add_argument("--gap-max", type=int, default=0,
                     help="random gaps of 0..N bytes between messages (frames not packed back to back)")
     ap.add_argument("--device-frames", action="store_true",
@@ -99,8 +101,9 @@ def main():
     nt = a.timing_launches
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(nt)]
-    with torch.cuda.stream(st):
-        torch.cuda._sleep(int(40e6))
+    if not a.no_hold:  # queue the timed launches behind a GPU-side hold so they run back to back
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(int(40e6))
     for i in range(nt):
         starts[i].record(st)
         ends[i].record(st)
