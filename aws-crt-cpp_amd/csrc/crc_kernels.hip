@@ -4123,16 +4123,29 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     // the prelude's first 12 bytes from the four aligned dwords holding them (issued now, used after
     // the scan on the flat path)
     const bool readable = in && off <= p.limit && p.limit - off >= 16;
-    uint32_t pd[4] = {0, 0, 0, 0};
-    if (readable) {
-        const uintptr_t qa = (uintptr_t)q & ~(uintptr_t)3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pd[j] = *(gu32 *)(qa + 4 * j);
-    }
+    // and the 4 bytes in front of it (a packed stream's previous stored CRC): 20 bytes from the aligned
+    // dword at q - 4 in one 16-byte and one 4-byte load (round 6: six dword loads here, each one 64
+    // scattered lines per wave, cost ~2 us of the 26 us call)
+    typedef v4u v4u_a4 __attribute__((aligned(4)));
+    uint32_t pd[4] = {0, 0, 0, 0}, prevraw = 0;
     const uint32_t qo = (uint32_t)((uintptr_t)q & 3u);
+    const bool back = off >= 4;
+    uint32_t px[5] = {0, 0, 0, 0, 0};
+    if (readable) {
+        const uintptr_t ea = ((uintptr_t)q - (back ? 4 : 0)) & ~(uintptr_t)3;
+        const v4u x = *(const __attribute__((address_space(1))) v4u_a4 *)ea;
+        px[0] = x.x, px[1] = x.y, px[2] = x.z, px[3] = x.w;
+        px[4] = *(gu32 *)(ea + (back ? 16 : 12));  // (without the 4 bytes in front: never past the 16 bytes)
+    }
+    auto prelude_words = [&]() {  // the prelude's dwords (pd) and the 4 bytes in front of the message
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pd[j] = back ? px[j + 1] : px[j];
+        prevraw = back ? __builtin_amdgcn_alignbyte(px[1], px[0], qo) : 0u;
+    };
     // the lane path: lengths from the preludes, one lane per message (eventstream_kernel's walk)
     auto lane_path = [&]() {
         if (!in) return;
+        prelude_words();
         uint32_t pre = 0, msg = 0, st = 4u;
         if (readable) {
             const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
@@ -4187,10 +4200,40 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
 #pragma unroll
     for (int j = 0; j < 4; ++j) pw[j] = W.P[i0 + j];
 
-    // the stored message CRC's two dwords, loaded now and used after the scan
+    // the stored message CRC: in front of the next message (its lane loaded those 4 bytes); lane 63's
+    // own load
     const uintptr_t crc_a = (uintptr_t)(q + total - 4);
-    const uint32_t crc_lo = *(gu32 *)(crc_a & ~(uintptr_t)3), crc_hi = *(gu32 *)((crc_a & ~(uintptr_t)3) + ((crc_a & 3u) ? 4 : 0));
-    const uint32_t raw = __builtin_amdgcn_alignbyte(crc_hi, crc_lo, (uint32_t)(crc_a & 3u));  // its bytes in memory order
+    uint32_t crc_lo = 0, crc_hi = 0;
+    if (lane == 63) {
+        crc_lo = *(gu32 *)(crc_a & ~(uintptr_t)3);
+        crc_hi = *(gu32 *)((crc_a & ~(uintptr_t)3) + ((crc_a & 3u) ? 4 : 0));
+    }
+    const uintptr_t rea = rs + re;
+    const uintptr_t qbase = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
+    // quad load j of a block step reads chunk 16 j + lane / 4; past the region's last 16 bytes it
+    // re-reads the chunk's last readable block (folded as garbage after the last message: harmless)
+    uintptr_t qb[4];
+    uint32_t qlast[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uintptr_t b0 = qbase + (uintptr_t)(16u * j) * C;
+        qb[j] = b0 + 16 <= rea ? b0 : rs + 16u * (lane & 3u);
+        qlast[j] = b0 + 16 <= rea ? (uint32_t)((rea - 16 - b0) >> 6) : 0u;
+    }
+    auto qaddr = [&](uint32_t j, uint32_t b) { return qb[j] + ((uintptr_t)min(b, qlast[j]) << 6); };
+    v4u v[4], nv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *(gv4u *)qaddr(j, 0);
+    prelude_words();
+    {  // the preludes (issued before these loads, so they land first) must agree with the offsets
+        const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
+        if (!__all(__builtin_bswap32(b0) == total && __builtin_bswap32(b1) <= total - 16)) {
+            lane_path();
+            return;
+        }
+    }
+    const uint32_t nraw = __shfl_down(prevraw, 1);
+    const uint32_t raw = lane == 63 ? __builtin_amdgcn_alignbyte(crc_hi, crc_lo, (uint32_t)(crc_a & 3u)) : nraw;  // in memory order
 
     // This message's end patch: the stored CRC's four bytes at [e_i, e_i + 4) XORed with themselves
     // (cleared) and the next message's first four bytes XORed with 0xFF (CRC32's ~0 start), so that
@@ -4210,29 +4253,7 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
         }
     }
 
-    const uintptr_t rea = rs + re;
-    const uintptr_t qbase = rs + (uintptr_t)(lane >> 2) * C + 16u * (lane & 3u);
-    // quad load j of a block step reads chunk 16 j + lane / 4; past the region's last 16 bytes it
-    // re-reads the chunk's last readable block (folded as garbage after the last message: harmless)
-    uintptr_t qb[4];
-    uint32_t qlast[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uintptr_t b0 = qbase + (uintptr_t)(16u * j) * C;
-        qb[j] = b0 + 16 <= rea ? b0 : rs + 16u * (lane & 3u);
-        qlast[j] = b0 + 16 <= rea ? (uint32_t)((rea - 16 - b0) >> 6) : 0u;
-    }
-    auto qaddr = [&](uint32_t j, uint32_t b) { return qb[j] + ((uintptr_t)min(b, qlast[j]) << 6); };
-    v4u v[4], nv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = *(gv4u *)qaddr(j, 0);
-    {  // the preludes (issued before these loads, so they land first) must agree with the offsets
-        const uint32_t b0 = __builtin_amdgcn_alignbyte(pd[1], pd[0], qo), b1 = __builtin_amdgcn_alignbyte(pd[2], pd[1], qo);
-        if (!__all(__builtin_bswap32(b0) == total && __builtin_bswap32(b1) <= total - 16)) {
-            lane_path();
-            return;
-        }
-    }
+
     char *wrow = W.rows + (lane >> 2) * kEsRow + 16 * (lane & 3);
     const char *rrow = W.rows + lane * kEsRow;
     uint32_t *rows32 = (uint32_t *)W.rows;
