@@ -3829,6 +3829,24 @@ struct LaneW8Basis {
             for (int i = 0; i < 8; ++i) b[t][i] = (uint32_t)gf2_table_entry(1u << i, t, POLY);
     }
 };
+// the bases of T_tl and T_(tl + 4) for a per-lane tl < 4, in registers: the selects are made over
+// register copies of the constants (the compiler had turned B.b[tl][b] into indexed loads from a
+// constant array in global memory -- a dependent memory round trip before every table build)
+template <uint32_t POLY>
+__device__ __forceinline__ void lane_w8_basis(uint32_t tl, uint32_t (&bl)[8], uint32_t (&bh)[8]) {
+    constexpr LaneW8Basis<POLY> B{};
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        uint32_t c[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            c[t] = B.b[t][b];
+            asm volatile("" : "+v"(c[t]));  // opaque: a register, not a table entry
+        }
+        bl[b] = tl == 0 ? c[0] : tl == 1 ? c[1] : tl == 2 ? c[2] : c[3];
+        bh[b] = tl == 0 ? c[4] : tl == 1 ? c[5] : tl == 2 ? c[6] : c[7];
+    }
+}
 // the 64 KiB table image from a 256-thread workgroup, 16 ds_write_b128 per thread.  Store k of thread
 // i writes entry e = (i >> 3) + 32 (k >> 1), table t = ((i & 7) >> 1) + 4 (k & 1), copies 4 (i & 1)..+3,
 // so the eight lanes of each ds_write_b128 lane group cover the 128 bytes of all 32 banks once (16
@@ -3836,14 +3854,9 @@ struct LaneW8Basis {
 // every group 8-way conflicted -- 8,000 conflict cycles per CU before the first message.
 template <uint32_t POLY>
 __device__ __forceinline__ void lane_w8_tables(char *lds) {
-    constexpr LaneW8Basis<POLY> B{};
     const uint32_t i = threadIdx.x, tl = (i & 7u) >> 1, half = i & 1u;
     uint32_t bl[8], bh[8];  // the bases of T_tl and T_(tl + 4)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        bl[b] = tl == 0 ? B.b[0][b] : tl == 1 ? B.b[1][b] : tl == 2 ? B.b[2][b] : B.b[3][b];
-        bh[b] = tl == 0 ? B.b[4][b] : tl == 1 ? B.b[5][b] : tl == 2 ? B.b[6][b] : B.b[7][b];
-    }
+    lane_w8_basis<POLY>(tl, bl, bh);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const uint32_t e = (i >> 3) + 32u * (uint32_t)(k >> 1), t = tl + 4u * (uint32_t)(k & 1);
@@ -4088,15 +4101,14 @@ __device__ __forceinline__ uint32_t es_word(const LaneW8 &f, uint32_t s, uint64_
 
 __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventStreamParams p) {
     __shared__ __attribute__((aligned(16))) char lds[kEsLds];
+    // the offsets first: their round trip overlaps the table build below
+    const uint64_t m = (uint64_t)blockIdx.x * kEsBlock + threadIdx.x;
+    const bool in = m < p.count, has_next = m + 1 < p.count;
+    const uint64_t off = in ? p.d_offsets[m] : 0, off_next = has_next ? p.d_offsets[m + 1] : 0;
     {  // tables (the 256-thread build's stores, split over the two halves) and images
-        constexpr LaneW8Basis<kPoly32> B{};
         const uint32_t i = threadIdx.x & 255u, tl = (i & 7u) >> 1, half = i & 1u, k0 = 8u * (threadIdx.x >> 8);
         uint32_t bl[8], bh[8];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            bl[b] = tl == 0 ? B.b[0][b] : tl == 1 ? B.b[1][b] : tl == 2 ? B.b[2][b] : B.b[3][b];
-            bh[b] = tl == 0 ? B.b[4][b] : tl == 1 ? B.b[5][b] : tl == 2 ? B.b[6][b] : B.b[7][b];
-        }
+        lane_w8_basis<kPoly32>(tl, bl, bh);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
             const uint32_t k = k0 + kk, e = (i >> 3) + 32u * (k >> 1), t = tl + 4u * (k & 1);
@@ -4116,9 +4128,6 @@ __global__ __launch_bounds__(kEsBlock) void eventstream_flat_kernel(const EventS
     const uint32_t *limg = (const uint32_t *)(lds + kLaneW8Lds);
     EsWave &W = ((EsWave *)(lds + kLaneW8Lds + kEsLdsImgs * 512))[threadIdx.x >> 6];
 
-    const uint64_t m = (uint64_t)blockIdx.x * kEsBlock + threadIdx.x;
-    const bool in = m < p.count, has_next = m + 1 < p.count;
-    const uint64_t off = in ? p.d_offsets[m] : 0, off_next = has_next ? p.d_offsets[m + 1] : 0;
     const uint8_t *q = p.base + off;
     // the prelude's first 12 bytes from the four aligned dwords holding them (issued now, used after
     // the scan on the flat path)
